@@ -1,0 +1,201 @@
+/*
+ * vr.h — C ABI of the MI355X-native volume ray-marcher.
+ *
+ * This is the drop-in boundary for the reference renderer's raycast pass,
+ * `Vol::Rendering::OffscreenPass` (reference: src/rendering/offscreen_pass.h:27-148)
+ * together with the fragment shader it drives (res/shaders/volume.frag:21-52) and the
+ * Vulkan fixed-function state around it (sampler, cull, depth, blend, UNORM store).
+ *
+ * Every entry point is `extern "C"`, takes plain pointers and sizes, never throws, and
+ * returns 0 on success or a negative errno-style code (VR_E*) on failure; the message of
+ * the last failure is available from vr_last_error().  A context is bound to ONE HIP
+ * device and is not thread-safe (one host thread per context, as the reference's single
+ * render thread).  Multi-GPU runs use one process (and one context) per GPU; see
+ * vr_render_device() row-block sharding and vr_assemble_rows().
+ *
+ * Mapping to the reference (each function lists the interface it replaces):
+ *   vr_create                 OffscreenPass::OffscreenPass(VulkanContext*, w, h)   offscreen_pass.cpp:112-134
+ *   vr_destroy                OffscreenPass::~OffscreenPass()                      offscreen_pass.cpp:136-161
+ *   vr_resize                 OffscreenPass::framebuffer_size_changed(w, h)        offscreen_pass.cpp:232-255
+ *   vr_set_volume             OffscreenPass::volume_dataset_changed(Dataset&)      offscreen_pass.cpp:257-269
+ *   vr_set_transfer_function  OffscreenPass::transfer_function_changed(vector<u32>) offscreen_pass.cpp:279-288
+ *   vr_set_slicing            OffscreenPass::slicing_changed(vec3 min, vec3 max)   offscreen_pass.cpp:271-277
+ *   vr_render / vr_render_device
+ *                             OffscreenPass::record(cmd, frame) + update_uniform_buffer
+ *                             offscreen_pass.cpp:163-230, 1152-1171; volume.vert:19-24;
+ *                             volume.frag:21-52
+ *   vr_last_error             (the reference throws std::runtime_error instead)
+ */
+#ifndef VR_VR_H
+#define VR_VR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VR_ABI_VERSION 1
+
+/* ---- status codes (negative errno style) ---- */
+#define VR_OK 0
+#define VR_EINVAL (-22)  /* bad argument */
+#define VR_ENOMEM (-12)  /* device or host allocation failed */
+#define VR_ENODEV (-19)  /* no such HIP device / HIP runtime failure */
+#define VR_ENODATA (-61) /* render called before a volume/TF is present (never: defaults exist) */
+#define VR_EIO (-5)      /* HIP runtime error during a launch or copy */
+
+/* ---- voxel element types accepted by vr_set_volume (NRRD element types the reference's
+ *      NrrdFileParser::convert accepts, nrrd_file_parser.cpp:49-66) ---- */
+enum vr_dtype {
+    VR_DTYPE_I8 = 1,  /* nrrdTypeChar   */
+    VR_DTYPE_U8 = 2,  /* nrrdTypeUChar  */
+    VR_DTYPE_I16 = 3, /* nrrdTypeShort  */
+    VR_DTYPE_U16 = 4, /* nrrdTypeUShort */
+    VR_DTYPE_I32 = 5, /* nrrdTypeInt    */
+    VR_DTYPE_U32 = 6, /* nrrdTypeUInt   */
+    VR_DTYPE_I64 = 7, /* nrrdTypeLLong  */
+    VR_DTYPE_U64 = 8, /* nrrdTypeULLong */
+    VR_DTYPE_F32 = 9, /* nrrdTypeFloat  */
+    VR_DTYPE_F64 = 10 /* nrrdTypeDouble */
+};
+
+/* ---- output pixel formats ---- */
+enum vr_out_format {
+    VR_OUT_RGBA8 = 0,  /* R8G8B8A8_UNORM, the reference colour attachment (offscreen_pass.cpp:293) */
+    VR_OUT_RGBA32F = 1 /* float RGBA after blend, before UNORM quantisation (parity format) */
+};
+
+/* Camera as the reference's Scene::Camera supplies it to the UBO
+ * (offscreen_pass.cpp:1155-1169; camera.cpp:36-48).
+ * view: column-major 4x4 (glm layout: element [col*4+row]).
+ * fovy_deg/znear/zfar: the projection constants of update_uniform_buffer
+ * (perspectiveRH(radians(40), W/H, 0.1, 10)); 0 selects those defaults. */
+typedef struct vr_camera {
+    float view[16];
+    float position[3];
+    float fovy_deg;
+    float znear;
+    float zfar;
+} vr_camera;
+
+/* Per-frame render parameters.  Defaults (vr_params_default) equal the reference
+ * constants: step 0.005, ray_dist 1.8 (volume.frag:29-30), clear (0.11,0.11,0.11,1)
+ * (offscreen_pass.cpp:170-173), no early-ray termination, no shading.
+ * Early-ray termination with ert_eps > 0 stops a ray once its transmittance T < ert_eps
+ * (bounded colour error <= ert_eps per channel).  T == 0 always terminates: bit-identical.
+ * shading = 1 enables the build's central-difference gradient Phong extension
+ * (the reference has none; see DESIGN.md "Shading extension"). */
+typedef struct vr_params {
+    float step;
+    float ray_dist;
+    float ert_eps;
+    int32_t shading;
+    float clear_color[4];
+    float ambient;
+    float diffuse;
+    float specular;
+    int32_t spec_power; /* integer exponent, evaluated by repeated multiplication */
+    int32_t reserved[4];
+} vr_params;
+
+/* Work counters of one frame (filled by vr_count_work). */
+typedef struct vr_stats {
+    uint64_t rays;            /* covered pixels (rays that enter the box)            */
+    uint64_t samples;         /* executed density samples (trilinear fetches in slab) */
+    uint64_t shaded_samples;  /* samples that also took the 6-tap gradient            */
+    uint64_t steps;           /* loop iterations taken (incl. out-of-slab steps)      */
+} vr_stats;
+
+/* ---- lifecycle ---- */
+int vr_abi_version(void);
+void vr_params_default(vr_params *p);
+
+/* Create a context on HIP device `device` with a w x h framebuffer.  Like the reference
+ * constructor it installs a 1x1x1 volume {0} with min 0 / max 1 and a 1-texel TF
+ * 0xFFFFFFFF (offscreen_pass.cpp:118-119).  Returns NULL on failure (see
+ * vr_last_error(NULL)). */
+typedef struct vr_ctx vr_ctx;
+vr_ctx *vr_create(int device, uint32_t width, uint32_t height);
+void vr_destroy(vr_ctx *ctx);
+const char *vr_last_error(const vr_ctx *ctx);
+
+/* framebuffer_size_changed: 0 sizes are ignored (offscreen_pass.cpp:237-239). */
+int vr_resize(vr_ctx *ctx, uint32_t width, uint32_t height);
+int vr_get_size(const vr_ctx *ctx, uint32_t *width, uint32_t *height);
+
+/* ---- inputs (the callee copies; the caller keeps ownership) ---- */
+
+/* volume_dataset_changed: `data` is nx*ny*nz elements of `dtype`, x fastest (NRRD axis 0),
+ * host memory.  vmin/vmax are Dataset.min/max (nrrd_file_parser.cpp:39-40).  8- and
+ * 16-bit integer and f32 voxels stay native on the device (float(v) is exact); 32/64-bit
+ * integers and f64 are converted to f32 exactly as NrrdFileParser::convert does. */
+int vr_set_volume(vr_ctx *ctx, const void *data, int dtype, uint32_t nx, uint32_t ny,
+                  uint32_t nz, float vmin, float vmax);
+/* Same, with `data` already in device memory of this context's device (linear layout).
+ * `stream` is a hipStream_t (NULL = default stream); the call is stream-ordered and
+ * returns after the bricking kernel was enqueued and completed. */
+int vr_set_volume_device(vr_ctx *ctx, const void *data_dev, int dtype, uint32_t nx,
+                         uint32_t ny, uint32_t nz, float vmin, float vmax, void *stream);
+/* Generate a synthetic volume directly into the bricked device layout (no host copy):
+ * kind 0 = sum of Gaussians (f32 or u8), parameters in DESIGN.md.  Used for the
+ * multi-GiB benchmark configurations. */
+int vr_generate_volume(vr_ctx *ctx, int kind, int dtype, uint32_t nx, uint32_t ny,
+                       uint32_t nz, uint32_t seed, float *vmin_out, float *vmax_out);
+/* Bytes the bricked volume occupies on the device. */
+uint64_t vr_volume_bytes(const vr_ctx *ctx);
+/* Debug/test helpers: read the resident volume back as dense float (x fastest, nx*ny*nz
+ * floats); query dims, min/max and the storage type (0 u8, 1 i8, 2 u16, 3 i16, 4 f32). */
+int vr_debug_read_volume(vr_ctx *ctx, float *out_host);
+int vr_debug_volume_info(const vr_ctx *ctx, uint32_t dims[3], float minmax[2], int *storage);
+
+/* transfer_function_changed: n texels, RGBA8 sRGB, R in the low byte (ImGui packing,
+ * gradient.cpp:102-103). */
+int vr_set_transfer_function(vr_ctx *ctx, const uint32_t *rgba8_srgb, uint32_t n);
+
+/* slicing_changed: samples are taken only strictly inside (min, max) (volume.frag:39-40). */
+int vr_set_slicing(vr_ctx *ctx, const float min_slice[3], const float max_slice[3]);
+
+/* ---- render ---- */
+
+/* Render one full frame synchronously into host memory `out` (W*H*4 bytes for RGBA8,
+ * W*H*16 for RGBA32F), row 0 = top (Vulkan framebuffer order). */
+int vr_render(vr_ctx *ctx, const vr_camera *cam, const vr_params *p, void *out,
+              int out_format);
+
+/* Render into DEVICE memory `out_dev` on `stream` (hipStream_t, NULL = default),
+ * asynchronously.  Image-space sharding for multi-GPU: the frame's rows are cut into
+ * blocks of `row_block` rows and block b is rendered by rank (b % nranks); this rank's
+ * blocks are written densely, in order, to `out_dev` (vr_shard_rows() rows x W pixels).
+ * nranks = 1, rank = 0 renders the whole frame. */
+int vr_render_device(vr_ctx *ctx, const vr_camera *cam, const vr_params *p, void *out_dev,
+                     int out_format, uint32_t row_block, uint32_t rank, uint32_t nranks,
+                     void *stream);
+/* Rows each rank writes for (H, row_block, nranks): ceil(ceil(H/row_block)/nranks)*row_block. */
+uint32_t vr_shard_rows(uint32_t height, uint32_t row_block, uint32_t nranks);
+/* Rank-0 assembly after the gather: `gathered_dev` holds nranks shards back to back
+ * (rank-major, vr_shard_rows() rows each); writes the H x W frame to `out_dev`. */
+int vr_assemble_rows(vr_ctx *ctx, const void *gathered_dev, void *out_dev, int out_format,
+                     uint32_t row_block, uint32_t nranks, void *stream);
+
+/* Count the work of one frame (same camera/params/shard) exactly; synchronous. */
+int vr_count_work(vr_ctx *ctx, const vr_camera *cam, const vr_params *p, uint32_t row_block,
+                  uint32_t rank, uint32_t nranks, vr_stats *out);
+
+/* Kernel timing: when enabled, every vr_render_device brackets the ray-march kernel with
+ * HIP events on the launch stream.  vr_timing_read synchronises and returns the summed
+ * kernel milliseconds and launch count since the last reset. */
+int vr_timing_enable(vr_ctx *ctx, int enable);
+int vr_timing_read(vr_ctx *ctx, double *total_ms, uint64_t *launches);
+int vr_timing_reset(vr_ctx *ctx);
+
+/* Name of the ray-march kernel variant vr_render_device launches for the current volume
+ * and params (for matching rocprof rows); returns a static string. */
+const char *vr_kernel_name(const vr_ctx *ctx, const vr_params *p);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VR_VR_H */

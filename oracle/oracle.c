@@ -1,0 +1,437 @@
+/*
+ * oracle.c — CPU restatement of the reference ray-march.  TEST INFRASTRUCTURE ONLY:
+ * loaded by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline; never by the
+ * product library.  See oracle.h for what it restates and its parity status.
+ *
+ * Build: oracle/Makefile (gcc -O2 -fopenmp -ffp-contract=off -mfma).  Contraction is OFF:
+ * every fused multiply-add below is an explicit fmaf(), so the HIP kernel (built with the
+ * same rule) performs the same IEEE operations in the same order.
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stddef.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ------------------------------------------------------------------------------------ */
+/* glm restatements (float), as used by offscreen_pass.cpp:1158-1167.                    */
+/* Matrices are column-major: m[col*4 + row].                                            */
+/* ------------------------------------------------------------------------------------ */
+
+/* glm operator*(mat4, mat4): Result[j] = A0*B[j][0] + A1*B[j][1] + A2*B[j][2] + A3*B[j][3] */
+static void glm_mul(const float *a, const float *b, float *r)
+{
+    float t[16];
+    for (int j = 0; j < 4; ++j)
+        for (int i = 0; i < 4; ++i) {
+            float acc = a[0 * 4 + i] * b[j * 4 + 0];
+            acc = acc + a[1 * 4 + i] * b[j * 4 + 1];
+            acc = acc + a[2 * 4 + i] * b[j * 4 + 2];
+            acc = acc + a[3 * 4 + i] * b[j * 4 + 3];
+            t[j * 4 + i] = acc;
+        }
+    memcpy(r, t, sizeof(t));
+}
+
+/* glm::perspectiveRH_NO (offscreen_pass.cpp:1166; GLM_FORCE_DEPTH_ZERO_TO_ONE is defined
+ * after glm was first included via offscreen_pass.h:3, so the [-1,1] form is in effect). */
+static void glm_perspective_rh_no(float fovy, float aspect, float zn, float zf, float *m)
+{
+    memset(m, 0, 16 * sizeof(float));
+    float th = tanf(fovy / 2.0f);
+    m[0 * 4 + 0] = 1.0f / (aspect * th);
+    m[1 * 4 + 1] = 1.0f / th;
+    m[2 * 4 + 2] = -(zf + zn) / (zf - zn);
+    m[2 * 4 + 3] = -1.0f;
+    m[3 * 4 + 2] = -(2.0f * zf * zn) / (zf - zn);
+}
+
+/* coordinate_conversion = rotate(I, radians(90), x) * scale(I, (-1,1,1)), glm float math
+ * (offscreen_pass.cpp:1159-1162). */
+static void coordinate_conversion(float *m)
+{
+    const float angle = 90.0f * 0.01745329251994329576923690768489f; /* glm::radians */
+    const float c = cosf(angle), s = sinf(angle);
+    const float ax = 1.0f, ay = 0.0f, az = 0.0f; /* normalize((1,0,0)) */
+    const float tx = (1.0f - c) * ax, ty = (1.0f - c) * ay, tz = (1.0f - c) * az;
+    float rot[16] = {0};
+    rot[0 * 4 + 0] = c + tx * ax;
+    rot[0 * 4 + 1] = tx * ay + s * az;
+    rot[0 * 4 + 2] = tx * az - s * ay;
+    rot[1 * 4 + 0] = ty * ax - s * az;
+    rot[1 * 4 + 1] = c + ty * ay;
+    rot[1 * 4 + 2] = ty * az + s * ax;
+    rot[2 * 4 + 0] = tz * ax + s * ay;
+    rot[2 * 4 + 1] = tz * ay - s * ax;
+    rot[2 * 4 + 2] = c + tz * az;
+    rot[3 * 4 + 3] = 1.0f;
+    float sc[16] = {0};
+    sc[0] = -1.0f;
+    sc[5] = 1.0f;
+    sc[10] = 1.0f;
+    sc[15] = 1.0f;
+    glm_mul(rot, sc, m);
+}
+
+/* Inverse of a 4x4 column-major matrix in double (cofactor expansion, fixed order). */
+static int inverse4d(const double *m, double *inv)
+{
+    double a[16];
+    a[0] = m[5] * m[10] * m[15] - m[5] * m[11] * m[14] - m[9] * m[6] * m[15] +
+           m[9] * m[7] * m[14] + m[13] * m[6] * m[11] - m[13] * m[7] * m[10];
+    a[4] = -m[4] * m[10] * m[15] + m[4] * m[11] * m[14] + m[8] * m[6] * m[15] -
+           m[8] * m[7] * m[14] - m[12] * m[6] * m[11] + m[12] * m[7] * m[10];
+    a[8] = m[4] * m[9] * m[15] - m[4] * m[11] * m[13] - m[8] * m[5] * m[15] +
+           m[8] * m[7] * m[13] + m[12] * m[5] * m[11] - m[12] * m[7] * m[9];
+    a[12] = -m[4] * m[9] * m[14] + m[4] * m[10] * m[13] + m[8] * m[5] * m[14] -
+            m[8] * m[6] * m[13] - m[12] * m[5] * m[10] + m[12] * m[6] * m[9];
+    a[1] = -m[1] * m[10] * m[15] + m[1] * m[11] * m[14] + m[9] * m[2] * m[15] -
+           m[9] * m[3] * m[14] - m[13] * m[2] * m[11] + m[13] * m[3] * m[10];
+    a[5] = m[0] * m[10] * m[15] - m[0] * m[11] * m[14] - m[8] * m[2] * m[15] +
+           m[8] * m[3] * m[14] + m[12] * m[2] * m[11] - m[12] * m[3] * m[10];
+    a[9] = -m[0] * m[9] * m[15] + m[0] * m[11] * m[13] + m[8] * m[1] * m[15] -
+           m[8] * m[3] * m[13] - m[12] * m[1] * m[11] + m[12] * m[3] * m[9];
+    a[13] = m[0] * m[9] * m[14] - m[0] * m[10] * m[13] - m[8] * m[1] * m[14] +
+            m[8] * m[2] * m[13] + m[12] * m[1] * m[10] - m[12] * m[2] * m[9];
+    a[2] = m[1] * m[6] * m[15] - m[1] * m[7] * m[14] - m[5] * m[2] * m[15] +
+           m[5] * m[3] * m[14] + m[13] * m[2] * m[7] - m[13] * m[3] * m[6];
+    a[6] = -m[0] * m[6] * m[15] + m[0] * m[7] * m[14] + m[4] * m[2] * m[15] -
+           m[4] * m[3] * m[14] - m[12] * m[2] * m[7] + m[12] * m[3] * m[6];
+    a[10] = m[0] * m[5] * m[15] - m[0] * m[7] * m[13] - m[4] * m[1] * m[15] +
+            m[4] * m[3] * m[13] + m[12] * m[1] * m[7] - m[12] * m[3] * m[5];
+    a[14] = -m[0] * m[5] * m[14] + m[0] * m[6] * m[13] + m[4] * m[1] * m[14] -
+            m[4] * m[2] * m[13] - m[12] * m[1] * m[6] + m[12] * m[2] * m[5];
+    a[3] = -m[1] * m[6] * m[11] + m[1] * m[7] * m[10] + m[5] * m[2] * m[11] -
+           m[5] * m[3] * m[10] - m[9] * m[2] * m[7] + m[9] * m[3] * m[6];
+    a[7] = m[0] * m[6] * m[11] - m[0] * m[7] * m[10] - m[4] * m[2] * m[11] +
+           m[4] * m[3] * m[10] + m[8] * m[2] * m[7] - m[8] * m[3] * m[6];
+    a[11] = -m[0] * m[5] * m[11] + m[0] * m[7] * m[9] + m[4] * m[1] * m[11] -
+            m[4] * m[3] * m[9] - m[8] * m[1] * m[7] + m[8] * m[3] * m[5];
+    a[15] = m[0] * m[5] * m[10] - m[0] * m[6] * m[9] - m[4] * m[1] * m[10] +
+            m[4] * m[2] * m[9] + m[8] * m[1] * m[6] - m[8] * m[2] * m[5];
+    double det = m[0] * a[0] + m[1] * a[4] + m[2] * a[8] + m[3] * a[12];
+    if (det == 0.0) return 0;
+    double id = 1.0 / det;
+    for (int i = 0; i < 16; ++i) inv[i] = a[i] * id;
+    return 1;
+}
+
+/* Per-frame unprojection: inverse of the float matrix (proj * view) that volume.vert:23
+ * applies ((proj*view)*v), in double. */
+typedef struct ray_frame {
+    double inv[16];
+    int ok;
+} ray_frame;
+
+static void make_ray_frame(const or_scene *s, ray_frame *f)
+{
+    float fovy = (s->fovy_deg > 0.0f ? s->fovy_deg : 40.0f) * 0.01745329251994329576923690768489f;
+    float zn = s->znear > 0.0f ? s->znear : 0.1f;
+    float zf = s->zfar > 0.0f ? s->zfar : 10.0f;
+    float aspect = (float)s->width / (float)s->height;
+    float persp[16], conv[16], proj[16], pv[16];
+    glm_perspective_rh_no(fovy, aspect, zn, zf, persp);
+    coordinate_conversion(conv);
+    glm_mul(persp, conv, proj);
+    glm_mul(proj, s->view, pv);
+    double pvd[16];
+    for (int i = 0; i < 16; ++i) pvd[i] = (double)pv[i];
+    f->ok = inverse4d(pvd, f->inv);
+}
+
+/* Ray entry of one pixel: the cube's camera-facing face hit by the pixel-centre ray,
+ * inside the Vulkan clip volume 0 <= z_ndc <= 1 (back faces culled, :680-681; clipped
+ * front faces leave the clear colour).  Returns 1 if covered. */
+static int pixel_ray(const or_scene *s, const ray_frame *f, int px, int py, float tex[3],
+                     float frag[3], float dir[3])
+{
+    if (!f->ok) return 0;
+    const double *m = f->inv;
+    double x = ((double)px + 0.5) / (double)s->width * 2.0 - 1.0;
+    double y = ((double)py + 0.5) / (double)s->height * 2.0 - 1.0;
+    double h0[4], h1[4];
+    for (int r = 0; r < 4; ++r) {
+        h0[r] = m[0 * 4 + r] * x + m[1 * 4 + r] * y + m[3 * 4 + r];
+        h1[r] = h0[r] + m[2 * 4 + r];
+    }
+    double p0[3], d[3];
+    for (int r = 0; r < 3; ++r) {
+        p0[r] = h0[r] / h0[3];
+        d[r] = h1[r] / h1[3] - p0[r];
+    }
+    double te = -INFINITY, tx = INFINITY;
+    int axis = 0;
+    for (int a = 0; a < 3; ++a) {
+        double lo, hi;
+        if (d[a] == 0.0) {
+            if (p0[a] < -0.5 || p0[a] > 0.5) return 0;
+            lo = -INFINITY;
+            hi = INFINITY;
+        } else {
+            double t1 = (-0.5 - p0[a]) / d[a];
+            double t2 = (0.5 - p0[a]) / d[a];
+            lo = t1 < t2 ? t1 : t2;
+            hi = t1 < t2 ? t2 : t1;
+        }
+        if (lo > te) {
+            te = lo;
+            axis = a;
+        }
+        if (hi < tx) tx = hi;
+    }
+    if (!(te < tx) || te < 0.0 || te > 1.0) return 0;
+    for (int a = 0; a < 3; ++a) {
+        double e = p0[a] + te * d[a];
+        frag[a] = (float)e;
+        tex[a] = (float)(e + 0.5);
+    }
+    frag[axis] = d[axis] > 0.0 ? -0.5f : 0.5f;
+    tex[axis] = d[axis] > 0.0 ? 0.0f : 1.0f;
+    /* volume.frag:23  ray_dir = normalize(in_frag_position - camera_position) */
+    float vx = frag[0] - s->cam_pos[0];
+    float vy = frag[1] - s->cam_pos[1];
+    float vz = frag[2] - s->cam_pos[2];
+    float len = sqrtf(vx * vx + vy * vy + vz * vz);
+    dir[0] = vx / len;
+    dir[1] = vy / len;
+    dir[2] = vz / len;
+    return 1;
+}
+
+int or_pixel_ray(const or_scene *s, int px, int py, float tex_out[3], float frag_out[3],
+                 float dir_out[3])
+{
+    ray_frame f;
+    make_ray_frame(s, &f);
+    return pixel_ray(s, &f, px, py, tex_out, frag_out, dir_out);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Samplers                                                                              */
+/* ------------------------------------------------------------------------------------ */
+
+static inline float lerpf(float a, float b, float w) { return fmaf(w, b - a, a); }
+
+/* R32_SFLOAT 3D image, CLAMP_TO_BORDER with TRANSPARENT_BLACK (offscreen_pass.cpp:968,
+ * 1016-1031): texels outside [0,N) read 0. */
+static inline float voxel(const float *v, int nx, int ny, int nz, int x, int y, int z)
+{
+    if (x < 0 || y < 0 || z < 0 || x >= nx || y >= ny || z >= nz) return 0.0f;
+    return v[(size_t)x + (size_t)nx * ((size_t)y + (size_t)ny * (size_t)z)];
+}
+
+/* Trilinear filter of the 2x2x2 cell whose low corner is (i,j,k), weights (ax,ay,az):
+ * lerp along x, then y, then z. */
+static inline float tri_cell(const float *v, int nx, int ny, int nz, int i, int j, int k,
+                             float ax, float ay, float az)
+{
+    float c00 = lerpf(voxel(v, nx, ny, nz, i, j, k), voxel(v, nx, ny, nz, i + 1, j, k), ax);
+    float c10 = lerpf(voxel(v, nx, ny, nz, i, j + 1, k), voxel(v, nx, ny, nz, i + 1, j + 1, k), ax);
+    float c01 = lerpf(voxel(v, nx, ny, nz, i, j, k + 1), voxel(v, nx, ny, nz, i + 1, j, k + 1), ax);
+    float c11 = lerpf(voxel(v, nx, ny, nz, i, j + 1, k + 1),
+                      voxel(v, nx, ny, nz, i + 1, j + 1, k + 1), ax);
+    float c0 = lerpf(c00, c10, ay);
+    float c1 = lerpf(c01, c11, ay);
+    return lerpf(c0, c1, az);
+}
+
+/* Normalised coordinate -> texel space: u = s*N - 0.5 (texel i's centre at (i+0.5)/N). */
+static inline void texel_coord(float p, int n, int *i, float *a)
+{
+    float u = p * (float)n - 0.5f;
+    float f = floorf(u);
+    *a = u - f;
+    *i = (int)f;
+}
+
+float or_trilinear(const float *vol, int nx, int ny, int nz, float px, float py, float pz)
+{
+    /* keep the integer conversion defined far outside the box (KAT helper only) */
+    px = fminf(fmaxf(px, -1.0f), 2.0f);
+    py = fminf(fmaxf(py, -1.0f), 2.0f);
+    pz = fminf(fmaxf(pz, -1.0f), 2.0f);
+    int i, j, k;
+    float ax, ay, az;
+    texel_coord(px, nx, &i, &ax);
+    texel_coord(py, ny, &j, &ay);
+    texel_coord(pz, nz, &k, &az);
+    return tri_cell(vol, nx, ny, nz, i, j, k, ax, ay, az);
+}
+
+/* R8G8B8A8_SRGB texels (offscreen_pass.cpp:1076): RGB UNORM-decoded then sRGB->linear
+ * BEFORE filtering; A linear c/255. */
+static float srgb_to_linear(uint32_t c8)
+{
+    double c = (double)c8 / 255.0;
+    double l = c <= 0.04045 ? c / 12.92 : pow((c + 0.055) / 1.055, 2.4);
+    return (float)l;
+}
+
+void or_tf_decode(const uint32_t *tf, int n, float *lut)
+{
+    for (int i = 0; i < n; ++i) {
+        uint32_t t = tf[i];
+        lut[i * 4 + 0] = srgb_to_linear(t & 0xFFu);
+        lut[i * 4 + 1] = srgb_to_linear((t >> 8) & 0xFFu);
+        lut[i * 4 + 2] = srgb_to_linear((t >> 16) & 0xFFu);
+        lut[i * 4 + 3] = (float)((t >> 24) & 0xFFu) / 255.0f;
+    }
+}
+
+/* 1D LINEAR filter, CLAMP_TO_EDGE (offscreen_pass.cpp:1125-1150).  The clamp of u to
+ * [-1, n] keeps the float->int conversion defined for t = +-inf/NaN (min == max). */
+static inline void tf_lookup(const float *lut, int n, float t, float out[4])
+{
+    float u = t * (float)n - 0.5f;
+    u = fminf(fmaxf(u, -1.0f), (float)n);
+    float f = floorf(u);
+    float w = u - f;
+    int i0 = (int)f, i1 = i0 + 1;
+    i0 = i0 < 0 ? 0 : (i0 > n - 1 ? n - 1 : i0);
+    i1 = i1 < 0 ? 0 : (i1 > n - 1 ? n - 1 : i1);
+    for (int c = 0; c < 4; ++c) out[c] = lerpf(lut[i0 * 4 + c], lut[i1 * 4 + c], w);
+}
+
+void or_tf_sample(const uint32_t *tf, int n, float t, float out[4])
+{
+    float *lut = (float *)malloc((size_t)n * 4 * sizeof(float));
+    or_tf_decode(tf, n, lut);
+    tf_lookup(lut, n, t, out);
+    free(lut);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* The ray-march (volume.frag:21-52) + blend (offscreen_pass.cpp:715-725)                */
+/* ------------------------------------------------------------------------------------ */
+
+static float powi(float x, int p)
+{
+    float r = 1.0f;
+    for (int k = 0; k < p; ++k) r = r * x;
+    return r;
+}
+
+static void march_pixel(const or_scene *s, const ray_frame *f, const float *lut, int px,
+                        int py, float *out, or_stats *st)
+{
+    float tex[3], frag[3], dir[3];
+    if (!pixel_ray(s, f, px, py, tex, frag, dir)) {
+        for (int c = 0; c < 4; ++c) out[c] = s->clear[c];
+        return;
+    }
+    st->rays++;
+    const int nx = s->nx, ny = s->ny, nz = s->nz;
+    const float step = s->step;
+    const int nsteps = (int)(s->ray_dist / step); /* volume.frag:31 int(ray_dist/step_size) */
+    const float range = s->vmax - s->vmin;
+    float T = 1.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f;
+    float p0 = tex[0], p1 = tex[1], p2 = tex[2];
+    for (int it = 0; it < nsteps; ++it) {
+        /* volume.frag:34-37: break if any component > 1 or < 0 */
+        if (p0 > 1.0f || p1 > 1.0f || p2 > 1.0f || p0 < 0.0f || p1 < 0.0f || p2 < 0.0f) break;
+        st->steps++;
+        /* volume.frag:39-40: strict slab test */
+        if (p0 < s->smax[0] && p1 < s->smax[1] && p2 < s->smax[2] && p0 > s->smin[0] &&
+            p1 > s->smin[1] && p2 > s->smin[2]) {
+            int i, j, k;
+            float ax, ay, az;
+            texel_coord(p0, nx, &i, &ax);
+            texel_coord(p1, ny, &j, &ay);
+            texel_coord(p2, nz, &k, &az);
+            const float d = tri_cell(s->vol, nx, ny, nz, i, j, k, ax, ay, az); /* :41 */
+            const float t = (d - s->vmin) / range;                              /* :42 */
+            float sc[4];
+            tf_lookup(lut, s->tf_n, t, sc); /* :43 */
+            st->samples++;
+            if (s->shading && sc[3] > 0.0f) {
+                /* extension: central differences one texel apart, same weights */
+                const float gx = tri_cell(s->vol, nx, ny, nz, i + 1, j, k, ax, ay, az) -
+                                 tri_cell(s->vol, nx, ny, nz, i - 1, j, k, ax, ay, az);
+                const float gy = tri_cell(s->vol, nx, ny, nz, i, j + 1, k, ax, ay, az) -
+                                 tri_cell(s->vol, nx, ny, nz, i, j - 1, k, ax, ay, az);
+                const float gz = tri_cell(s->vol, nx, ny, nz, i, j, k + 1, ax, ay, az) -
+                                 tri_cell(s->vol, nx, ny, nz, i, j, k - 1, ax, ay, az);
+                st->shaded_samples++;
+                const float wx = gx * (float)nx, wy = gy * (float)ny, wz = gz * (float)nz;
+                const float g2 = wx * wx + wy * wy + wz * wz;
+                if (g2 > 0.0f) {
+                    const float inv = 1.0f / sqrtf(g2);
+                    const float ndl = fabsf((wx * dir[0] + wy * dir[1] + wz * dir[2]) * inv);
+                    const float kdiff = s->ka + s->kd * ndl;
+                    const float spec = s->ks * powi(ndl, s->spec_power);
+                    sc[0] = sc[0] * kdiff + spec;
+                    sc[1] = sc[1] * kdiff + spec;
+                    sc[2] = sc[2] * kdiff + spec;
+                }
+            }
+            /* volume.frag:44-45  C.rgb += T * (s.a * s.rgb);  T *= 1 - s.a */
+            cr = cr + (sc[0] * sc[3]) * T;
+            cg = cg + (sc[1] * sc[3]) * T;
+            cb = cb + (sc[2] * sc[3]) * T;
+            T = T * (1.0f - sc[3]);
+            if (T == 0.0f) break; /* exact: later samples add (rgb*a)*0 */
+            if (T < s->ert_eps) break;
+        }
+        /* volume.frag:47  ray_pos += ray_dir * step_size */
+        p0 = p0 + dir[0] * step;
+        p1 = p1 + dir[1] * step;
+        p2 = p2 + dir[2] * step;
+    }
+    /* volume.frag:50 alpha = 1 - T; blend SRC_ALPHA / ONE_MINUS_SRC_ALPHA over clear */
+    const float A = 1.0f - T;
+    const float omA = 1.0f - A;
+    out[0] = cr * A + s->clear[0] * omA;
+    out[1] = cg * A + s->clear[1] * omA;
+    out[2] = cb * A + s->clear[2] * omA;
+    out[3] = A * A + s->clear[3] * omA;
+}
+
+int or_render_rows(const or_scene *s, float *out, int row0, int row1, int nthreads,
+                   or_stats *stats)
+{
+    if (!s || !out || !s->vol || !s->tf || s->tf_n <= 0 || s->width <= 0 || s->height <= 0)
+        return -22;
+    if (row0 < 0) row0 = 0;
+    if (row1 > s->height) row1 = s->height;
+    ray_frame f;
+    make_ray_frame(s, &f);
+    float *lut = (float *)malloc((size_t)s->tf_n * 4 * sizeof(float));
+    if (!lut) return -12;
+    or_tf_decode(s->tf, s->tf_n, lut);
+    uint64_t rays = 0, samples = 0, shaded = 0, steps = 0;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) \
+    reduction(+ : rays, samples, shaded, steps)
+#endif
+    for (int y = row0; y < row1; ++y) {
+        or_stats st = {0, 0, 0, 0};
+        for (int x = 0; x < s->width; ++x)
+            march_pixel(s, &f, lut, x, y, out + ((size_t)y * s->width + x) * 4, &st);
+        rays += st.rays;
+        samples += st.samples;
+        shaded += st.shaded_samples;
+        steps += st.steps;
+    }
+    free(lut);
+    if (stats) {
+        stats->rays = rays;
+        stats->samples = samples;
+        stats->shaded_samples = shaded;
+        stats->steps = steps;
+    }
+    return 0;
+}
+
+int or_max_threads(void)
+{
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}

@@ -1,0 +1,84 @@
+/*
+ * oracle.h — CPU restatement of the reference ray-march (TEST INFRASTRUCTURE ONLY).
+ *
+ * This is the parity checker for the MI355X HIP path.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it; the product library never links it.
+ *
+ * It restates, in plain C (OpenMP over pixel rows):
+ *   res/shaders/volume.frag:21-52      the ray-march loop, predicates, composite, op order
+ *   res/shaders/volume.vert:19-24      tex_coords / frag_position attributes (ray entry)
+ *   src/rendering/offscreen_pass.cpp   :55-90 cube geometry (tex = pos + 0.5), :170-173 clear,
+ *                                      :293 RGBA8 target, :680-681 cull back, :701-712 depth,
+ *                                      :715-725 blend, :968 + :1014-1039 R32F volume + border
+ *                                      sampler, :1076 + :1125-1150 sRGB TF + clamp sampler,
+ *                                      :1152-1171 projection * coordinate_conversion
+ *   src/data/nrrd_file_parser.cpp:39-40 min/max density normalisation inputs
+ * plus the build's own extension (central-difference gradient Phong shading; the reference
+ * has no shading).
+ *
+ * Parity status: the reference's hot path is a Vulkan fragment shader that cannot run in
+ * this container (no Vulkan/ICD/glslc) and the reference ships no tests or
+ * golden images, so pixel parity against the REAL reference is unpinned.  This restatement
+ * is pinned by (1) closed-form known-answer tests (constant TF,
+ * transparent TF, startup TF, sampler unit KATs) and (2) an independent float64 numpy
+ * restatement (oracle/ref_numpy.py); both are committed under tests/golden/.
+ */
+#ifndef VR_ORACLE_H
+#define VR_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct or_scene {
+    /* Dataset (src/data/dataset.h:9-13): dense float voxels, x fastest. */
+    const float *vol;
+    int32_t nx, ny, nz;
+    float vmin, vmax;
+    /* transfer function texels, RGBA8 sRGB, R in the low byte */
+    const uint32_t *tf;
+    int32_t tf_n;
+    /* slicing box */
+    float smin[3], smax[3];
+    /* camera (view column-major, as Camera::get_view) */
+    float view[16];
+    float cam_pos[3];
+    float fovy_deg, znear, zfar;
+    int32_t width, height;
+    /* params */
+    float step, ray_dist, ert_eps;
+    int32_t shading;
+    float clear[4];
+    float ka, kd, ks;
+    int32_t spec_power;
+} or_scene;
+
+typedef struct or_stats {
+    uint64_t rays, samples, shaded_samples, steps;
+} or_stats;
+
+/* Render rows [row0, row1) of the frame into out (float RGBA, row-major, full-frame
+ * indexing: out[(y*W + x)*4 + c]).  nthreads <= 0 uses the OpenMP default. */
+int or_render_rows(const or_scene *s, float *out, int row0, int row1, int nthreads,
+                   or_stats *stats);
+
+/* Sampler unit functions (KATs). */
+float or_trilinear(const float *vol, int nx, int ny, int nz, float px, float py, float pz);
+void or_tf_decode(const uint32_t *tf, int n, float *lut /* n*4 */);
+void or_tf_sample(const uint32_t *tf, int n, float t, float out[4]);
+
+/* Ray setup of one pixel: returns 1 if the pixel is covered by the cube's front face.
+ * tex_out = in_tex_coords, frag_out = in_frag_position, dir_out = normalize(frag - cam). */
+int or_pixel_ray(const or_scene *s, int px, int py, float tex_out[3], float frag_out[3],
+                 float dir_out[3]);
+
+/* Number of OpenMP threads this build would use by default. */
+int or_max_threads(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VR_ORACLE_H */

@@ -1,0 +1,195 @@
+"""Generate the committed golden fixtures under tests/golden/ (run in the build container).
+
+scenes.npz      small render fixtures: inputs (volume, TF, camera, params, slicing) and the C
+                oracle's float RGBA output + work counters; each cross-checked against the
+                independent float64 restatement (oracle/ref_numpy.py) before it is written.
+kat_b4.json     sampler known-answer vectors, computed in closed form.
+nrrd/           small NRRD files in every element type and encoding the reference's NrrdIO
+                build reads (raw LE/BE, ascii, hex; attached .nrrd and detached .nhdr), plus
+                gzip (must be rejected) and dim != 3 (must be rejected).
+nrrd/expect.json  what the REFERENCE's NrrdIO (compiled from /root/reference/extern/NrrdIO
+                by oracle/Makefile) loads from each file through the restated
+                NrrdFileParser::parse: dims, type, min, max, sha256 of the float32 data.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import struct
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for sub in ("volumetric-renderer_amd", "oracle", "tools"):
+    sys.path.insert(0, os.path.join(ROOT, sub))
+import pyoracle  # noqa: E402
+import ref_numpy  # noqa: E402
+import synth  # noqa: E402
+import vr_amd  # noqa: E402
+
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+SCENES = [
+    # name, volume, W, H, camera, tf, shading, slicing
+    ("blob8_default_tf1", ("blob", 8), 32, 32, "default", "tf1", 0, None),
+    ("blob16_rotA_tf2", ("blob", 16), 32, 24, "rotA", "tf2", 0, None),
+    ("gauss16_rotB_tfc", ("gauss", 16), 32, 32, "rotB", "tfc", 0, None),
+    ("gauss16_fill_tfc_shaded", ("gauss", 16), 32, 32, "fill_oblique", "tfc", 1, None),
+    ("gauss12_rotA_tf2_sliced", ("gauss", 12), 24, 32, "rotA", "tf2", 0,
+     ((0.2, 0.0, 0.1), (0.8, 1.0, 0.9))),
+    ("blob8_default_tf0", ("blob", 8), 16, 16, "default", "tf0", 0, None),
+]
+
+
+def make_volume(spec):
+    kind, n = spec
+    if kind == "blob":
+        return synth.gaussian_blob(n)
+    return synth.gaussians_numpy((n, n, n), seed=13)
+
+
+def scenes():
+    out = {}
+    for name, vspec, W, H, camname, tfname, shading, sl in SCENES:
+        vol = make_volume(vspec)
+        tf = synth.TFS[tfname]()
+        cam = synth.camera(camname).to_vr_camera()
+        p = vr_amd.default_params(shading=shading)
+        smin, smax = sl if sl else ((0, 0, 0), (1, 1, 1))
+        sc = pyoracle.Scene.from_params(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p,
+                                        smin, smax)
+        img, st = sc.render()
+        ref = ref_numpy.render(vol, float(vol.min()), float(vol.max()), tf, list(cam.view),
+                               list(cam.position), W, H, smin, smax, shading=bool(shading))
+        d = img.astype(np.float64) - ref
+        rmse = float(np.sqrt(np.mean(d * d)))
+        assert rmse < 1e-5, (name, rmse)
+        out[name + "/vol"] = vol
+        out[name + "/tf"] = tf
+        out[name + "/view"] = np.array(cam.view[:], np.float32)
+        out[name + "/pos"] = np.array(cam.position[:], np.float32)
+        out[name + "/size"] = np.array([W, H], np.int32)
+        out[name + "/shading"] = np.array(shading, np.int32)
+        out[name + "/slice"] = np.array([smin, smax], np.float32)
+        out[name + "/img"] = img
+        out[name + "/stats"] = np.array([st["rays"], st["samples"], st["shaded_samples"], st["steps"]],
+                                        np.uint64)
+        print(f"{name}: rmse vs float64 restatement {rmse:.2e}, stats {st}")
+    np.savez_compressed(os.path.join(GOLD, "scenes.npz"), **out)
+
+
+def kat_b4():
+    v = np.arange(1, 9, dtype=np.float32).reshape(2, 2, 2) * np.float32(1.5)  # v[z][y][x]
+    kat = {
+        "volume_zyx": v.tolist(),
+        "trilinear": [
+            {"pos": [0.25, 0.25, 0.25], "expect": float(v[0, 0, 0])},                 # texel centre
+            {"pos": [0.5, 0.5, 0.5], "expect": float(v.mean())},                      # mean of all 8
+            {"pos": [0.125, 0.25, 0.25], "expect": float(0.75 * v[0, 0, 0])},         # border = 0
+            {"pos": [0.75, 0.75, 0.75], "expect": float(v[1, 1, 1])},
+            {"pos": [1.0, 0.25, 0.25], "expect": float(0.5 * v[0, 0, 1])},            # u = 1.5
+        ],
+        "tf_texels": [0xFF000000, 0xFFFFFFFF],
+        "tf": [
+            {"t": 0.5, "expect_rgb": 0.5, "expect_a": 1.0},    # decode BEFORE lerp (not 0.214)
+            {"t": 0.1, "expect_rgb": 0.0, "expect_a": 1.0},    # clamp to texel 0
+            {"t": 0.375, "expect_rgb": 0.25, "expect_a": 1.0},
+            {"t": 2.0, "expect_rgb": 1.0, "expect_a": 1.0},
+        ],
+    }
+    with open(os.path.join(GOLD, "kat_b4.json"), "w") as f:
+        json.dump(kat, f, indent=1)
+
+
+# ---- NRRD fixtures ----
+NRRD_TYPES = {"int8": np.int8, "uchar": np.uint8, "short": np.int16, "ushort": np.uint16,
+              "int": np.int32, "uint": np.uint32, "longlong": np.int64, "ulonglong": np.uint64,
+              "float": np.float32, "double": np.float64}
+
+
+def nrrd_files():
+    d = os.path.join(GOLD, "nrrd")
+    os.makedirs(d, exist_ok=True)
+    rng = np.random.default_rng(99)
+    files = []
+    dims = (5, 4, 3)
+    for tname, dt in NRRD_TYPES.items():
+        if np.issubdtype(dt, np.integer):
+            info = np.iinfo(dt)
+            a = rng.integers(max(info.min, -1000), min(info.max, 1000) + 1, size=dims[::-1]).astype(dt)
+        else:
+            a = (rng.standard_normal(dims[::-1]) * 100).astype(dt)
+        for enc in ("raw", "ascii", "hex"):
+            for endian in (("little", "big") if a.itemsize > 1 and enc != "ascii" else ("little",)):
+                name = f"{tname}_{enc}_{endian}"
+                hdr = [f"NRRD0004", "# fixture", f"type: {tname}", "dimension: 3",
+                       f"sizes: {dims[0]} {dims[1]} {dims[2]}", f"encoding: {enc}",
+                       "spacings: 1.0 1.5 2.0", "key:=value"]
+                if a.itemsize > 1 and enc != "ascii":
+                    hdr.append(f"endian: {endian}")
+                raw = a.astype(a.dtype.newbyteorder("<" if endian == "little" else ">")).tobytes()
+                if enc == "raw":
+                    body = raw
+                elif enc == "hex":
+                    h = raw.hex()
+                    body = ("\n".join(h[i:i + 64] for i in range(0, len(h), 64)) + "\n").encode()
+                else:
+                    vals = [repr(float(x)) if a.dtype.kind == "f" else str(int(x)) for x in a.ravel()]
+                    body = ("\n".join(" ".join(vals[i:i + 7]) for i in range(0, len(vals), 7)) + "\n").encode()
+                # attached .nrrd
+                with open(os.path.join(d, name + ".nrrd"), "wb") as f:
+                    f.write(("\n".join(hdr) + "\n\n").encode() + body)
+                files.append(name + ".nrrd")
+                if enc == "raw" and endian == "little":
+                    # detached .nhdr + data file
+                    with open(os.path.join(d, name + ".nhdr"), "w") as f:
+                        f.write("\n".join(hdr) + f"\ndata file: {name}.data\n")
+                    with open(os.path.join(d, name + ".data"), "wb") as f:
+                        f.write(body)
+                    files.append(name + ".nhdr")
+    # byte skip -1 (data at the end) and line skip on a detached file
+    a = np.arange(60, dtype=np.uint16).reshape(3, 4, 5)
+    with open(os.path.join(d, "skip.nhdr"), "w") as f:
+        f.write("NRRD0004\ntype: ushort\ndimension: 3\nsizes: 5 4 3\nencoding: raw\n"
+                "endian: little\nbyte skip: -1\ndata file: skip.data\n")
+    with open(os.path.join(d, "skip.data"), "wb") as f:
+        f.write(b"JUNKHEADER" * 7 + a.astype("<u2").tobytes())
+    files.append("skip.nhdr")
+    with open(os.path.join(d, "lineskip.nhdr"), "w") as f:
+        f.write("NRRD0004\ntype: uchar\ndimension: 3\nsizes: 2 2 2\nencoding: ascii\n"
+                "line skip: 2\ndata file: lineskip.txt\n")
+    with open(os.path.join(d, "lineskip.txt"), "w") as f:
+        f.write("comment line one\ncomment line two\n1 2 3 4\n5 6 7 250\n")
+    files.append("lineskip.nhdr")
+    # must be rejected: gzip (NrrdIO built without zlib), dimension 2, truncated raw
+    with open(os.path.join(d, "gzip.nrrd"), "wb") as f:
+        f.write(b"NRRD0004\ntype: uchar\ndimension: 3\nsizes: 2 2 2\nencoding: gzip\n\n" + b"\x1f\x8b" + b"\0" * 20)
+    with open(os.path.join(d, "dim2.nrrd"), "wb") as f:
+        f.write(b"NRRD0004\ntype: uchar\ndimension: 2\nsizes: 2 2\nencoding: raw\n\n" + bytes(4))
+    with open(os.path.join(d, "short.nrrd"), "wb") as f:
+        f.write(b"NRRD0004\ntype: float\ndimension: 3\nsizes: 4 4 4\nencoding: raw\nendian: little\n\n" + bytes(16))
+    files += ["gzip.nrrd", "dim2.nrrd", "short.nrrd"]
+    expect = {}
+    if not pyoracle.nrrdio_available():
+        raise SystemExit("oracle/_ref/libnrrdref.so missing: run make -C oracle (needs /root/reference)")
+    for fn in files:
+        rc, res = pyoracle.nrrdio_load(os.path.join(d, fn))
+        if rc != 0:
+            expect[fn] = {"rc": rc}
+            continue
+        data = res["data"].astype(np.float32)
+        expect[fn] = {"rc": 0, "dims": list(res["dims"]), "nrrd_type": res["nrrd_type"],
+                      "vmin": float(res["vmin"]), "vmax": float(res["vmax"]),
+                      "sha256_f32": hashlib.sha256(data.tobytes()).hexdigest()}
+    with open(os.path.join(d, "expect.json"), "w") as f:
+        json.dump(expect, f, indent=1, sort_keys=True)
+    print(f"{len(files)} NRRD fixtures; NrrdIO accepted {sum(1 for v in expect.values() if v['rc'] == 0)}")
+
+
+if __name__ == "__main__":
+    os.makedirs(GOLD, exist_ok=True)
+    scenes()
+    kat_b4()
+    nrrd_files()

@@ -1,0 +1,788 @@
+// vr_api.hip — the C ABI (include/vr/vr.h) over the gfx950 kernels.
+//
+// Restates the resource side of Vol::Rendering::OffscreenPass
+// (src/rendering/offscreen_pass.cpp): volume upload (:940-989, here: native dtype, bricked
+// on the device), TF upload (:1049-1099, here: sRGB decoded once on the host, staged in LDS by
+// the kernel), slicing (:271-277), and update_uniform_buffer (:1152-1171, here: the per-frame
+// unprojection matrix the kernel's ray setup uses).  No exceptions cross the ABI; HIP errors
+// become negative status codes with a message in vr_last_error().
+#include "../../include/vr/vr.h"
+#include "vr_internal.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#pragma clang fp contract(off)
+
+using namespace vr;
+
+struct vr_ctx {
+    int device = 0;
+    uint32_t width = 0, height = 0;
+    // volume (bricked, native storage type)
+    void *bricks = nullptr;
+    size_t brick_bytes = 0;
+    int storage = ST_F32;
+    uint32_t nx = 1, ny = 1, nz = 1;
+    float vmin = 0.0f, vmax = 1.0f;
+    // transfer function (decoded, linear float RGBA)
+    float4 *tf = nullptr;
+    uint32_t tf_n = 0;
+    float smin[3] = {0.0f, 0.0f, 0.0f};
+    float smax[3] = {1.0f, 1.0f, 1.0f};
+    // scratch
+    unsigned long long *counters = nullptr;
+    void *frame_dev = nullptr;
+    size_t frame_bytes = 0;
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
+    double timed_ms = 0.0;
+    uint64_t timed_launches = 0;
+    std::string err;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(vr_ctx *c, int code, const std::string &msg)
+{
+    if (c)
+        c->err = msg;
+    else
+        g_err = msg;
+    return code;
+}
+
+int hip_fail(vr_ctx *c, hipError_t e, const char *what)
+{
+    std::string m = std::string(what) + ": " + hipGetErrorString(e);
+    return fail(c, e == hipErrorOutOfMemory ? VR_ENOMEM : VR_EIO, m);
+}
+
+#define HIP_TRY(c, expr, what)                        \
+    do {                                              \
+        hipError_t _e = (expr);                       \
+        if (_e != hipSuccess) return hip_fail(c, _e, what); \
+    } while (0)
+
+int storage_for(int dtype)
+{
+    switch (dtype) {
+        case VR_DTYPE_U8: return ST_U8;
+        case VR_DTYPE_I8: return ST_I8;
+        case VR_DTYPE_U16: return ST_U16;
+        case VR_DTYPE_I16: return ST_I16;
+        case VR_DTYPE_I32:
+        case VR_DTYPE_U32:
+        case VR_DTYPE_I64:
+        case VR_DTYPE_U64:
+        case VR_DTYPE_F32:
+        case VR_DTYPE_F64: return ST_F32;  // static_cast<float>, nrrd_file_parser.cpp:67-77
+        default: return -1;
+    }
+}
+
+size_t dtype_size(int dtype)
+{
+    switch (dtype) {
+        case VR_DTYPE_U8:
+        case VR_DTYPE_I8: return 1;
+        case VR_DTYPE_U16:
+        case VR_DTYPE_I16: return 2;
+        case VR_DTYPE_I32:
+        case VR_DTYPE_U32:
+        case VR_DTYPE_F32: return 4;
+        default: return 8;
+    }
+}
+
+// ---- glm restatements (float), offscreen_pass.cpp:1158-1167 ----
+void glm_mul(const float *a, const float *b, float *r)
+{
+    float t[16];
+    for (int j = 0; j < 4; ++j)
+        for (int i = 0; i < 4; ++i) {
+            float acc = a[0 * 4 + i] * b[j * 4 + 0];
+            acc = acc + a[1 * 4 + i] * b[j * 4 + 1];
+            acc = acc + a[2 * 4 + i] * b[j * 4 + 2];
+            acc = acc + a[3 * 4 + i] * b[j * 4 + 3];
+            t[j * 4 + i] = acc;
+        }
+    std::memcpy(r, t, sizeof(t));
+}
+
+void perspective_rh_no(float fovy, float aspect, float zn, float zf, float *m)
+{
+    std::memset(m, 0, 16 * sizeof(float));
+    const float th = std::tan(fovy / 2.0f);
+    m[0] = 1.0f / (aspect * th);
+    m[5] = 1.0f / th;
+    m[10] = -(zf + zn) / (zf - zn);
+    m[11] = -1.0f;
+    m[14] = -(2.0f * zf * zn) / (zf - zn);
+}
+
+void coordinate_conversion(float *m)
+{
+    const float angle = 90.0f * 0.01745329251994329576923690768489f;
+    const float c = std::cos(angle), s = std::sin(angle);
+    const float ax = 1.0f, ay = 0.0f, az = 0.0f;
+    const float tx = (1.0f - c) * ax, ty = (1.0f - c) * ay, tz = (1.0f - c) * az;
+    float rot[16] = {0};
+    rot[0] = c + tx * ax;
+    rot[1] = tx * ay + s * az;
+    rot[2] = tx * az - s * ay;
+    rot[4] = ty * ax - s * az;
+    rot[5] = c + ty * ay;
+    rot[6] = ty * az + s * ax;
+    rot[8] = tz * ax + s * ay;
+    rot[9] = tz * ay - s * ax;
+    rot[10] = c + tz * az;
+    rot[15] = 1.0f;
+    float sc[16] = {0};
+    sc[0] = -1.0f;
+    sc[5] = 1.0f;
+    sc[10] = 1.0f;
+    sc[15] = 1.0f;
+    glm_mul(rot, sc, m);
+}
+
+bool inverse4d(const double *m, double *inv)
+{
+    double a[16];
+    a[0] = m[5] * m[10] * m[15] - m[5] * m[11] * m[14] - m[9] * m[6] * m[15] +
+           m[9] * m[7] * m[14] + m[13] * m[6] * m[11] - m[13] * m[7] * m[10];
+    a[4] = -m[4] * m[10] * m[15] + m[4] * m[11] * m[14] + m[8] * m[6] * m[15] -
+           m[8] * m[7] * m[14] - m[12] * m[6] * m[11] + m[12] * m[7] * m[10];
+    a[8] = m[4] * m[9] * m[15] - m[4] * m[11] * m[13] - m[8] * m[5] * m[15] +
+           m[8] * m[7] * m[13] + m[12] * m[5] * m[11] - m[12] * m[7] * m[9];
+    a[12] = -m[4] * m[9] * m[14] + m[4] * m[10] * m[13] + m[8] * m[5] * m[14] -
+            m[8] * m[6] * m[13] - m[12] * m[5] * m[10] + m[12] * m[6] * m[9];
+    a[1] = -m[1] * m[10] * m[15] + m[1] * m[11] * m[14] + m[9] * m[2] * m[15] -
+           m[9] * m[3] * m[14] - m[13] * m[2] * m[11] + m[13] * m[3] * m[10];
+    a[5] = m[0] * m[10] * m[15] - m[0] * m[11] * m[14] - m[8] * m[2] * m[15] +
+           m[8] * m[3] * m[14] + m[12] * m[2] * m[11] - m[12] * m[3] * m[10];
+    a[9] = -m[0] * m[9] * m[15] + m[0] * m[11] * m[13] + m[8] * m[1] * m[15] -
+           m[8] * m[3] * m[13] - m[12] * m[1] * m[11] + m[12] * m[3] * m[9];
+    a[13] = m[0] * m[9] * m[14] - m[0] * m[10] * m[13] - m[8] * m[1] * m[14] +
+            m[8] * m[2] * m[13] + m[12] * m[1] * m[10] - m[12] * m[2] * m[9];
+    a[2] = m[1] * m[6] * m[15] - m[1] * m[7] * m[14] - m[5] * m[2] * m[15] +
+           m[5] * m[3] * m[14] + m[13] * m[2] * m[7] - m[13] * m[3] * m[6];
+    a[6] = -m[0] * m[6] * m[15] + m[0] * m[7] * m[14] + m[4] * m[2] * m[15] -
+           m[4] * m[3] * m[14] - m[12] * m[2] * m[7] + m[12] * m[3] * m[6];
+    a[10] = m[0] * m[5] * m[15] - m[0] * m[7] * m[13] - m[4] * m[1] * m[15] +
+            m[4] * m[3] * m[13] + m[12] * m[1] * m[7] - m[12] * m[3] * m[5];
+    a[14] = -m[0] * m[5] * m[14] + m[0] * m[6] * m[13] + m[4] * m[1] * m[14] -
+            m[4] * m[2] * m[13] - m[12] * m[1] * m[6] + m[12] * m[2] * m[5];
+    a[3] = -m[1] * m[6] * m[11] + m[1] * m[7] * m[10] + m[5] * m[2] * m[11] -
+           m[5] * m[3] * m[10] - m[9] * m[2] * m[7] + m[9] * m[3] * m[6];
+    a[7] = m[0] * m[6] * m[11] - m[0] * m[7] * m[10] - m[4] * m[2] * m[11] +
+           m[4] * m[3] * m[10] + m[8] * m[2] * m[7] - m[8] * m[3] * m[6];
+    a[11] = -m[0] * m[5] * m[11] + m[0] * m[7] * m[9] + m[4] * m[1] * m[11] -
+            m[4] * m[3] * m[9] - m[8] * m[1] * m[7] + m[8] * m[3] * m[5];
+    a[15] = m[0] * m[5] * m[10] - m[0] * m[6] * m[9] - m[4] * m[1] * m[10] +
+            m[4] * m[2] * m[9] + m[8] * m[1] * m[6] - m[8] * m[2] * m[5];
+    const double det = m[0] * a[0] + m[1] * a[4] + m[2] * a[8] + m[3] * a[12];
+    if (det == 0.0) return false;
+    const double id = 1.0 / det;
+    for (int i = 0; i < 16; ++i) inv[i] = a[i] * id;
+    return true;
+}
+
+// update_uniform_buffer (offscreen_pass.cpp:1152-1169): proj = perspectiveRH(fovy, W/H, n, f)
+// * coordinate_conversion; the kernel needs inverse(proj * view) (volume.vert:23 order).
+bool unprojection(const vr_camera *cam, uint32_t W, uint32_t H, double *inv)
+{
+    const float fovy = (cam->fovy_deg > 0.0f ? cam->fovy_deg : 40.0f) *
+                       0.01745329251994329576923690768489f;
+    const float zn = cam->znear > 0.0f ? cam->znear : 0.1f;
+    const float zf = cam->zfar > 0.0f ? cam->zfar : 10.0f;
+    const float aspect = (float)W / (float)H;
+    float persp[16], conv[16], proj[16], pv[16];
+    perspective_rh_no(fovy, aspect, zn, zf, persp);
+    coordinate_conversion(conv);
+    glm_mul(persp, conv, proj);
+    glm_mul(proj, cam->view, pv);
+    double pvd[16];
+    for (int i = 0; i < 16; ++i) pvd[i] = (double)pv[i];
+    return inverse4d(pvd, inv);
+}
+
+// R8G8B8A8_SRGB decode (offscreen_pass.cpp:1076): RGB sRGB->linear before filtering.
+float srgb_to_linear(uint32_t c8)
+{
+    const double c = (double)c8 / 255.0;
+    const double l = c <= 0.04045 ? c / 12.92 : std::pow((c + 0.055) / 1.055, 2.4);
+    return (float)l;
+}
+
+// splitmix64 -> uniform [0,1) floats (synthetic volume parameters; restated in
+// tests/vrtools.py for the generator test)
+struct SplitMix {
+    uint64_t s;
+    uint64_t next()
+    {
+        uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    }
+    float uniform() { return (float)(next() >> 40) * (1.0f / 16777216.0f); }
+};
+
+int set_bricks(vr_ctx *c, int storage, uint32_t nx, uint32_t ny, uint32_t nz, void **out)
+{
+    const size_t bytes = (size_t)bricks_for(nx) * bricks_for(ny) * bricks_for(nz) *
+                         kBrickVoxels * storage_size(storage);
+    if (c->bricks && c->brick_bytes == bytes) {
+        *out = c->bricks;
+        return VR_OK;
+    }
+    if (c->bricks) {
+        hipFree(c->bricks);
+        c->bricks = nullptr;
+        c->brick_bytes = 0;
+    }
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) return hip_fail(c, e, "hipMalloc(volume bricks)");
+    c->bricks = p;
+    c->brick_bytes = bytes;
+    *out = p;
+    return VR_OK;
+}
+
+int upload_tf(vr_ctx *c, const uint32_t *tf, uint32_t n)
+{
+    std::vector<float4> lut(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t t = tf[i];
+        lut[i] = make_float4(srgb_to_linear(t & 0xFFu), srgb_to_linear((t >> 8) & 0xFFu),
+                             srgb_to_linear((t >> 16) & 0xFFu),
+                             (float)((t >> 24) & 0xFFu) / 255.0f);
+    }
+    if (c->tf && c->tf_n != n) {
+        hipFree(c->tf);
+        c->tf = nullptr;
+    }
+    if (!c->tf) HIP_TRY(c, hipMalloc(&c->tf, n * sizeof(float4)), "hipMalloc(TF)");
+    HIP_TRY(c, hipMemcpy(c->tf, lut.data(), n * sizeof(float4), hipMemcpyHostToDevice),
+            "hipMemcpy(TF)");
+    c->tf_n = n;
+    return VR_OK;
+}
+
+int check_params(vr_ctx *c, const vr_params *p)
+{
+    if (!p) return fail(c, VR_EINVAL, "params is NULL");
+    if (!(p->step > 0.0f) || !std::isfinite(p->step))
+        return fail(c, VR_EINVAL, "params.step must be a positive finite float");
+    if (!(p->ray_dist >= 0.0f) || !std::isfinite(p->ray_dist))
+        return fail(c, VR_EINVAL, "params.ray_dist must be finite and >= 0");
+    if (p->spec_power < 0 || p->spec_power > 256)
+        return fail(c, VR_EINVAL, "params.spec_power must be in [0, 256]");
+    const float n = p->ray_dist / p->step;
+    if (n > 1.0e8f) return fail(c, VR_EINVAL, "params.ray_dist / step too large");
+    return VR_OK;
+}
+
+int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
+                 int out_format, uint32_t row_block, uint32_t rank, uint32_t nranks,
+                 MarchParams &P)
+{
+    if (!cam) return fail(c, VR_EINVAL, "camera is NULL");
+    int rc = check_params(c, p);
+    if (rc) return rc;
+    if (out_format != VR_OUT_RGBA8 && out_format != VR_OUT_RGBA32F)
+        return fail(c, VR_EINVAL, "unknown out_format");
+    if (nranks == 0 || rank >= nranks || row_block == 0)
+        return fail(c, VR_EINVAL, "bad shard (row_block, rank, nranks)");
+    std::memset(&P, 0, sizeof(P));
+    if (!unprojection(cam, c->width, c->height, P.inv))
+        return fail(c, VR_EINVAL, "proj * view is singular");
+    P.vol = c->bricks;
+    P.tf = c->tf;
+    P.out = out;
+    P.counters = c->counters;
+    P.fw = (double)c->width;
+    P.fh = (double)c->height;
+    P.nx = c->nx;
+    P.ny = c->ny;
+    P.nz = c->nz;
+    P.nbx = bricks_for(c->nx);
+    P.nby = bricks_for(c->ny);
+    P.fnx = (float)c->nx;
+    P.fny = (float)c->ny;
+    P.fnz = (float)c->nz;
+    P.vmin = c->vmin;
+    P.range = c->vmax - c->vmin;
+    P.tf_n = (int32_t)c->tf_n;
+    P.tf_nf = (float)c->tf_n;
+    for (int a = 0; a < 3; ++a) {
+        P.smin[a] = c->smin[a];
+        P.smax[a] = c->smax[a];
+        P.cam[a] = cam->position[a];
+    }
+    P.step = p->step;
+    P.nsteps = (int32_t)(p->ray_dist / p->step);  // volume.frag:31
+    P.ert_eps = p->ert_eps;
+    for (int k = 0; k < 4; ++k) P.clear[k] = p->clear_color[k];
+    P.ka = p->ambient;
+    P.kd = p->diffuse;
+    P.ks = p->specular;
+    P.spec_power = p->spec_power;
+    P.W = c->width;
+    P.H = c->height;
+    P.row_block = row_block;
+    P.rank = rank;
+    P.nranks = nranks;
+    P.local_rows = vr_shard_rows(c->height, row_block, nranks);
+    P.tiles_x = (c->width + 15) / 16;
+    P.tiles_y = (P.local_rows + 15) / 16;
+    P.out_format = out_format;
+    return VR_OK;
+}
+
+hipEvent_t pooled_event(vr_ctx *c)
+{
+    if (!c->ev_pool.empty()) {
+        hipEvent_t e = c->ev_pool.back();
+        c->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vr_abi_version(void) { return VR_ABI_VERSION; }
+
+void vr_params_default(vr_params *p)
+{
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->step = 0.005f;      // volume.frag:30
+    p->ray_dist = 1.8f;    // volume.frag:29
+    p->ert_eps = 0.0f;     // reference: no early-ray termination
+    p->shading = 0;        // reference: no shading
+    p->clear_color[0] = 0.11f;  // offscreen_pass.cpp:171
+    p->clear_color[1] = 0.11f;
+    p->clear_color[2] = 0.11f;
+    p->clear_color[3] = 1.0f;
+    p->ambient = 0.3f;
+    p->diffuse = 0.7f;
+    p->specular = 0.25f;
+    p->spec_power = 16;
+}
+
+const char *vr_last_error(const vr_ctx *ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+vr_ctx *vr_create(int device, uint32_t width, uint32_t height)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        fail(nullptr, VR_ENODEV, "no HIP device available");
+        return nullptr;
+    }
+    if (device < 0 || device >= ndev) {
+        fail(nullptr, VR_ENODEV, "device index out of range");
+        return nullptr;
+    }
+    if (width == 0 || height == 0) {
+        fail(nullptr, VR_EINVAL, "framebuffer size must be non-zero");
+        return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        fail(nullptr, VR_ENODEV, "hipSetDevice failed");
+        return nullptr;
+    }
+    vr_ctx *c = new (std::nothrow) vr_ctx();
+    if (!c) {
+        fail(nullptr, VR_ENOMEM, "out of host memory");
+        return nullptr;
+    }
+    c->device = device;
+    c->width = width;
+    c->height = height;
+    if (hipMalloc(&c->counters, 8 * sizeof(unsigned long long)) != hipSuccess) {
+        fail(nullptr, VR_ENOMEM, "hipMalloc(counters)");
+        delete c;
+        return nullptr;
+    }
+    // reference constructor placeholders (offscreen_pass.cpp:118-119)
+    const float zero = 0.0f;
+    const uint32_t white = 0xFFFFFFFFu;
+    if (vr_set_volume(c, &zero, VR_DTYPE_F32, 1, 1, 1, 0.0f, 1.0f) != VR_OK ||
+        vr_set_transfer_function(c, &white, 1) != VR_OK) {
+        g_err = c->err;
+        vr_destroy(c);
+        return nullptr;
+    }
+    return c;
+}
+
+void vr_destroy(vr_ctx *c)
+{
+    if (!c) return;
+    hipSetDevice(c->device);
+    hipDeviceSynchronize();
+    for (auto &pr : c->ev_pending) {
+        hipEventDestroy(pr.first);
+        hipEventDestroy(pr.second);
+    }
+    for (auto e : c->ev_pool) hipEventDestroy(e);
+    if (c->bricks) hipFree(c->bricks);
+    if (c->tf) hipFree(c->tf);
+    if (c->counters) hipFree(c->counters);
+    if (c->frame_dev) hipFree(c->frame_dev);
+    delete c;
+}
+
+int vr_resize(vr_ctx *c, uint32_t width, uint32_t height)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (width == 0 || height == 0) return VR_OK;  // offscreen_pass.cpp:237-239
+    c->width = width;
+    c->height = height;
+    return VR_OK;
+}
+
+int vr_get_size(const vr_ctx *c, uint32_t *w, uint32_t *h)
+{
+    if (!c || !w || !h) return fail(nullptr, VR_EINVAL, "NULL argument");
+    *w = c->width;
+    *h = c->height;
+    return VR_OK;
+}
+
+int vr_set_volume_device(vr_ctx *c, const void *data_dev, int dtype, uint32_t nx, uint32_t ny,
+                         uint32_t nz, float vmin, float vmax, void *stream)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (!data_dev) return fail(c, VR_EINVAL, "volume data is NULL");
+    const int st = storage_for(dtype);
+    if (st < 0) return fail(c, VR_EINVAL, "unsupported volume dtype");
+    if (nx == 0 || ny == 0 || nz == 0) return fail(c, VR_EINVAL, "volume dims must be non-zero");
+    if (nx > 65536 || ny > 65536 || nz > 65536) return fail(c, VR_EINVAL, "volume dim > 65536");
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    void *dst = nullptr;
+    int rc = set_bricks(c, st, nx, ny, nz, &dst);
+    if (rc) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    HIP_TRY(c, launch_brick_from_linear(dtype, data_dev, dst, nx, ny, nz, st, s), "brick kernel");
+    HIP_TRY(c, hipStreamSynchronize(s), "brick kernel sync");
+    c->storage = st;
+    c->nx = nx;
+    c->ny = ny;
+    c->nz = nz;
+    c->vmin = vmin;  // offscreen_pass.cpp:265-266
+    c->vmax = vmax;
+    return VR_OK;
+}
+
+int vr_set_volume(vr_ctx *c, const void *data, int dtype, uint32_t nx, uint32_t ny, uint32_t nz,
+                  float vmin, float vmax)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (!data) return fail(c, VR_EINVAL, "volume data is NULL");
+    if (storage_for(dtype) < 0) return fail(c, VR_EINVAL, "unsupported volume dtype");
+    if (nx == 0 || ny == 0 || nz == 0) return fail(c, VR_EINVAL, "volume dims must be non-zero");
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    const size_t bytes = (size_t)nx * ny * nz * dtype_size(dtype);
+    void *tmp = nullptr;
+    HIP_TRY(c, hipMalloc(&tmp, bytes), "hipMalloc(volume staging)");
+    hipError_t e = hipMemcpy(tmp, data, bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        hipFree(tmp);
+        return hip_fail(c, e, "hipMemcpy(volume)");
+    }
+    int rc = vr_set_volume_device(c, tmp, dtype, nx, ny, nz, vmin, vmax, nullptr);
+    hipFree(tmp);
+    return rc;
+}
+
+int vr_generate_volume(vr_ctx *c, int kind, int dtype, uint32_t nx, uint32_t ny, uint32_t nz,
+                       uint32_t seed, float *vmin_out, float *vmax_out)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (kind != 0) return fail(c, VR_EINVAL, "unknown synthetic volume kind");
+    int st;
+    float scale;
+    switch (dtype) {
+        case VR_DTYPE_U8: st = ST_U8; scale = 160.0f; break;
+        case VR_DTYPE_U16: st = ST_U16; scale = 40000.0f; break;
+        case VR_DTYPE_F32: st = ST_F32; scale = 1.0f; break;
+        default: return fail(c, VR_EINVAL, "generator supports u8, u16, f32");
+    }
+    if (nx == 0 || ny == 0 || nz == 0) return fail(c, VR_EINVAL, "volume dims must be non-zero");
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    const int ng = 32;
+    std::vector<float> prm(3 + 5 * ng);
+    prm[0] = (float)ng;
+    prm[1] = 0.05f;
+    prm[2] = scale;
+    SplitMix rng{(uint64_t)seed};
+    const float dims[3] = {(float)nx, (float)ny, (float)nz};
+    const float nmin = std::fmin(dims[0], std::fmin(dims[1], dims[2]));
+    for (int g = 0; g < ng; ++g) {
+        float *q = &prm[3 + 5 * g];
+        for (int a = 0; a < 3; ++a) q[a] = dims[a] * (0.15f + 0.7f * rng.uniform());
+        const float sigma = nmin * (0.04f + 0.10f * rng.uniform());
+        q[3] = 1.0f / (2.0f * sigma * sigma);
+        q[4] = 0.3f + 0.7f * rng.uniform();
+    }
+    float *prm_dev = nullptr;
+    HIP_TRY(c, hipMalloc(&prm_dev, prm.size() * sizeof(float) + 2 * sizeof(uint32_t)),
+            "hipMalloc(generator params)");
+    void *dst = nullptr;
+    int rc = set_bricks(c, st, nx, ny, nz, &dst);
+    if (rc) {
+        hipFree(prm_dev);
+        return rc;
+    }
+    uint32_t *mm = reinterpret_cast<uint32_t *>(prm_dev + prm.size());
+    const uint32_t mm_init[2] = {0xFFFFFFFFu, 0u};
+    hipError_t e = hipMemcpy(prm_dev, prm.data(), prm.size() * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(mm, mm_init, sizeof(mm_init), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_generate(kind, st, dst, nx, ny, nz, prm_dev, (int)prm.size(), nullptr);
+    if (e == hipSuccess) e = launch_minmax(st, dst, nx, ny, nz, reinterpret_cast<float *>(mm), nullptr);
+    uint32_t mm_host[2] = {0, 0};
+    if (e == hipSuccess) e = hipMemcpy(mm_host, mm, sizeof(mm_host), hipMemcpyDeviceToHost);
+    hipFree(prm_dev);
+    if (e != hipSuccess) return hip_fail(c, e, "generate volume");
+    auto unorder = [](uint32_t o) {
+        const uint32_t u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
+        float f;
+        std::memcpy(&f, &u, 4);
+        return f;
+    };
+    c->storage = st;
+    c->nx = nx;
+    c->ny = ny;
+    c->nz = nz;
+    c->vmin = unorder(mm_host[0]);
+    c->vmax = unorder(mm_host[1]);
+    if (vmin_out) *vmin_out = c->vmin;
+    if (vmax_out) *vmax_out = c->vmax;
+    return VR_OK;
+}
+
+uint64_t vr_volume_bytes(const vr_ctx *c) { return c ? (uint64_t)c->brick_bytes : 0; }
+
+int vr_debug_read_volume(vr_ctx *c, float *out)
+{
+    if (!c || !out) return fail(c, VR_EINVAL, "NULL argument");
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    std::vector<unsigned char> host(c->brick_bytes);
+    HIP_TRY(c, hipMemcpy(host.data(), c->bricks, c->brick_bytes, hipMemcpyDeviceToHost),
+            "hipMemcpy(bricks)");
+    const uint32_t nbx = bricks_for(c->nx), nby = bricks_for(c->ny);
+    const size_t es = storage_size(c->storage);
+    for (uint32_t z = 0; z < c->nz; ++z)
+        for (uint32_t y = 0; y < c->ny; ++y)
+            for (uint32_t x = 0; x < c->nx; ++x) {
+                const uint32_t pi = x + kPad, pj = y + kPad, pk = z + kPad;
+                const size_t b = ((size_t)(pk >> 4) * nby + (pj >> 4)) * nbx + (pi >> 4);
+                const size_t l = ((size_t)(pk & 15) * kStore + (pj & 15)) * kStore + (pi & 15);
+                const unsigned char *src = host.data() + (b * kBrickVoxels + l) * es;
+                float v;
+                switch (c->storage) {
+                    case ST_U8: v = (float)*(const uint8_t *)src; break;
+                    case ST_I8: v = (float)*(const int8_t *)src; break;
+                    case ST_U16: { uint16_t t; std::memcpy(&t, src, 2); v = (float)t; } break;
+                    case ST_I16: { int16_t t; std::memcpy(&t, src, 2); v = (float)t; } break;
+                    default: std::memcpy(&v, src, 4); break;
+                }
+                out[(size_t)x + (size_t)c->nx * ((size_t)y + (size_t)c->ny * z)] = v;
+            }
+    return VR_OK;
+}
+
+int vr_debug_volume_info(const vr_ctx *c, uint32_t dims[3], float minmax[2], int *storage)
+{
+    if (!c) return VR_EINVAL;
+    if (dims) {
+        dims[0] = c->nx;
+        dims[1] = c->ny;
+        dims[2] = c->nz;
+    }
+    if (minmax) {
+        minmax[0] = c->vmin;
+        minmax[1] = c->vmax;
+    }
+    if (storage) *storage = c->storage;
+    return VR_OK;
+}
+
+int vr_set_transfer_function(vr_ctx *c, const uint32_t *rgba8_srgb, uint32_t n)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (!rgba8_srgb || n == 0) return fail(c, VR_EINVAL, "transfer function is empty");
+    if (n > (1u << 20)) return fail(c, VR_EINVAL, "transfer function too large");
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    return upload_tf(c, rgba8_srgb, n);
+}
+
+int vr_set_slicing(vr_ctx *c, const float min_slice[3], const float max_slice[3])
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (!min_slice || !max_slice) return fail(c, VR_EINVAL, "slice bounds are NULL");
+    for (int a = 0; a < 3; ++a) {
+        c->smin[a] = min_slice[a];
+        c->smax[a] = max_slice[a];
+    }
+    return VR_OK;
+}
+
+uint32_t vr_shard_rows(uint32_t height, uint32_t row_block, uint32_t nranks)
+{
+    if (row_block == 0 || nranks == 0) return 0;
+    const uint32_t blocks = (height + row_block - 1) / row_block;
+    return ((blocks + nranks - 1) / nranks) * row_block;
+}
+
+int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out_dev,
+                     int out_format, uint32_t row_block, uint32_t rank, uint32_t nranks,
+                     void *stream)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (!out_dev) return fail(c, VR_EINVAL, "output buffer is NULL");
+    MarchParams P;
+    int rc = build_params(c, cam, p, out_dev, out_format, row_block, rank, nranks, P);
+    if (rc) return rc;
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->timing) {
+        e0 = pooled_event(c);
+        e1 = pooled_event(c);
+        if (!e0 || !e1) return fail(c, VR_EIO, "hipEventCreate failed");
+        HIP_TRY(c, hipEventRecord(e0, s), "hipEventRecord");
+    }
+    HIP_TRY(c, launch_march(c->storage, p->shading != 0, false, P, s), "march kernel launch");
+    if (c->timing) {
+        HIP_TRY(c, hipEventRecord(e1, s), "hipEventRecord");
+        c->ev_pending.emplace_back(e0, e1);
+    }
+    return VR_OK;
+}
+
+int vr_render(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out, int out_format)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (!out) return fail(c, VR_EINVAL, "output buffer is NULL");
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    const size_t bytes = (size_t)c->width * c->height * (out_format == VR_OUT_RGBA32F ? 16 : 4);
+    if (c->frame_bytes < bytes) {
+        if (c->frame_dev) hipFree(c->frame_dev);
+        c->frame_dev = nullptr;
+        c->frame_bytes = 0;
+        HIP_TRY(c, hipMalloc(&c->frame_dev, bytes), "hipMalloc(frame)");
+        c->frame_bytes = bytes;
+    }
+    int rc = vr_render_device(c, cam, p, c->frame_dev, out_format, 16, 0, 1, nullptr);
+    if (rc) return rc;
+    HIP_TRY(c, hipMemcpy(out, c->frame_dev, bytes, hipMemcpyDeviceToHost), "hipMemcpy(frame)");
+    return VR_OK;
+}
+
+int vr_assemble_rows(vr_ctx *c, const void *gathered_dev, void *out_dev, int out_format,
+                     uint32_t row_block, uint32_t nranks, void *stream)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (!gathered_dev || !out_dev) return fail(c, VR_EINVAL, "NULL buffer");
+    if (row_block == 0 || nranks == 0) return fail(c, VR_EINVAL, "bad shard");
+    if (out_format != VR_OUT_RGBA8 && out_format != VR_OUT_RGBA32F)
+        return fail(c, VR_EINVAL, "unknown out_format");
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    HIP_TRY(c, launch_assemble(gathered_dev, out_dev, out_format, c->width, c->height, row_block,
+                               nranks, vr_shard_rows(c->height, row_block, nranks),
+                               static_cast<hipStream_t>(stream)),
+            "assemble kernel");
+    return VR_OK;
+}
+
+int vr_count_work(vr_ctx *c, const vr_camera *cam, const vr_params *p, uint32_t row_block,
+                  uint32_t rank, uint32_t nranks, vr_stats *out)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (!out) return fail(c, VR_EINVAL, "stats is NULL");
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    const size_t bytes = (size_t)c->width * vr_shard_rows(c->height, row_block ? row_block : 1,
+                                                          nranks ? nranks : 1) * 4;
+    if (c->frame_bytes < bytes) {
+        if (c->frame_dev) hipFree(c->frame_dev);
+        c->frame_dev = nullptr;
+        c->frame_bytes = 0;
+        HIP_TRY(c, hipMalloc(&c->frame_dev, bytes), "hipMalloc(frame)");
+        c->frame_bytes = bytes;
+    }
+    MarchParams P;
+    int rc = build_params(c, cam, p, c->frame_dev, VR_OUT_RGBA8, row_block, rank, nranks, P);
+    if (rc) return rc;
+    HIP_TRY(c, hipMemset(c->counters, 0, 8 * sizeof(unsigned long long)), "hipMemset(counters)");
+    HIP_TRY(c, launch_march(c->storage, p->shading != 0, true, P, nullptr), "march (count) launch");
+    unsigned long long h[4];
+    HIP_TRY(c, hipMemcpy(h, c->counters, sizeof(h), hipMemcpyDeviceToHost), "hipMemcpy(counters)");
+    out->rays = h[0];
+    out->samples = h[1];
+    out->shaded_samples = h[2];
+    out->steps = h[3];
+    return VR_OK;
+}
+
+int vr_timing_enable(vr_ctx *c, int enable)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    c->timing = enable != 0;
+    return VR_OK;
+}
+
+int vr_timing_read(vr_ctx *c, double *total_ms, uint64_t *launches)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    for (auto &pr : c->ev_pending) {
+        HIP_TRY(c, hipEventSynchronize(pr.second), "hipEventSynchronize");
+        float ms = 0.0f;
+        HIP_TRY(c, hipEventElapsedTime(&ms, pr.first, pr.second), "hipEventElapsedTime");
+        c->timed_ms += ms;
+        c->timed_launches++;
+        c->ev_pool.push_back(pr.first);
+        c->ev_pool.push_back(pr.second);
+    }
+    c->ev_pending.clear();
+    if (total_ms) *total_ms = c->timed_ms;
+    if (launches) *launches = c->timed_launches;
+    return VR_OK;
+}
+
+int vr_timing_reset(vr_ctx *c)
+{
+    double ms;
+    uint64_t n;
+    int rc = vr_timing_read(c, &ms, &n);
+    if (rc) return rc;
+    c->timed_ms = 0.0;
+    c->timed_launches = 0;
+    return VR_OK;
+}
+
+const char *vr_kernel_name(const vr_ctx *c, const vr_params *p)
+{
+    if (!c) return "";
+    return march_kernel_name(c->storage, p && p->shading != 0, false);
+}
+
+}  // extern "C"

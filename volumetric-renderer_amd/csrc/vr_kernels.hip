@@ -1,0 +1,552 @@
+// vr_kernels.hip — gfx950 (CDNA4) kernels of the volume ray-marcher.
+//
+// The hot path is march_kernel: one lane per pixel, a 64-lane wavefront marches an 8x8
+// pixel tile (ray coherence), a 256-thread workgroup a 16x16 tile.  It restates the
+// reference fragment shader res/shaders/volume.frag:21-52 plus the Vulkan fixed-function
+// state it runs under (src/rendering/offscreen_pass.cpp: cube ray entry :55-90 + cull
+// :680-681 + depth clip :701-712, border trilinear sampler :1014-1039, sRGB TF sampler
+// :1076/:1125-1150, blend :715-725 over the clear colour :170-173, UNORM8 store :293).
+//
+// Design points (DESIGN.md has the roofline discussion):
+//  * memory-bound gather, no MFMA: each density sample is a 2x2x2 trilinear footprint;
+//  * bricked native-dtype volume (vr_internal.h): one brick base address + 7 immediate
+//    offsets per sample, zero apron = CLAMP_TO_BORDER without bounds tests;
+//  * TF decoded to linear float4 once per frame on the host and staged in LDS;
+//  * XCD-aware tile order: workgroups that share an XCD's L2 get a contiguous band of tiles,
+//    so the volume region behind that band stays in that L2;
+//  * fp contraction is OFF (pragma below + -ffp-contract=off): every fused multiply-add is
+//    an explicit fmaf(), matching the CPU oracle's operation order bit for bit.
+#include "vr_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace vr {
+namespace {
+
+constexpr int kTile = 16;       // pixels per workgroup side
+constexpr int kThreads = 256;   // 4 waves, each an 8x8 pixel sub-tile
+constexpr int kTfLds = 256;     // TF texels staged in LDS
+
+__device__ __forceinline__ float lerpf(float a, float b, float w) { return fmaf(w, b - a, a); }
+
+// 64-bit element offset (brick index * 4913 exceeds 2^32 for 2048^3 volumes) of padded cell (pi, pj, pk) in the bricked layout.
+__device__ __forceinline__ size_t cell_offset(int pi, int pj, int pk, uint32_t nbx, uint32_t nby)
+{
+    const uint32_t b = ((uint32_t)(pk >> 4) * nby + (uint32_t)(pj >> 4)) * nbx + (uint32_t)(pi >> 4);
+    const uint32_t l = ((uint32_t)(pk & 15) * kStore + (uint32_t)(pj & 15)) * kStore + (uint32_t)(pi & 15);
+    return (size_t)b * (size_t)kBrickVoxels + l;
+}
+
+// Trilinear filter of the 2x2x2 cell at p: lerp x, then y, then z (oracle tri_cell order).
+template <typename VT>
+__device__ __forceinline__ float cell(const VT *__restrict__ p, float ax, float ay, float az)
+{
+    constexpr int S = kStore, S2 = kStore * kStore;
+    const float v000 = (float)p[0], v100 = (float)p[1];
+    const float v010 = (float)p[S], v110 = (float)p[S + 1];
+    const float v001 = (float)p[S2], v101 = (float)p[S2 + 1];
+    const float v011 = (float)p[S2 + S], v111 = (float)p[S2 + S + 1];
+    const float c00 = lerpf(v000, v100, ax);
+    const float c10 = lerpf(v010, v110, ax);
+    const float c01 = lerpf(v001, v101, ax);
+    const float c11 = lerpf(v011, v111, ax);
+    const float c0 = lerpf(c00, c10, ay);
+    const float c1 = lerpf(c01, c11, ay);
+    return lerpf(c0, c1, az);
+}
+
+__device__ __forceinline__ void texel_coord(float p, float n, int &i, float &a)
+{
+    const float u = p * n - 0.5f;
+    const float f = floorf(u);
+    a = u - f;
+    i = (int)f;
+}
+
+// Pixel-centre ray -> cube entry (front face inside the clip volume), as the oracle's
+// pixel_ray: unproject ndc z = 0 and z = 1 through inverse(proj*view) in double.
+__device__ __forceinline__ bool pixel_ray(const MarchParams &P, uint32_t px, uint32_t py,
+                                          float tex[3], float dir[3])
+{
+    const double *m = P.inv;
+    const double x = ((double)px + 0.5) / P.fw * 2.0 - 1.0;
+    const double y = ((double)py + 0.5) / P.fh * 2.0 - 1.0;
+    double h0[4], h1[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        h0[r] = m[0 * 4 + r] * x + m[1 * 4 + r] * y + m[3 * 4 + r];
+        h1[r] = h0[r] + m[2 * 4 + r];
+    }
+    double p0[3], d[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        p0[r] = h0[r] / h0[3];
+        d[r] = h1[r] / h1[3] - p0[r];
+    }
+    double te = -__builtin_inf(), tx = __builtin_inf();
+    int axis = 0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        double lo, hi;
+        if (d[a] == 0.0) {
+            if (p0[a] < -0.5 || p0[a] > 0.5) return false;
+            lo = -__builtin_inf();
+            hi = __builtin_inf();
+        } else {
+            const double t1 = (-0.5 - p0[a]) / d[a];
+            const double t2 = (0.5 - p0[a]) / d[a];
+            lo = t1 < t2 ? t1 : t2;
+            hi = t1 < t2 ? t2 : t1;
+        }
+        if (lo > te) {
+            te = lo;
+            axis = a;
+        }
+        if (hi < tx) tx = hi;
+    }
+    if (!(te < tx) || te < 0.0 || te > 1.0) return false;
+    float frag[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const double e = p0[a] + te * d[a];
+        frag[a] = (float)e;
+        tex[a] = (float)(e + 0.5);
+    }
+    // the entry face's coordinate is constant over the face (volume.vert:20, cube :55-90)
+    frag[axis] = d[axis] > 0.0 ? -0.5f : 0.5f;
+    tex[axis] = d[axis] > 0.0 ? 0.0f : 1.0f;
+    // volume.frag:23
+    const float vx = frag[0] - P.cam[0];
+    const float vy = frag[1] - P.cam[1];
+    const float vz = frag[2] - P.cam[2];
+    const float len = sqrtf(vx * vx + vy * vy + vz * vz);
+    dir[0] = vx / len;
+    dir[1] = vy / len;
+    dir[2] = vz / len;
+    return true;
+}
+
+__device__ __forceinline__ float4 tf_lookup(const float4 *lut, int n, float nf, float t)
+{
+    float u = t * nf - 0.5f;
+    u = fminf(fmaxf(u, -1.0f), nf);
+    const float f = floorf(u);
+    const float w = u - f;
+    int i0 = (int)f, i1 = i0 + 1;
+    i0 = i0 < 0 ? 0 : (i0 > n - 1 ? n - 1 : i0);
+    i1 = i1 < 0 ? 0 : (i1 > n - 1 ? n - 1 : i1);
+    const float4 a = lut[i0], b = lut[i1];
+    return make_float4(lerpf(a.x, b.x, w), lerpf(a.y, b.y, w), lerpf(a.z, b.z, w),
+                       lerpf(a.w, b.w, w));
+}
+
+__device__ __forceinline__ uint32_t unorm8(float x)
+{
+    const float v = fminf(fmaxf(x, 0.0f), 1.0f);
+    return (uint32_t)(v * 255.0f + 0.5f);
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <typename VT, bool SHADE, bool COUNT>
+__global__ __launch_bounds__(kThreads) void march_kernel(const MarchParams P)
+{
+    __shared__ float4 s_tf[kTfLds];
+    const int tid = threadIdx.x;
+    const bool tf_in_lds = P.tf_n <= kTfLds;
+    if (tf_in_lds)
+        for (int i = tid; i < P.tf_n; i += kThreads) s_tf[i] = P.tf[i];
+    __syncthreads();
+    const float4 *lut = tf_in_lds ? s_tf : P.tf;
+
+    // XCD-aware, bijective block -> tile remap (blocks b and b+8 share an XCD's L2: give
+    // each such group a contiguous band of tiles in raster order).
+    const uint32_t nwg = gridDim.x, b = blockIdx.x;
+    const uint32_t xcd = b & 7u, q = nwg >> 3, r = nwg & 7u;
+    const uint32_t t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    const uint32_t tile_x = t % P.tiles_x, tile_y = t / P.tiles_x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const uint32_t px = tile_x * kTile + (wave & 1) * 8 + (lane & 7);
+    const uint32_t ly = tile_y * kTile + (wave >> 1) * 8 + (lane >> 3);
+    bool active = px < P.W && ly < P.local_rows;
+    const uint32_t blk = ly / P.row_block;
+    const uint32_t gy = (blk * P.nranks + P.rank) * P.row_block + (ly - blk * P.row_block);
+    active = active && gy < P.H;
+
+    float tex[3] = {0.f, 0.f, 0.f}, dir[3] = {0.f, 0.f, 0.f};
+    const bool covered = active && pixel_ray(P, px, gy, tex, dir);
+
+    float T = 1.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f;
+    unsigned long long n_samples = 0, n_shaded = 0, n_steps = 0;
+    const VT *__restrict__ vol = static_cast<const VT *>(P.vol);
+    const int nsteps = covered ? P.nsteps : 0;
+    float p0 = tex[0], p1 = tex[1], p2 = tex[2];
+    const float d0 = dir[0], d1 = dir[1], d2 = dir[2];
+    for (int it = 0; it < nsteps; ++it) {
+        // volume.frag:34-37
+        if (p0 > 1.0f || p1 > 1.0f || p2 > 1.0f || p0 < 0.0f || p1 < 0.0f || p2 < 0.0f) break;
+        if (COUNT) ++n_steps;
+        // volume.frag:39-40 (strict)
+        if (p0 < P.smax[0] && p1 < P.smax[1] && p2 < P.smax[2] && p0 > P.smin[0] &&
+            p1 > P.smin[1] && p2 > P.smin[2]) {
+            int i, j, k;
+            float ax, ay, az;
+            texel_coord(p0, P.fnx, i, ax);
+            texel_coord(p1, P.fny, j, ay);
+            texel_coord(p2, P.fnz, k, az);
+            const int pi = i + kPad, pj = j + kPad, pk = k + kPad;
+            const float d = cell(vol + cell_offset(pi, pj, pk, P.nbx, P.nby), ax, ay, az);
+            const float tt = (d - P.vmin) / P.range;
+            float4 s = tf_lookup(lut, P.tf_n, P.tf_nf, tt);
+            if (COUNT) ++n_samples;
+            if (SHADE && s.w > 0.0f) {
+                const float gx = cell(vol + cell_offset(pi + 1, pj, pk, P.nbx, P.nby), ax, ay, az) -
+                                 cell(vol + cell_offset(pi - 1, pj, pk, P.nbx, P.nby), ax, ay, az);
+                const float gy_ = cell(vol + cell_offset(pi, pj + 1, pk, P.nbx, P.nby), ax, ay, az) -
+                                  cell(vol + cell_offset(pi, pj - 1, pk, P.nbx, P.nby), ax, ay, az);
+                const float gz = cell(vol + cell_offset(pi, pj, pk + 1, P.nbx, P.nby), ax, ay, az) -
+                                 cell(vol + cell_offset(pi, pj, pk - 1, P.nbx, P.nby), ax, ay, az);
+                if (COUNT) ++n_shaded;
+                const float wx = gx * P.fnx, wy = gy_ * P.fny, wz = gz * P.fnz;
+                const float g2 = wx * wx + wy * wy + wz * wz;
+                if (g2 > 0.0f) {
+                    const float inv = 1.0f / sqrtf(g2);
+                    const float ndl = fabsf((wx * d0 + wy * d1 + wz * d2) * inv);
+                    const float kdiff = P.ka + P.kd * ndl;
+                    float sp = 1.0f;
+                    for (int e = 0; e < P.spec_power; ++e) sp = sp * ndl;
+                    const float spec = P.ks * sp;
+                    s.x = s.x * kdiff + spec;
+                    s.y = s.y * kdiff + spec;
+                    s.z = s.z * kdiff + spec;
+                }
+            }
+            // volume.frag:44-45
+            cr = cr + (s.x * s.w) * T;
+            cg = cg + (s.y * s.w) * T;
+            cb = cb + (s.z * s.w) * T;
+            T = T * (1.0f - s.w);
+            if (T == 0.0f) break;
+            if (T < P.ert_eps) break;
+        }
+        // volume.frag:47
+        p0 = p0 + d0 * P.step;
+        p1 = p1 + d1 * P.step;
+        p2 = p2 + d2 * P.step;
+    }
+
+    if (COUNT) {
+        const unsigned long long rays = wave_sum(covered ? 1ull : 0ull);
+        const unsigned long long sm = wave_sum(n_samples);
+        const unsigned long long sh = wave_sum(n_shaded);
+        const unsigned long long st = wave_sum(n_steps);
+        if (lane == 0) {
+            atomicAdd(&P.counters[0], rays);
+            atomicAdd(&P.counters[1], sm);
+            atomicAdd(&P.counters[2], sh);
+            atomicAdd(&P.counters[3], st);
+        }
+    }
+    if (!active) return;
+
+    // volume.frag:50 + blend (offscreen_pass.cpp:715-725); uncovered: T = 1, C = 0 -> clear
+    const float A = 1.0f - T;
+    const float omA = 1.0f - A;
+    const float o0 = cr * A + P.clear[0] * omA;
+    const float o1 = cg * A + P.clear[1] * omA;
+    const float o2 = cb * A + P.clear[2] * omA;
+    const float o3 = A * A + P.clear[3] * omA;
+    const size_t idx = (size_t)ly * P.W + px;
+    if (P.out_format == 0) {
+        static_cast<uint32_t *>(P.out)[idx] =
+            unorm8(o0) | (unorm8(o1) << 8) | (unorm8(o2) << 16) | (unorm8(o3) << 24);
+    } else {
+        static_cast<float4 *>(P.out)[idx] = make_float4(o0, o1, o2, o3);
+    }
+}
+
+// ---- volume ingest: linear (any NRRD element type) -> bricked storage ----------------------
+
+template <typename SrcT, typename DstT>
+__global__ __launch_bounds__(256) void brick_kernel(const SrcT *__restrict__ src,
+                                                    DstT *__restrict__ dst, uint32_t nx,
+                                                    uint32_t ny, uint32_t nz, uint32_t nbx,
+                                                    uint32_t nby, size_t total)
+{
+    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+         g += (size_t)gridDim.x * blockDim.x) {
+        const size_t bidx = g / kBrickVoxels;
+        const uint32_t l = (uint32_t)(g - bidx * kBrickVoxels);
+        const uint32_t lx = l % kStore, lyz = l / kStore, lyy = lyz % kStore, lz = lyz / kStore;
+        const uint32_t bx = (uint32_t)(bidx % nbx), byz = (uint32_t)(bidx / nbx);
+        const uint32_t by = byz % nby, bz = byz / nby;
+        const long x = (long)bx * kBrick + lx - kPad;
+        const long y = (long)by * kBrick + lyy - kPad;
+        const long z = (long)bz * kBrick + lz - kPad;
+        DstT v = (DstT)0;
+        if (x >= 0 && y >= 0 && z >= 0 && x < (long)nx && y < (long)ny && z < (long)nz)
+            v = (DstT)src[(size_t)x + (size_t)nx * ((size_t)y + (size_t)ny * (size_t)z)];
+        dst[g] = v;
+    }
+}
+
+// ---- synthetic volumes generated in place (multi-GiB configs) ------------------------------
+
+__device__ __forceinline__ float hash01(uint32_t x, uint32_t y, uint32_t z)
+{
+    uint32_t h = (x * 73856093u) ^ (y * 19349663u) ^ (z * 83492791u);
+    h ^= h >> 13;
+    h *= 0x5bd1e995u;
+    h ^= h >> 15;
+    return (float)(h & 0xFFFFFFu) * (1.0f / 16777216.0f);
+}
+
+template <typename DstT>
+__device__ __forceinline__ DstT to_storage(float v)
+{
+    if constexpr (sizeof(DstT) == 4) {
+        return v;
+    } else {
+        constexpr float lo = (DstT)(-1) < (DstT)0 ? (sizeof(DstT) == 1 ? -128.f : -32768.f) : 0.f;
+        constexpr float hi = (DstT)(-1) < (DstT)0 ? (sizeof(DstT) == 1 ? 127.f : 32767.f)
+                                                  : (sizeof(DstT) == 1 ? 255.f : 65535.f);
+        return (DstT)fminf(fmaxf(rintf(v), lo), hi);
+    }
+}
+
+// params: [ng, noise_amp, out_scale, ng * (cx, cy, cz, k, amp)] in voxel units;
+// value = out_scale * (sum_g amp exp(-k |x - c|^2) + noise_amp * hash01(x,y,z)).
+template <typename DstT>
+__global__ __launch_bounds__(256) void generate_kernel(DstT *__restrict__ dst, uint32_t nx,
+                                                       uint32_t ny, uint32_t nz, uint32_t nbx,
+                                                       uint32_t nby, size_t total,
+                                                       const float *__restrict__ prm)
+{
+    const int ng = (int)prm[0];
+    const float noise = prm[1], scale = prm[2];
+    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+         g += (size_t)gridDim.x * blockDim.x) {
+        const size_t bidx = g / kBrickVoxels;
+        const uint32_t l = (uint32_t)(g - bidx * kBrickVoxels);
+        const uint32_t lx = l % kStore, lyz = l / kStore, lyy = lyz % kStore, lz = lyz / kStore;
+        const uint32_t bx = (uint32_t)(bidx % nbx), byz = (uint32_t)(bidx / nbx);
+        const uint32_t by = byz % nby, bz = byz / nby;
+        const long x = (long)bx * kBrick + lx - kPad;
+        const long y = (long)by * kBrick + lyy - kPad;
+        const long z = (long)bz * kBrick + lz - kPad;
+        DstT v = (DstT)0;
+        if (x >= 0 && y >= 0 && z >= 0 && x < (long)nx && y < (long)ny && z < (long)nz) {
+            const float fx = (float)x, fy = (float)y, fz = (float)z;
+            float acc = 0.0f;
+            for (int q = 0; q < ng; ++q) {
+                const float *c = prm + 3 + 5 * q;
+                const float dx = fx - c[0], dy = fy - c[1], dz = fz - c[2];
+                acc += c[4] * __expf(-c[3] * (dx * dx + dy * dy + dz * dz));
+            }
+            acc += noise * hash01((uint32_t)x, (uint32_t)y, (uint32_t)z);
+            v = to_storage<DstT>(acc * scale);
+        }
+        dst[g] = v;
+    }
+}
+
+// ---- min/max over logical voxels (generated volumes) ----------------------------------------
+
+__device__ __forceinline__ uint32_t ordered(float f)
+{
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+template <typename VT>
+__global__ __launch_bounds__(256) void minmax_kernel(const VT *__restrict__ vol, uint32_t nx,
+                                                     uint32_t ny, uint32_t nz, uint32_t nbx,
+                                                     uint32_t nby, uint32_t *out)
+{
+    const size_t total = (size_t)nx * ny * nz;
+    uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+         g += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t x = (uint32_t)(g % nx);
+        const size_t yz = g / nx;
+        const uint32_t y = (uint32_t)(yz % ny), z = (uint32_t)(yz / ny);
+        const float v = (float)vol[cell_offset((int)x + kPad, (int)y + kPad, (int)z + kPad, nbx, nby)];
+        const uint32_t o = ordered(v);
+        lo = o < lo ? o : lo;
+        hi = o > hi ? o : hi;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t l2 = __shfl_xor(lo, off, 64), h2 = __shfl_xor(hi, off, 64);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&out[0], lo);
+        atomicMax(&out[1], hi);
+    }
+}
+
+// ---- rank-0 framebuffer assembly after the RCCL gather ---------------------------------------
+
+template <typename PixT>
+__global__ __launch_bounds__(256) void assemble_kernel(const PixT *__restrict__ gathered,
+                                                       PixT *__restrict__ out, uint32_t W,
+                                                       uint32_t H, uint32_t rb, uint32_t nranks,
+                                                       uint32_t shard_rows)
+{
+    const size_t total = (size_t)W * H;
+    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+         g += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t y = (uint32_t)(g / W), x = (uint32_t)(g - (size_t)y * W);
+        const uint32_t blk = y / rb;
+        const uint32_t rank = blk % nranks, lb = blk / nranks;
+        const uint32_t ly = lb * rb + (y - blk * rb);
+        out[g] = gathered[((size_t)rank * shard_rows + ly) * W + x];
+    }
+}
+
+template <typename VT, bool SHADE, bool COUNT>
+hipError_t launch_march_t(const MarchParams &p, hipStream_t stream)
+{
+    const uint32_t nblocks = p.tiles_x * p.tiles_y;
+    if (nblocks == 0) return hipSuccess;
+    hipLaunchKernelGGL((march_kernel<VT, SHADE, COUNT>), dim3(nblocks), dim3(kThreads), 0,
+                       stream, p);
+    return hipGetLastError();
+}
+
+template <typename VT>
+hipError_t launch_march_vt(bool shade, bool count, const MarchParams &p, hipStream_t s)
+{
+    if (shade) return count ? launch_march_t<VT, true, true>(p, s) : launch_march_t<VT, true, false>(p, s);
+    return count ? launch_march_t<VT, false, true>(p, s) : launch_march_t<VT, false, false>(p, s);
+}
+
+inline unsigned grid_for(size_t total)
+{
+    size_t g = (total + 255) / 256;
+    return (unsigned)(g > 2048 * 8 ? 2048 * 8 : (g == 0 ? 1 : g));
+}
+
+template <typename SrcT>
+hipError_t brick_from(const void *src, void *dst, uint32_t nx, uint32_t ny, uint32_t nz,
+                      int storage, hipStream_t s)
+{
+    const uint32_t nbx = bricks_for(nx), nby = bricks_for(ny), nbz = bricks_for(nz);
+    const size_t total = (size_t)nbx * nby * nbz * kBrickVoxels;
+    const SrcT *sp = static_cast<const SrcT *>(src);
+    switch (storage) {
+        case ST_U8: hipLaunchKernelGGL((brick_kernel<SrcT, uint8_t>), dim3(grid_for(total)), dim3(256), 0, s, sp, (uint8_t *)dst, nx, ny, nz, nbx, nby, total); break;
+        case ST_I8: hipLaunchKernelGGL((brick_kernel<SrcT, int8_t>), dim3(grid_for(total)), dim3(256), 0, s, sp, (int8_t *)dst, nx, ny, nz, nbx, nby, total); break;
+        case ST_U16: hipLaunchKernelGGL((brick_kernel<SrcT, uint16_t>), dim3(grid_for(total)), dim3(256), 0, s, sp, (uint16_t *)dst, nx, ny, nz, nbx, nby, total); break;
+        case ST_I16: hipLaunchKernelGGL((brick_kernel<SrcT, int16_t>), dim3(grid_for(total)), dim3(256), 0, s, sp, (int16_t *)dst, nx, ny, nz, nbx, nby, total); break;
+        default: hipLaunchKernelGGL((brick_kernel<SrcT, float>), dim3(grid_for(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &p,
+                        hipStream_t stream)
+{
+    switch (storage) {
+        case ST_U8: return launch_march_vt<uint8_t>(shade, count, p, stream);
+        case ST_I8: return launch_march_vt<int8_t>(shade, count, p, stream);
+        case ST_U16: return launch_march_vt<uint16_t>(shade, count, p, stream);
+        case ST_I16: return launch_march_vt<int16_t>(shade, count, p, stream);
+        case ST_F32: return launch_march_vt<float>(shade, count, p, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+const char *march_kernel_name(int storage, bool shade, bool count)
+{
+    static const char *names[5][2][2] = {
+        {{"march_kernel<unsigned char, false, false>", "march_kernel<unsigned char, false, true>"},
+         {"march_kernel<unsigned char, true, false>", "march_kernel<unsigned char, true, true>"}},
+        {{"march_kernel<signed char, false, false>", "march_kernel<signed char, false, true>"},
+         {"march_kernel<signed char, true, false>", "march_kernel<signed char, true, true>"}},
+        {{"march_kernel<unsigned short, false, false>", "march_kernel<unsigned short, false, true>"},
+         {"march_kernel<unsigned short, true, false>", "march_kernel<unsigned short, true, true>"}},
+        {{"march_kernel<short, false, false>", "march_kernel<short, false, true>"},
+         {"march_kernel<short, true, false>", "march_kernel<short, true, true>"}},
+        {{"march_kernel<float, false, false>", "march_kernel<float, false, true>"},
+         {"march_kernel<float, true, false>", "march_kernel<float, true, true>"}},
+    };
+    if (storage < 0 || storage > 4) return "march_kernel<?>";
+    return names[storage][shade ? 1 : 0][count ? 1 : 0];
+}
+
+hipError_t launch_brick_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,
+                                    uint32_t ny, uint32_t nz, int storage, hipStream_t s)
+{
+    switch (src_dtype) {  // enum vr_dtype
+        case 1: return brick_from<int8_t>(src, dst, nx, ny, nz, storage, s);
+        case 2: return brick_from<uint8_t>(src, dst, nx, ny, nz, storage, s);
+        case 3: return brick_from<int16_t>(src, dst, nx, ny, nz, storage, s);
+        case 4: return brick_from<uint16_t>(src, dst, nx, ny, nz, storage, s);
+        case 5: return brick_from<int32_t>(src, dst, nx, ny, nz, storage, s);
+        case 6: return brick_from<uint32_t>(src, dst, nx, ny, nz, storage, s);
+        case 7: return brick_from<int64_t>(src, dst, nx, ny, nz, storage, s);
+        case 8: return brick_from<uint64_t>(src, dst, nx, ny, nz, storage, s);
+        case 9: return brick_from<float>(src, dst, nx, ny, nz, storage, s);
+        case 10: return brick_from<double>(src, dst, nx, ny, nz, storage, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_generate(int kind, int storage, void *dst, uint32_t nx, uint32_t ny,
+                           uint32_t nz, const float *params_dev, int nparams, hipStream_t s)
+{
+    (void)nparams;
+    if (kind != 0) return hipErrorInvalidValue;
+    const uint32_t nbx = bricks_for(nx), nby = bricks_for(ny), nbz = bricks_for(nz);
+    const size_t total = (size_t)nbx * nby * nbz * kBrickVoxels;
+    switch (storage) {
+        case ST_U8: hipLaunchKernelGGL((generate_kernel<uint8_t>), dim3(grid_for(total)), dim3(256), 0, s, (uint8_t *)dst, nx, ny, nz, nbx, nby, total, params_dev); break;
+        case ST_U16: hipLaunchKernelGGL((generate_kernel<uint16_t>), dim3(grid_for(total)), dim3(256), 0, s, (uint16_t *)dst, nx, ny, nz, nbx, nby, total, params_dev); break;
+        case ST_F32: hipLaunchKernelGGL((generate_kernel<float>), dim3(grid_for(total)), dim3(256), 0, s, (float *)dst, nx, ny, nz, nbx, nby, total, params_dev); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_minmax(int storage, const void *bricks, uint32_t nx, uint32_t ny, uint32_t nz,
+                         float *minmax_dev, hipStream_t s)
+{
+    uint32_t *o = reinterpret_cast<uint32_t *>(minmax_dev);
+    const uint32_t nbx = bricks_for(nx), nby = bricks_for(ny);
+    const size_t total = (size_t)nx * ny * nz;
+    const unsigned g = grid_for(total);
+    switch (storage) {
+        case ST_U8: hipLaunchKernelGGL((minmax_kernel<uint8_t>), dim3(g), dim3(256), 0, s, (const uint8_t *)bricks, nx, ny, nz, nbx, nby, o); break;
+        case ST_I8: hipLaunchKernelGGL((minmax_kernel<int8_t>), dim3(g), dim3(256), 0, s, (const int8_t *)bricks, nx, ny, nz, nbx, nby, o); break;
+        case ST_U16: hipLaunchKernelGGL((minmax_kernel<uint16_t>), dim3(g), dim3(256), 0, s, (const uint16_t *)bricks, nx, ny, nz, nbx, nby, o); break;
+        case ST_I16: hipLaunchKernelGGL((minmax_kernel<int16_t>), dim3(g), dim3(256), 0, s, (const int16_t *)bricks, nx, ny, nz, nbx, nby, o); break;
+        default: hipLaunchKernelGGL((minmax_kernel<float>), dim3(g), dim3(256), 0, s, (const float *)bricks, nx, ny, nz, nbx, nby, o); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_assemble(const void *gathered, void *out, int out_format, uint32_t W,
+                           uint32_t H, uint32_t row_block, uint32_t nranks,
+                           uint32_t shard_rows, hipStream_t s)
+{
+    const unsigned g = grid_for((size_t)W * H);
+    if (out_format == 0)
+        hipLaunchKernelGGL((assemble_kernel<uint32_t>), dim3(g), dim3(256), 0, s,
+                           (const uint32_t *)gathered, (uint32_t *)out, W, H, row_block, nranks, shard_rows);
+    else
+        hipLaunchKernelGGL((assemble_kernel<float4>), dim3(g), dim3(256), 0, s,
+                           (const float4 *)gathered, (float4 *)out, W, H, row_block, nranks, shard_rows);
+    return hipGetLastError();
+}
+
+}  // namespace vr

@@ -1,0 +1,448 @@
+"""ctypes binding of the MI355X ray-marcher's C ABI (include/vr/vr.h, include/vr/vr_host.h).
+
+Python here is plumbing for tests and the benchmark; the product is lib/libvr_amd.so (HIP
+kernels for gfx950 + the C ABI).  The class `OffscreenPass` mirrors the reference's
+`Vol::Rendering::OffscreenPass` API (src/rendering/offscreen_pass.h:40-54): same method names,
+argument meaning and error behaviour (failures raise RuntimeError, as the reference throws
+std::runtime_error).  There is NO CPU fallback: if the shared library is missing this module
+raises at import-time use, and every render goes through the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libvr_amd.so")
+
+# enum vr_dtype
+DTYPE_I8, DTYPE_U8, DTYPE_I16, DTYPE_U16, DTYPE_I32, DTYPE_U32 = 1, 2, 3, 4, 5, 6
+DTYPE_I64, DTYPE_U64, DTYPE_F32, DTYPE_F64 = 7, 8, 9, 10
+NP_TO_DTYPE = {
+    np.dtype(np.int8): DTYPE_I8, np.dtype(np.uint8): DTYPE_U8,
+    np.dtype(np.int16): DTYPE_I16, np.dtype(np.uint16): DTYPE_U16,
+    np.dtype(np.int32): DTYPE_I32, np.dtype(np.uint32): DTYPE_U32,
+    np.dtype(np.int64): DTYPE_I64, np.dtype(np.uint64): DTYPE_U64,
+    np.dtype(np.float32): DTYPE_F32, np.dtype(np.float64): DTYPE_F64,
+}
+DTYPE_TO_NP = {v: k for k, v in NP_TO_DTYPE.items()}
+STORAGE_BYTES = {0: 1, 1: 1, 2: 2, 3: 2, 4: 4}  # vr::StorageType -> bytes per voxel
+
+OUT_RGBA8, OUT_RGBA32F = 0, 1
+
+
+class vr_camera(C.Structure):
+    _fields_ = [("view", C.c_float * 16), ("position", C.c_float * 3),
+                ("fovy_deg", C.c_float), ("znear", C.c_float), ("zfar", C.c_float)]
+
+
+class vr_params(C.Structure):
+    _fields_ = [("step", C.c_float), ("ray_dist", C.c_float), ("ert_eps", C.c_float),
+                ("shading", C.c_int32), ("clear_color", C.c_float * 4),
+                ("ambient", C.c_float), ("diffuse", C.c_float), ("specular", C.c_float),
+                ("spec_power", C.c_int32), ("reserved", C.c_int32 * 4)]
+
+
+class vr_stats(C.Structure):
+    _fields_ = [("rays", C.c_uint64), ("samples", C.c_uint64),
+                ("shaded_samples", C.c_uint64), ("steps", C.c_uint64)]
+
+
+class vr_orbit_camera(C.Structure):
+    _fields_ = [("center", C.c_float * 3), ("orientation", C.c_float * 4),
+                ("radius", C.c_float)]
+
+
+class vr_dataset(C.Structure):
+    _fields_ = [("dims", C.c_uint32 * 3), ("dtype", C.c_int), ("data", C.c_void_p),
+                ("vmin", C.c_float), ("vmax", C.c_float)]
+
+
+# Every entry point include/vr/vr.h and include/vr/vr_host.h declare (checked by the CPU tests).
+ABI_SYMBOLS = [
+    "vr_abi_version", "vr_params_default", "vr_create", "vr_destroy", "vr_last_error",
+    "vr_resize", "vr_get_size", "vr_set_volume", "vr_set_volume_device", "vr_generate_volume",
+    "vr_volume_bytes", "vr_debug_read_volume", "vr_debug_volume_info",
+    "vr_set_transfer_function", "vr_set_slicing", "vr_render", "vr_render_device",
+    "vr_shard_rows", "vr_assemble_rows", "vr_count_work", "vr_timing_enable",
+    "vr_timing_read", "vr_timing_reset", "vr_kernel_name",
+]
+HOST_SYMBOLS = [
+    "vr_cam_init", "vr_cam_rotate", "vr_cam_zoom", "vr_cam_position", "vr_cam_view",
+    "vr_cam_to_camera", "vr_gradient_create", "vr_gradient_destroy",
+    "vr_gradient_add_color_marker", "vr_gradient_add_alpha_marker",
+    "vr_gradient_remove_color_marker", "vr_gradient_remove_alpha_marker",
+    "vr_gradient_set_alpha_marker", "vr_gradient_set_color_marker", "vr_gradient_marker_count",
+    "vr_gradient_sample", "vr_gradient_discretize", "vr_nrrd_load", "vr_nrrd_write_raw",
+    "vr_csv_load", "vr_dataset_free", "vr_host_last_error",
+]
+
+_LIB = None
+
+
+def lib() -> C.CDLL:
+    """Load lib/libvr_amd.so (fails loudly: there is no fallback path)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C volumetric-renderer_amd` "
+                           "(or __graft_entry__.build()); there is no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    vp, u32, f32, i32 = C.c_void_p, C.c_uint32, C.c_float, C.c_int
+    sig = {
+        "vr_abi_version": (i32, []),
+        "vr_params_default": (None, [C.POINTER(vr_params)]),
+        "vr_create": (vp, [i32, u32, u32]),
+        "vr_destroy": (None, [vp]),
+        "vr_last_error": (C.c_char_p, [vp]),
+        "vr_resize": (i32, [vp, u32, u32]),
+        "vr_get_size": (i32, [vp, C.POINTER(u32), C.POINTER(u32)]),
+        "vr_set_volume": (i32, [vp, vp, i32, u32, u32, u32, f32, f32]),
+        "vr_set_volume_device": (i32, [vp, vp, i32, u32, u32, u32, f32, f32, vp]),
+        "vr_generate_volume": (i32, [vp, i32, i32, u32, u32, u32, u32, C.POINTER(f32), C.POINTER(f32)]),
+        "vr_volume_bytes": (C.c_uint64, [vp]),
+        "vr_debug_read_volume": (i32, [vp, vp]),
+        "vr_debug_volume_info": (i32, [vp, C.POINTER(u32), C.POINTER(f32), C.POINTER(i32)]),
+        "vr_set_transfer_function": (i32, [vp, C.POINTER(u32), u32]),
+        "vr_set_slicing": (i32, [vp, C.POINTER(f32), C.POINTER(f32)]),
+        "vr_render": (i32, [vp, C.POINTER(vr_camera), C.POINTER(vr_params), vp, i32]),
+        "vr_render_device": (i32, [vp, C.POINTER(vr_camera), C.POINTER(vr_params), vp, i32, u32, u32, u32, vp]),
+        "vr_shard_rows": (u32, [u32, u32, u32]),
+        "vr_assemble_rows": (i32, [vp, vp, vp, i32, u32, u32, vp]),
+        "vr_count_work": (i32, [vp, C.POINTER(vr_camera), C.POINTER(vr_params), u32, u32, u32, C.POINTER(vr_stats)]),
+        "vr_timing_enable": (i32, [vp, i32]),
+        "vr_timing_read": (i32, [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
+        "vr_timing_reset": (i32, [vp]),
+        "vr_kernel_name": (C.c_char_p, [vp, C.POINTER(vr_params)]),
+        "vr_cam_init": (None, [C.POINTER(vr_orbit_camera)]),
+        "vr_cam_rotate": (None, [C.POINTER(vr_orbit_camera), f32, f32]),
+        "vr_cam_zoom": (None, [C.POINTER(vr_orbit_camera), f32]),
+        "vr_cam_position": (None, [C.POINTER(vr_orbit_camera), C.POINTER(f32)]),
+        "vr_cam_view": (None, [C.POINTER(vr_orbit_camera), C.POINTER(f32)]),
+        "vr_cam_to_camera": (None, [C.POINTER(vr_orbit_camera), C.POINTER(vr_camera)]),
+        "vr_gradient_create": (vp, []),
+        "vr_gradient_destroy": (None, [vp]),
+        "vr_gradient_add_color_marker": (i32, [vp, f32, f32, f32, f32]),
+        "vr_gradient_add_alpha_marker": (i32, [vp, f32, f32]),
+        "vr_gradient_remove_color_marker": (i32, [vp, C.c_size_t]),
+        "vr_gradient_remove_alpha_marker": (i32, [vp, C.c_size_t]),
+        "vr_gradient_set_alpha_marker": (i32, [vp, C.c_size_t, f32, f32]),
+        "vr_gradient_set_color_marker": (i32, [vp, C.c_size_t, f32, f32, f32, f32]),
+        "vr_gradient_marker_count": (C.c_size_t, [vp, i32]),
+        "vr_gradient_sample": (None, [vp, f32, C.POINTER(f32)]),
+        "vr_gradient_discretize": (i32, [vp, C.c_size_t, C.POINTER(u32)]),
+        "vr_nrrd_load": (i32, [C.c_char_p, C.POINTER(vr_dataset)]),
+        "vr_nrrd_write_raw": (i32, [C.c_char_p, vp, i32, C.POINTER(u32)]),
+        "vr_csv_load": (i32, [C.POINTER(C.c_char_p), C.c_size_t, C.POINTER(vr_dataset)]),
+        "vr_dataset_free": (None, [C.POINTER(vr_dataset)]),
+        "vr_host_last_error": (C.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = L
+    return L
+
+
+def default_params(**overrides) -> vr_params:
+    p = vr_params()
+    lib().vr_params_default(C.byref(p))
+    for k, v in overrides.items():
+        if k == "clear_color":
+            for i in range(4):
+                p.clear_color[i] = v[i]
+        else:
+            setattr(p, k, v)
+    return p
+
+
+# --------------------------------------------------------------------------------------
+# Inputs that feed the pass (C++ restatements in host/vr_host.cpp)
+# --------------------------------------------------------------------------------------
+class OrbitCamera:
+    """Vol::Scene::Camera (src/scene/camera.cpp:7-48), via vr_cam_*."""
+
+    def __init__(self):
+        self._c = vr_orbit_camera()
+        lib().vr_cam_init(C.byref(self._c))
+
+    def rotate(self, dx: float, dy: float) -> "OrbitCamera":
+        lib().vr_cam_rotate(C.byref(self._c), dx, dy)
+        return self
+
+    def zoom(self, delta: float) -> "OrbitCamera":
+        lib().vr_cam_zoom(C.byref(self._c), delta)
+        return self
+
+    def set_radius(self, r: float) -> "OrbitCamera":
+        self._c.radius = r
+        return self
+
+    @property
+    def radius(self) -> float:
+        return float(self._c.radius)
+
+    def get_position(self) -> np.ndarray:
+        out = (C.c_float * 3)()
+        lib().vr_cam_position(C.byref(self._c), out)
+        return np.array(out[:], dtype=np.float32)
+
+    def get_view(self) -> np.ndarray:
+        out = (C.c_float * 16)()
+        lib().vr_cam_view(C.byref(self._c), out)
+        return np.array(out[:], dtype=np.float32)
+
+    def to_vr_camera(self) -> vr_camera:
+        cam = vr_camera()
+        lib().vr_cam_to_camera(C.byref(self._c), C.byref(cam))
+        return cam
+
+
+def make_camera(radius: float = 3.0, rotate=None) -> OrbitCamera:
+    cam = OrbitCamera()
+    if rotate is not None:
+        cam.rotate(float(rotate[0]), float(rotate[1]))
+    cam.set_radius(radius)
+    return cam
+
+
+class Gradient:
+    """Vol::UI::Components::Gradient (src/ui/components/gradient.cpp), via vr_gradient_*."""
+
+    def __init__(self):
+        self._g = lib().vr_gradient_create()
+
+    def __del__(self):
+        if getattr(self, "_g", None):
+            lib().vr_gradient_destroy(self._g)
+            self._g = None
+
+    def add_color_marker(self, loc, rgb) -> int:
+        return lib().vr_gradient_add_color_marker(self._g, loc, *[float(x) for x in rgb])
+
+    def add_alpha_marker(self, loc, a) -> int:
+        return lib().vr_gradient_add_alpha_marker(self._g, loc, float(a))
+
+    def remove_color_marker(self, i) -> bool:
+        return bool(lib().vr_gradient_remove_color_marker(self._g, i))
+
+    def remove_alpha_marker(self, i) -> bool:
+        return bool(lib().vr_gradient_remove_alpha_marker(self._g, i))
+
+    def set_alpha_marker(self, i, loc, a) -> int:
+        return lib().vr_gradient_set_alpha_marker(self._g, i, loc, float(a))
+
+    def set_color_marker(self, i, loc, rgb) -> int:
+        return lib().vr_gradient_set_color_marker(self._g, i, loc, *[float(x) for x in rgb])
+
+    def marker_count(self, alpha: bool) -> int:
+        return int(lib().vr_gradient_marker_count(self._g, 1 if alpha else 0))
+
+    def sample(self, loc) -> np.ndarray:
+        out = (C.c_float * 4)()
+        lib().vr_gradient_sample(self._g, loc, out)
+        return np.array(out[:], dtype=np.float32)
+
+    def discretize(self, count: int = 256) -> np.ndarray:
+        out = (C.c_uint32 * count)()
+        if lib().vr_gradient_discretize(self._g, count, out) != 0:
+            raise RuntimeError("discretize failed")
+        return np.array(out[:], dtype=np.uint32)
+
+
+@dataclass
+class Dataset:
+    """Vol::Data::Dataset (src/data/dataset.h:9-13), kept in the file's native dtype."""
+    dims: tuple
+    vmin: float
+    vmax: float
+    data: np.ndarray  # shape (nz, ny, nx), native dtype, x fastest
+
+
+def _take_dataset(ds: vr_dataset) -> Dataset:
+    dims = tuple(int(x) for x in ds.dims)
+    npdt = DTYPE_TO_NP[ds.dtype]
+    n = dims[0] * dims[1] * dims[2]
+    buf = (C.c_char * (n * npdt.itemsize)).from_address(ds.data)
+    arr = np.frombuffer(bytes(buf), dtype=npdt).reshape(dims[2], dims[1], dims[0]).copy()
+    out = Dataset(dims, float(ds.vmin), float(ds.vmax), arr)
+    lib().vr_dataset_free(C.byref(ds))
+    return out
+
+
+def load_nrrd(path: str) -> Dataset:
+    """NrrdFileParser::parse (nrrd_file_parser.cpp:21-47); raises RuntimeError like the reference."""
+    ds = vr_dataset()
+    rc = lib().vr_nrrd_load(path.encode(), C.byref(ds))
+    if rc != 0:
+        raise RuntimeError(lib().vr_host_last_error().decode())
+    return _take_dataset(ds)
+
+
+def load_csv(paths: Sequence[str]) -> Dataset:
+    """CsvFileParser::parse (csv_file_parser.cpp:14-50)."""
+    arr = (C.c_char_p * len(paths))(*[p.encode() for p in paths])
+    ds = vr_dataset()
+    rc = lib().vr_csv_load(arr, len(paths), C.byref(ds))
+    if rc != 0:
+        raise RuntimeError(lib().vr_host_last_error().decode())
+    return _take_dataset(ds)
+
+
+def write_nrrd_raw(nhdr_path: str, data: np.ndarray) -> None:
+    """Write data (nz, ny, nx) as a detached raw NRRD pair (nhdr + raw)."""
+    data = np.ascontiguousarray(data)
+    dims = (C.c_uint32 * 3)(data.shape[2], data.shape[1], data.shape[0])
+    rc = lib().vr_nrrd_write_raw(nhdr_path.encode(), data.ctypes.data, NP_TO_DTYPE[data.dtype], dims)
+    if rc != 0:
+        raise RuntimeError(lib().vr_host_last_error().decode())
+
+
+# --------------------------------------------------------------------------------------
+# The pass
+# --------------------------------------------------------------------------------------
+class OffscreenPass:
+    """Mirror of Vol::Rendering::OffscreenPass (offscreen_pass.h:40-54) over the C ABI."""
+
+    def __init__(self, width: int, height: int, device: int = 0):
+        L = lib()
+        self._ctx = L.vr_create(device, width, height)
+        if not self._ctx:
+            raise RuntimeError(f"vr_create failed: {L.vr_last_error(None).decode()}")
+
+    # -- lifecycle --
+    def close(self):
+        if getattr(self, "_ctx", None):
+            lib().vr_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed ({rc}): {lib().vr_last_error(self._ctx).decode()}")
+
+    @property
+    def size(self):
+        w, h = C.c_uint32(), C.c_uint32()
+        self._check(lib().vr_get_size(self._ctx, C.byref(w), C.byref(h)), "vr_get_size")
+        return int(w.value), int(h.value)
+
+    # -- reference setters --
+    def framebuffer_size_changed(self, width: int, height: int):
+        self._check(lib().vr_resize(self._ctx, width, height), "framebuffer_size_changed")
+
+    def volume_dataset_changed(self, dataset: Dataset):
+        data = np.ascontiguousarray(dataset.data)
+        nx, ny, nz = dataset.dims
+        assert data.size == nx * ny * nz, "dataset dims do not match data"
+        self._check(lib().vr_set_volume(self._ctx, data.ctypes.data, NP_TO_DTYPE[data.dtype],
+                                        nx, ny, nz, float(dataset.vmin), float(dataset.vmax)),
+                    "volume_dataset_changed")
+
+    def volume_dataset_changed_device(self, ptr: int, dtype, dims, vmin, vmax, stream: int = 0):
+        nx, ny, nz = dims
+        self._check(lib().vr_set_volume_device(self._ctx, C.c_void_p(ptr), NP_TO_DTYPE[np.dtype(dtype)],
+                                               nx, ny, nz, float(vmin), float(vmax),
+                                               C.c_void_p(stream or None)),
+                    "volume_dataset_changed(device)")
+
+    def generate_volume(self, dims, dtype=np.float32, seed: int = 2024, kind: int = 0):
+        lo, hi = C.c_float(), C.c_float()
+        self._check(lib().vr_generate_volume(self._ctx, kind, NP_TO_DTYPE[np.dtype(dtype)],
+                                             dims[0], dims[1], dims[2], seed,
+                                             C.byref(lo), C.byref(hi)), "vr_generate_volume")
+        return float(lo.value), float(hi.value)
+
+    def read_volume(self) -> np.ndarray:
+        dims, mm, st = self.volume_info()
+        out = np.empty((dims[2], dims[1], dims[0]), dtype=np.float32)
+        self._check(lib().vr_debug_read_volume(self._ctx, out.ctypes.data), "vr_debug_read_volume")
+        return out
+
+    def volume_info(self):
+        dims = (C.c_uint32 * 3)()
+        mm = (C.c_float * 2)()
+        st = C.c_int()
+        self._check(lib().vr_debug_volume_info(self._ctx, dims, mm, C.byref(st)), "vr_debug_volume_info")
+        return tuple(dims[:]), (float(mm[0]), float(mm[1])), int(st.value)
+
+    def volume_bytes(self) -> int:
+        return int(lib().vr_volume_bytes(self._ctx))
+
+    def slicing_changed(self, vmin, vmax):
+        a = (C.c_float * 3)(*[float(x) for x in vmin])
+        b = (C.c_float * 3)(*[float(x) for x in vmax])
+        self._check(lib().vr_set_slicing(self._ctx, a, b), "slicing_changed")
+
+    def transfer_function_changed(self, data):
+        arr = np.ascontiguousarray(np.asarray(data, dtype=np.uint32))
+        ptr = arr.ctypes.data_as(C.POINTER(C.c_uint32))
+        self._check(lib().vr_set_transfer_function(self._ctx, ptr, int(arr.size)),
+                    "transfer_function_changed")
+
+    # -- record/render --
+    def render(self, camera: OrbitCamera, params: Optional[vr_params] = None,
+               out_format: int = OUT_RGBA32F) -> np.ndarray:
+        """Synchronous full frame into host memory: (H, W, 4) float32 or uint8."""
+        w, h = self.size
+        p = params if params is not None else default_params()
+        cam = camera.to_vr_camera() if isinstance(camera, OrbitCamera) else camera
+        if out_format == OUT_RGBA32F:
+            out = np.empty((h, w, 4), dtype=np.float32)
+        else:
+            out = np.empty((h, w, 4), dtype=np.uint8)
+        self._check(lib().vr_render(self._ctx, C.byref(cam), C.byref(p), out.ctypes.data, out_format),
+                    "render")
+        return out
+
+    def render_device(self, camera, params, out_ptr: int, out_format: int = OUT_RGBA8,
+                      row_block: int = 16, rank: int = 0, nranks: int = 1, stream: int = 0):
+        cam = camera.to_vr_camera() if isinstance(camera, OrbitCamera) else camera
+        self._check(lib().vr_render_device(self._ctx, C.byref(cam), C.byref(params),
+                                           C.c_void_p(out_ptr), out_format, row_block, rank,
+                                           nranks, C.c_void_p(stream or None)), "render_device")
+
+    def assemble_rows(self, gathered_ptr: int, out_ptr: int, out_format: int, row_block: int,
+                      nranks: int, stream: int = 0):
+        self._check(lib().vr_assemble_rows(self._ctx, C.c_void_p(gathered_ptr), C.c_void_p(out_ptr),
+                                           out_format, row_block, nranks, C.c_void_p(stream or None)),
+                    "assemble_rows")
+
+    def count_work(self, camera, params, row_block=16, rank=0, nranks=1) -> dict:
+        cam = camera.to_vr_camera() if isinstance(camera, OrbitCamera) else camera
+        st = vr_stats()
+        self._check(lib().vr_count_work(self._ctx, C.byref(cam), C.byref(params), row_block, rank,
+                                        nranks, C.byref(st)), "count_work")
+        return dict(rays=st.rays, samples=st.samples, shaded_samples=st.shaded_samples, steps=st.steps)
+
+    def timing_enable(self, on: bool = True):
+        self._check(lib().vr_timing_enable(self._ctx, 1 if on else 0), "timing_enable")
+
+    def timing_read(self):
+        ms, n = C.c_double(), C.c_uint64()
+        self._check(lib().vr_timing_read(self._ctx, C.byref(ms), C.byref(n)), "timing_read")
+        return float(ms.value), int(n.value)
+
+    def timing_reset(self):
+        self._check(lib().vr_timing_reset(self._ctx), "timing_reset")
+
+    def kernel_name(self, params) -> str:
+        return lib().vr_kernel_name(self._ctx, C.byref(params)).decode()
+
+
+def shard_rows(height: int, row_block: int, nranks: int) -> int:
+    return int(lib().vr_shard_rows(height, row_block, nranks))
+
+
+def unorm8(img: np.ndarray) -> np.ndarray:
+    """Float RGBA -> R8G8B8A8_UNORM exactly as the kernel stores it: (u8)(clamp*255 + 0.5)."""
+    v = np.clip(np.nan_to_num(img.astype(np.float32), nan=0.0), np.float32(0), np.float32(1))
+    return np.floor(v * np.float32(255.0) + np.float32(0.5)).astype(np.uint8)
