@@ -1,0 +1,264 @@
+"""Benchmark of the MI355X ray-march (BASELINE.json metric: Gsamples/s + fps, 512^3 NRRD @ 1080p;
+achieved HBM GB/s vs peak).
+
+A step = one frame of the hot path: every rank ray-marches its row blocks of the 1920x1080
+frame (HIP kernel through the C ABI) and, for N > 1, the row shards are gathered to rank 0
+over RCCL (torch.distributed "nccl") and assembled there.  The volume is resident in HBM
+before timing starts (generated on device); timing brackets exactly K steps with a barrier +
+device synchronize on both sides and takes the max over ranks.
+
+Workload (configs[2] of BASELINE.json, the configuration the metric is quoted on):
+  512^3 f32 synthetic volume (sum of 32 Gaussians + 0.05 value noise, seed 2024),
+  1920x1080, camera r = 1.6 (frame-filling), TF-2 (demo ramp), gradient Phong shading +
+  early-ray termination (eps 1e-5).  The reference-semantics variant (no shading, no ERT) is
+  timed as well and reported under "variants".
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]; N > 1 under torch.distributed.run.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for sub in ("volumetric-renderer_amd", "tools", "oracle"):
+    sys.path.insert(0, os.path.join(ROOT, sub))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import vr_amd  # noqa: E402
+import synth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "Gsamples/sec + fps, 512³ NRRD @ 1080p; achieved HBM GB/s vs peak"
+
+CONFIGS = {
+    # name: volume dims, dtype, viewport, camera, tf, shading, ert
+    "c3": dict(dims=(512, 512, 512), dtype=np.float32, W=1920, H=1080, cam="fill", tf="tf2",
+               shading=1, ert=1e-5, seed=2024,
+               workload="C3: 512^3 f32 synthetic NRRD-equivalent volume, 1920x1080, "
+                        "gradient Phong + early-ray termination, camera r=1.6"),
+    "c3_ref": dict(dims=(512, 512, 512), dtype=np.float32, W=1920, H=1080, cam="fill", tf="tf2",
+                   shading=0, ert=0.0, seed=2024,
+                   workload="C3 reference semantics: no shading, no ERT (volume.frag as written)"),
+    "c2": dict(dims=(256, 256, 256), dtype=np.uint8, W=1024, H=1024, cam="fill", tf="tf2",
+               shading=0, ert=0.0, seed=1234, workload="C2: 256^3 u8, 1024x1024, trilinear + 1D TF"),
+    "c4": dict(dims=(1024, 1024, 1024), dtype=np.uint8, W=2048, H=2048, cam="fill", tf="tf2",
+               shading=0, ert=0.0, seed=7, workload="C4: 1024^3 u8, 2048x2048"),
+}
+
+
+def algorithmic_bytes(stats, voxel_bytes, pixels, out_bytes=4):
+    """8 x sizeof(voxel) per executed density sample, + 48 x sizeof(voxel) per
+    shaded sample (6 extra trilinear footprints), + 4 B per written pixel."""
+    return (stats["samples"] * 8 * voxel_bytes + stats["shaded_samples"] * 48 * voxel_bytes
+            + pixels * out_bytes)
+
+
+def setup_pass(cfg, device):
+    rp = vr_amd.OffscreenPass(cfg["W"], cfg["H"], device=device)
+    lo, hi = rp.generate_volume(cfg["dims"], cfg["dtype"], seed=cfg["seed"])
+    rp.transfer_function_changed(synth.TFS[cfg["tf"]]())
+    return rp
+
+
+def run_variant(rp, cfg, steps, warmup, rank, world, stream, row_block=16):
+    """Time `steps` frames; returns (max-over-ranks seconds, kernel ms avg, frame stats, rank0 stats)."""
+    W, H = cfg["W"], cfg["H"]
+    cam = synth.camera(cfg["cam"]).to_vr_camera()
+    p = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"])
+    sr = vr_amd.shard_rows(H, row_block, world)
+    local = torch.empty((sr, W), dtype=torch.int32, device="cuda")
+    gathered = frame = gbuf = None
+    if world > 1 and rank == 0:
+        # RCCL gathers straight into the rank-major buffer the assembly kernel reads
+        gbuf = torch.empty((world, sr, W), dtype=torch.int32, device="cuda")
+        gathered = [gbuf[r] for r in range(world)]
+        frame = torch.empty((H, W), dtype=torch.int32, device="cuda")
+
+    my_stats = rp.count_work(cam, p, row_block, rank, world)
+    tot = torch.tensor([my_stats[k] for k in ("rays", "samples", "shaded_samples", "steps")],
+                       dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    frame_stats = dict(zip(("rays", "samples", "shaded_samples", "steps"), [int(x) for x in tot.tolist()]))
+
+    def step():
+        rp.render_device(cam, p, local.data_ptr(), vr_amd.OUT_RGBA8, row_block, rank, world, stream)
+        if world > 1:
+            dist.gather(local, gathered if rank == 0 else None, dst=0)
+            if rank == 0:
+                rp.assemble_rows(gbuf.data_ptr(), frame.data_ptr(), vr_amd.OUT_RGBA8, row_block, world, stream)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    rp.timing_reset()
+    rp.timing_enable(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    rp.timing_enable(False)
+    kms, nl = rp.timing_read()
+    el = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    return float(el.item()), kms / max(nl, 1), frame_stats, my_stats, sr * W
+
+
+def cpu_baseline(rp, cfg, budget_s=12.0):
+    """The CPU oracle (oracle/oracle.c, OpenMP) on a bounded row sample of the same frame."""
+    import pyoracle
+    nthreads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    vol = rp.read_volume()
+    _, (vmin, vmax), _ = rp.volume_info()
+    cam = synth.camera(cfg["cam"]).to_vr_camera()
+    p = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"])
+    sc = pyoracle.Scene.from_params(vol, vmin, vmax, synth.TFS[cfg["tf"]](), cam, cfg["W"], cfg["H"], p)
+    H = cfg["H"]
+    buf = np.empty((H, cfg["W"], 4), np.float32)
+    # calibrate on rows spread over the frame, then size the sample to ~budget_s of CPU work
+    probe = list(range(H // 32, H, H // 16))
+    t0 = time.perf_counter()
+    sc.render_rows(probe, buf, nthreads)
+    per_row = (time.perf_counter() - t0) / len(probe)
+    nrows = int(max(16, min(H, budget_s / max(per_row, 1e-6))))
+    stride = max(1, H // nrows)
+    rows = list(range(stride // 2, H, stride))
+    # a whole frame can take well under a second on a many-core host: repeat the sample until
+    # ~budget_s of CPU work has been timed, so the rate is not a sub-second measurement
+    t, samples, reps = 0.0, 0, 0
+    while t < budget_s * 0.8 or reps == 0:
+        t0 = time.perf_counter()
+        _, st = sc.render_rows(rows, buf, nthreads)
+        t += time.perf_counter() - t0
+        samples += st["samples"]
+        reps += 1
+    return dict(value=round(samples / t / 1e9, 4), unit="Gsamples/s", cores=nthreads, kind="port",
+                sample=f"{len(rows)} of {H} frame rows (every {stride}th row) x {reps} repeats, same "
+                       f"volume/camera/TF/params; {samples} samples in {t:.2f} s (oracle/oracle.c, "
+                       f"OpenMP x{nthreads})")
+
+
+def load_traffic(cfg_name, world):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        e = d.get(cfg_name)
+        if e and int(e.get("n_gpus", 1)) == world:
+            return float(e["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-variants", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    cfg = CONFIGS[args.config]
+    rp = setup_pass(cfg, local_rank)
+    vbytes = np.dtype(cfg["dtype"]).itemsize
+
+    secs, kms, fstats, r0stats, shard_px = run_variant(rp, cfg, args.steps, args.warmup, rank, world, stream)
+    value = fstats["samples"] * args.steps / secs / 1e9
+    fps = args.steps / secs
+    achieved = algorithmic_bytes(r0stats, vbytes, shard_px) / (kms * 1e-3) / 1e9
+    traffic = load_traffic(args.config, world)
+
+    variants = {}
+    if not args.no_variants and args.config == "c3":
+        vcfg = CONFIGS["c3_ref"]
+        rp.transfer_function_changed(synth.TFS[vcfg["tf"]]())
+        s2, k2, f2, r2, _ = run_variant(rp, vcfg, args.steps, min(args.warmup, 5), rank, world, stream)
+        variants["reference_semantics_no_shading_no_ert"] = dict(
+            value=round(f2["samples"] * args.steps / s2 / 1e9, 3), unit="Gsamples/s",
+            fps=round(args.steps / s2, 2), samples_per_frame=f2["samples"],
+            kernel_ms=round(k2, 4),
+            roofline_frac=round(algorithmic_bytes(r2, vbytes, shard_px) / (k2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(rp, cfg, args.cpu_budget)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Gsamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(secs / args.steps * 1e3, 4),
+            "fps": round(fps, 2),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (generated on device; no dataset download)",
+            "config": {
+                "workload": cfg["workload"],
+                "volume": f"{cfg['dims'][0]}x{cfg['dims'][1]}x{cfg['dims'][2]} {np.dtype(cfg['dtype']).name}",
+                "viewport": f"{cfg['W']}x{cfg['H']}",
+                "camera": synth.CAMERAS[cfg["cam"]],
+                "tf": cfg["tf"], "shading": cfg["shading"], "ert_eps": cfg["ert"],
+                "parallelism": f"image row-blocks x{world}" + (" + RCCL gather" if world > 1 else ""),
+                "samples_per_frame": fstats["samples"],
+                "shaded_samples_per_frame": fstats["shaded_samples"],
+                "rays_per_frame": fstats["rays"],
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": rp.kernel_name(vr_amd.default_params(shading=cfg["shading"])),
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel_ms": round(kms, 4),
+                "bytes_model": "8*sizeof(voxel)/sample + 48*sizeof(voxel)/shaded sample + 4 B/pixel (SURVEY.md 8d)",
+            },
+            "cpu_baseline": cpu,
+            "variants": variants,
+        }
+        print(json.dumps(out), flush=True)
+    rp.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -427,6 +427,43 @@ int or_render_rows(const or_scene *s, float *out, int row0, int row1, int nthrea
     return 0;
 }
 
+int or_render_row_list(const or_scene *s, float *out, const int32_t *rows, int nrows,
+                       int nthreads, or_stats *stats)
+{
+    if (!s || !out || !rows || !s->vol || !s->tf || s->tf_n <= 0 || s->width <= 0 || s->height <= 0)
+        return -22;
+    ray_frame f;
+    make_ray_frame(s, &f);
+    float *lut = (float *)malloc((size_t)s->tf_n * 4 * sizeof(float));
+    if (!lut) return -12;
+    or_tf_decode(s->tf, s->tf_n, lut);
+    uint64_t rays = 0, samples = 0, shaded = 0, steps = 0;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) \
+    reduction(+ : rays, samples, shaded, steps)
+#endif
+    for (int r = 0; r < nrows; ++r) {
+        const int y = rows[r];
+        if (y < 0 || y >= s->height) continue;
+        or_stats st = {0, 0, 0, 0};
+        for (int x = 0; x < s->width; ++x)
+            march_pixel(s, &f, lut, x, y, out + ((size_t)y * s->width + x) * 4, &st);
+        rays += st.rays;
+        samples += st.samples;
+        shaded += st.shaded_samples;
+        steps += st.steps;
+    }
+    free(lut);
+    if (stats) {
+        stats->rays = rays;
+        stats->samples = samples;
+        stats->shaded_samples = shaded;
+        stats->steps = steps;
+    }
+    return 0;
+}
+
 int or_max_threads(void)
 {
 #ifdef _OPENMP

@@ -64,6 +64,10 @@ typedef struct or_stats {
 int or_render_rows(const or_scene *s, float *out, int row0, int row1, int nthreads,
                    or_stats *stats);
 
+/* Render the listed rows (any order) — the bounded CPU-baseline sample. */
+int or_render_row_list(const or_scene *s, float *out, const int32_t *rows, int nrows,
+                       int nthreads, or_stats *stats);
+
 /* Sampler unit functions (KATs). */
 float or_trilinear(const float *vol, int nx, int ny, int nz, float px, float py, float pz);
 void or_tf_decode(const uint32_t *tf, int n, float *lut /* n*4 */);

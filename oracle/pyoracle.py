@@ -57,6 +57,9 @@ def lib():
         L.or_render_rows.restype = C.c_int
         L.or_render_rows.argtypes = [C.POINTER(or_scene), C.c_void_p, C.c_int, C.c_int, C.c_int,
                                      C.POINTER(or_stats)]
+        L.or_render_row_list.restype = C.c_int
+        L.or_render_row_list.argtypes = [C.POINTER(or_scene), C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                         C.POINTER(or_stats)]
         L.or_trilinear.restype = C.c_float
         L.or_trilinear.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float]
         L.or_tf_decode.restype = None
@@ -121,6 +124,20 @@ class Scene:
         rc = lib().or_render_rows(C.byref(self.s), out.ctypes.data, row0, row1, nthreads, C.byref(st))
         if rc != 0:
             raise RuntimeError(f"or_render_rows failed ({rc})")
+        return out, dict(rays=st.rays, samples=st.samples, shaded_samples=st.shaded_samples,
+                         steps=st.steps)
+
+    def render_rows(self, rows, out=None, nthreads=0):
+        """Render an arbitrary list of rows (OpenMP over the list) into `out` (H, W, 4)."""
+        H, W = self.s.height, self.s.width
+        if out is None:
+            out = np.full((H, W, 4), np.nan, dtype=np.float32)
+        rows = np.ascontiguousarray(np.asarray(rows, dtype=np.int32))
+        st = or_stats()
+        rc = lib().or_render_row_list(C.byref(self.s), out.ctypes.data, rows.ctypes.data,
+                                      int(rows.size), nthreads, C.byref(st))
+        if rc != 0:
+            raise RuntimeError(f"or_render_row_list failed ({rc})")
         return out, dict(rays=st.rays, samples=st.samples, shaded_samples=st.shaded_samples,
                          steps=st.steps)
 

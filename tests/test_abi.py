@@ -1,0 +1,94 @@
+"""CPU: the C-ABI library loads and exports every entry point include/vr/*.h declares.
+No compute calls here (no GPU in the build container)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+import vr_amd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared(header):
+    src = open(os.path.join(ROOT, "include", "vr", header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = set(re.findall(r"\b(vr_[a-z0-9_]+)\s*\(", src))
+    return names
+
+
+def exported():
+    out = subprocess.run(["nm", "-D", "--defined-only", vr_amd.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    return {l.split()[-1] for l in out.splitlines() if " T " in l}
+
+
+@pytest.mark.parametrize("header", ["vr.h", "vr_host.h"])
+def test_every_declared_symbol_is_exported(header):
+    names = declared(header)
+    assert len(names) > 10
+    missing = names - exported()
+    assert not missing, missing
+
+
+def test_binding_lists_cover_headers():
+    assert declared("vr.h") == set(vr_amd.ABI_SYMBOLS)
+    assert declared("vr_host.h") == set(vr_amd.HOST_SYMBOLS)
+
+
+def test_library_loads_and_pure_entry_points():
+    L = vr_amd.lib()
+    assert L.vr_abi_version() == 1
+    p = vr_amd.default_params()
+    assert p.step == pytest.approx(0.005) and p.ray_dist == pytest.approx(1.8)
+    assert list(p.clear_color) == pytest.approx([0.11, 0.11, 0.11, 1.0])
+    assert p.ert_eps == 0.0 and p.shading == 0
+    # row-block sharding arithmetic
+    assert vr_amd.shard_rows(1080, 16, 1) == 1088
+    assert vr_amd.shard_rows(1080, 16, 8) == 144
+    assert vr_amd.shard_rows(53, 1, 5) == 11
+    assert vr_amd.shard_rows(10, 0, 2) == 0
+
+
+def test_struct_layouts_match_header():
+    # sizes of the ABI structs as declared in vr.h (no padding surprises across the boundary)
+    assert C.sizeof(vr_amd.vr_camera) == 4 * (16 + 3 + 3)
+    assert C.sizeof(vr_amd.vr_params) == 4 * (3 + 1 + 4 + 3 + 1 + 4)
+    assert C.sizeof(vr_amd.vr_stats) == 32
+    src = open(os.path.join(ROOT, "include", "vr", "vr.h")).read()
+    test = r"""
+#include "vr/vr.h"
+#include <stdio.h>
+#include <stddef.h>
+int main(void) { printf("%zu %zu %zu %zu\n", sizeof(vr_camera), sizeof(vr_params),
+  sizeof(vr_stats), offsetof(vr_params, spec_power)); return 0; }
+"""
+    tmp = os.path.join("/tmp", "vr_abi_layout")
+    with open(tmp + ".c", "w") as f:
+        f.write(test)
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), tmp + ".c", "-o", tmp], check=True)
+    out = subprocess.run([tmp], capture_output=True, text=True, check=True).stdout.split()
+    assert [int(x) for x in out] == [C.sizeof(vr_amd.vr_camera), C.sizeof(vr_amd.vr_params),
+                                     C.sizeof(vr_amd.vr_stats), vr_amd.vr_params.spec_power.offset]
+    assert "VR_ABI_VERSION 1" in src
+
+
+def test_create_without_device_fails_cleanly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a device is present")
+    with pytest.raises(RuntimeError, match="vr_create failed"):
+        vr_amd.OffscreenPass(8, 8)
+
+
+def test_no_cpu_fallback_in_product():
+    """The product path never routes through the oracle or any CPU renderer."""
+    for path in ("volumetric-renderer_amd/vr_amd.py", "volumetric-renderer_amd/csrc/vr_api.hip",
+                 "volumetric-renderer_amd/csrc/vr_kernels.hip", "volumetric-renderer_amd/host/vr_host.cpp"):
+        txt = open(os.path.join(ROOT, path)).read()
+        for needle in ("pyoracle", "liboracle", "oracle.h", "import oracle", "ref_numpy", "or_render"):
+            assert needle not in txt, (path, needle)
+    out = subprocess.run(["nm", "-D", vr_amd.LIB_PATH], capture_output=True, text=True).stdout
+    assert "or_render_rows" not in out
