@@ -1,0 +1,159 @@
+"""Cache-line footprint model of the ray-march gathers (design tool, CPU only).
+
+For a sample of 8x8-pixel wavefront tiles, march the 64 rays in lock-step exactly as one
+wavefront does and, for every load instruction the kernel would issue, count the distinct
+cache lines the 64 lanes touch.  The L1 (TCP) access rate is the measured limiter of the
+kernel (profiles/r01/pmc_*), so "lines per wave-instruction x instructions per sample" is the
+figure of merit for a volume layout.  Layouts are given as functions (x, y, z) -> element
+offset, voxel size and the loads a sample issues.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import ref_numpy  # noqa: E402
+
+
+def rays(view, cam_pos, W, H, px, py):
+    V = np.asarray(view, dtype=np.float64).reshape(4, 4).T
+    inv = np.linalg.inv(ref_numpy.projection(W, H) @ V)
+    x = (px + 0.5) / W * 2 - 1
+    y = (py + 0.5) / H * 2 - 1
+    h0 = inv @ np.stack([x, y, np.zeros_like(x), np.ones_like(x)])
+    h1 = inv @ np.stack([x, y, np.ones_like(x), np.ones_like(x)])
+    p0 = (h0[:3] / h0[3]).T
+    d = (h1[:3] / h1[3]).T - p0
+    with np.errstate(divide="ignore", invalid="ignore"):
+        t1 = (-0.5 - p0) / d
+        t2 = (0.5 - p0) / d
+    lo = np.minimum(t1, t2).max(axis=1)
+    hi = np.maximum(t1, t2).min(axis=1)
+    ok = (lo < hi) & (lo >= 0) & (lo <= 1)
+    e = p0 + lo[:, None] * d
+    dirs = e - np.asarray(cam_pos)
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    return ok, e + 0.5, dirs
+
+
+# ---- layouts: each returns a list of per-lane byte-address arrays, one per load instruction --
+def brick_apron(B, vb, pair_x=True):
+    S = B + 1
+
+    def fn(i, j, k, nb):
+        pi, pj, pk = i + 2, j + 2, k + 2
+        b = ((pk // B) * nb + (pj // B)) * nb + (pi // B)
+        base = (b * S ** 3 + ((pk % B) * S + (pj % B)) * S + (pi % B)) * vb
+        loads = []
+        for dz in (0, 1):
+            for dy in (0, 1):
+                o = base + (dz * S * S + dy * S) * vb
+                if pair_x:
+                    loads.append((o, 2 * vb))
+                else:
+                    loads.append((o, vb))
+                    loads.append((o + vb, vb))
+        return loads
+    return fn
+
+
+def brick_apron_zpair(B, vb):
+    """Each stored element holds (v(z), v(z+1)): one 4*vb-byte load gets x-pair x z-pair."""
+    S = B + 1
+
+    def fn(i, j, k, nb):
+        pi, pj, pk = i + 2, j + 2, k + 2
+        b = ((pk // B) * nb + (pj // B)) * nb + (pi // B)
+        base = (b * S ** 3 + ((pk % B) * S + (pj % B)) * S + (pi % B)) * 2 * vb
+        return [(base, 4 * vb), (base + S * 2 * vb, 4 * vb)]
+    return fn
+
+
+def brick_apron_yzquad(B, vb):
+    """Each stored element holds v(y..y+1, z..z+1): one 8*vb-byte run at x gets the whole
+    2x2x2 footprint (f32: two dwordx4; u16: one dwordx4; u8: one dwordx2)."""
+    S = B + 1
+
+    def fn(i, j, k, nb):
+        pi, pj, pk = i + 2, j + 2, k + 2
+        b = ((pk // B) * nb + (pj // B)) * nb + (pi // B)
+        base = (b * S ** 3 + ((pk % B) * S + (pj % B)) * S + (pi % B)) * 4 * vb
+        w = 8 * vb
+        if w <= 16:
+            return [(base, w)]
+        return [(base, 16), (base + 16, 16)]
+    return fn
+
+
+def linear(vb, n):
+    def fn(i, j, k, nb):
+        loads = []
+        for dz in (0, 1):
+            for dy in (0, 1):
+                o = ((np.clip(k + dz, 0, n - 1) * n + np.clip(j + dy, 0, n - 1)) * n + np.clip(i, 0, n - 1)) * vb
+                loads.append((o, 2 * vb))
+        return loads
+    return fn
+
+
+def simulate(layout, n, vb, view, pos, W=1920, H=1080, ntiles=300, seed=0, line=128):
+    rng = np.random.default_rng(seed)
+    nb = (n + 3 + 15) // 16
+    tot_instr = 0
+    tot_lines = 0
+    samples = 0
+    tiles = 0
+    while tiles < ntiles:
+        tx = rng.integers(0, W // 8)
+        ty = rng.integers(0, H // 8)
+        px, py = np.meshgrid(np.arange(8) + tx * 8, np.arange(8) + ty * 8)
+        ok, pos0, dirs = rays(view, pos, W, H, px.ravel().astype(float), py.ravel().astype(float))
+        if ok.sum() < 32:
+            continue
+        tiles += 1
+        p = pos0.copy()
+        alive = ok.copy()
+        for _ in range(360):
+            alive &= np.all((p >= 0) & (p <= 1), axis=1)
+            if not alive.any():
+                break
+            u = p[alive] * n - 0.5
+            i0 = np.floor(u).astype(np.int64)
+            loads = layout(i0[:, 0], i0[:, 1], i0[:, 2], nb)
+            for addr, width in loads:
+                first = addr // line
+                last = (addr + width - 1) // line
+                tot_lines += len(np.unique(np.concatenate([first, last])))
+                tot_instr += 1
+            samples += int(alive.sum())
+            p = p + dirs * 0.005
+    return dict(lines_per_instr=tot_lines / tot_instr, instr_per_wave_step=tot_instr / max(1, tiles),
+                lines_per_sample=tot_lines / samples, samples=samples)
+
+
+if __name__ == "__main__":
+    sys.path.insert(0, os.path.join(ROOT, "volumetric-renderer_amd"))
+    import synth
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+    cams = {"fill": synth.camera("fill"), "fill_oblique": synth.camera("fill_oblique"),
+            "side_x": synth.vr_amd.make_camera(radius=1.6, rotate=(360.0, 0.0)),
+            "top_z": synth.vr_amd.make_camera(radius=1.6, rotate=(0.0, 360.0))}
+    layouts = {
+        "brick16+apron f32 (current, dwordx2)": (brick_apron(16, 4), 4),
+        "brick8+apron f32 (dwordx2)": (brick_apron(8, 4), 4),
+        "brick4+apron f32 (dwordx2)": (brick_apron(4, 4), 4),
+        "brick16+apron f32 zpair (dwordx4 x2)": (brick_apron_zpair(16, 4), 4),
+        "brick8+apron f32 zpair (dwordx4 x2)": (brick_apron_zpair(8, 4), 4),
+        "brick4+apron f32 zpair (dwordx4 x2)": (brick_apron_zpair(4, 4), 4),
+    }
+    for cname, cam in cams.items():
+        vc = cam.to_vr_camera()
+        for lname, (fn, vb) in layouts.items():
+            r = simulate(fn, n, vb, list(vc.view), list(vc.position), ntiles=60)
+            print(f"{cname:13s} {lname:40s} lines/instr {r['lines_per_instr']:6.2f}  "
+                  f"lines/sample {r['lines_per_sample']:.3f}")

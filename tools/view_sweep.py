@@ -1,0 +1,73 @@
+"""Throughput of the ray-march kernel across view directions (GPU; exploration tool).
+
+Renders one frame per camera K times through vr_render_device and prints the kernel time
+(HIP events) and Gsamples/s per view, for the C3 volume by default.  Used to check the
+layout model of tools/line_sim.py on hardware (view dependence of the gather cost).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for sub in ("volumetric-renderer_amd", "tools"):
+    sys.path.insert(0, os.path.join(ROOT, sub))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import synth  # noqa: E402
+import vr_amd  # noqa: E402
+
+VIEWS = {
+    "fill": dict(radius=1.6, rotate=None),
+    "fill_oblique": dict(radius=1.6, rotate=(40.0, 25.0)),
+    "side_x": dict(radius=1.6, rotate=(360.0, 0.0)),
+    "top_z": dict(radius=1.6, rotate=(0.0, 360.0)),
+    "diag": dict(radius=2.0, rotate=(180.0, 140.0)),
+    "default": dict(radius=3.0, rotate=None),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=512)
+    ap.add_argument("--dtype", default="float32")
+    ap.add_argument("--size", default="1920x1080")
+    ap.add_argument("--tf", default="tf2")
+    ap.add_argument("--shading", type=int, default=0)
+    ap.add_argument("--ert", type=float, default=0.0)
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    W, H = (int(x) for x in args.size.split("x"))
+    rp = vr_amd.OffscreenPass(W, H)
+    rp.generate_volume((args.n,) * 3, np.dtype(args.dtype), seed=2024)
+    rp.transfer_function_changed(synth.TFS[args.tf]())
+    out = torch.empty((H + 16, W), dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    p = vr_amd.default_params(shading=args.shading, ert_eps=args.ert)
+    res = {}
+    for name, v in VIEWS.items():
+        cam = vr_amd.make_camera(**v).to_vr_camera()
+        st = rp.count_work(cam, p)
+        for _ in range(3):
+            rp.render_device(cam, p, out.data_ptr(), vr_amd.OUT_RGBA8, 16, 0, 1, stream)
+        torch.cuda.synchronize()
+        rp.timing_reset()
+        rp.timing_enable(True)
+        for _ in range(args.reps):
+            rp.render_device(cam, p, out.data_ptr(), vr_amd.OUT_RGBA8, 16, 0, 1, stream)
+        ms, n = rp.timing_read()
+        rp.timing_enable(False)
+        kms = ms / n
+        res[name] = dict(kernel_ms=round(kms, 4), samples=st["samples"],
+                         gsamples_s=round(st["samples"] / (kms * 1e-3) / 1e9, 2),
+                         shaded=st["shaded_samples"])
+        print(name, json.dumps(res[name]), flush=True)
+    print(json.dumps(dict(args=vars(args), views=res)))
+
+
+if __name__ == "__main__":
+    main()

@@ -37,15 +37,12 @@ __device__ __forceinline__ size_t cell_offset(int pi, int pj, int pk, uint32_t n
     return (size_t)b * (size_t)kBrickVoxels + l;
 }
 
-// Trilinear filter of the 2x2x2 cell at p: lerp x, then y, then z (oracle tri_cell order).
-template <typename VT>
-__device__ __forceinline__ float cell(const VT *__restrict__ p, float ax, float ay, float az)
+// Trilinear filter of a 2x2x2 cell given its voxels v[dz][dy][dx]: lerp x, then y, then z
+// (the oracle's tri_cell operation order).
+__device__ __forceinline__ float tri8(float v000, float v100, float v010, float v110, float v001,
+                                      float v101, float v011, float v111, float ax, float ay,
+                                      float az)
 {
-    constexpr int S = kStore, S2 = kStore * kStore;
-    const float v000 = (float)p[0], v100 = (float)p[1];
-    const float v010 = (float)p[S], v110 = (float)p[S + 1];
-    const float v001 = (float)p[S2], v101 = (float)p[S2 + 1];
-    const float v011 = (float)p[S2 + S], v111 = (float)p[S2 + S + 1];
     const float c00 = lerpf(v000, v100, ax);
     const float c10 = lerpf(v010, v110, ax);
     const float c01 = lerpf(v001, v101, ax);
@@ -53,6 +50,72 @@ __device__ __forceinline__ float cell(const VT *__restrict__ p, float ax, float 
     const float c0 = lerpf(c00, c10, ay);
     const float c1 = lerpf(c01, c11, ay);
     return lerpf(c0, c1, az);
+}
+
+// The 8 voxels of the cell whose low corner is at p (x-pairs are adjacent: the compiler
+// fuses each pair into one global_load_dwordx2 for f32).
+template <typename VT>
+struct Cell8 {
+    float v[8];  // index dx + 2 dy + 4 dz
+    __device__ __forceinline__ void load(const VT *__restrict__ p)
+    {
+        constexpr int S = kStore, S2 = kStore * kStore;
+        v[0] = (float)p[0];
+        v[1] = (float)p[1];
+        v[2] = (float)p[S];
+        v[3] = (float)p[S + 1];
+        v[4] = (float)p[S2];
+        v[5] = (float)p[S2 + 1];
+        v[6] = (float)p[S2 + S];
+        v[7] = (float)p[S2 + S + 1];
+    }
+    __device__ __forceinline__ float tri(float ax, float ay, float az) const
+    {
+        return tri8(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], ax, ay, az);
+    }
+};
+
+// Central-difference gradient (extension): cells one texel either side along each axis
+// share the centre cell's weights, so only 24 new voxels are needed (a 4-wide stencil per
+// axis).  The voxel one below / two above the cell may sit in the neighbouring brick (the
+// 1-voxel apron covers only +1): the per-axis deltas below pick the right brick.
+// Result is bit-identical to six independent trilinear fetches (same voxels, same ops).
+template <typename VT>
+__device__ __forceinline__ void gradient(const VT *__restrict__ p, const Cell8<VT> &c,
+                                         int lx, int ly, int lz, long by_stride, long bz_stride,
+                                         float ax, float ay, float az, float &gx, float &gy,
+                                         float &gz)
+{
+    constexpr int S = kStore, S2 = kStore * kStore, B = kBrickVoxels;
+    const long dxm = lx > 0 ? -1 : (15 - B);
+    const long dxp = lx < 15 ? 2 : (B - 14);
+    const long dym = ly > 0 ? -S : (15 * S - by_stride);
+    const long dyp = ly < 15 ? 2 * S : (by_stride - 14 * S);
+    const long dzm = lz > 0 ? -S2 : (15L * S2 - bz_stride);
+    const long dzp = lz < 15 ? 2 * S2 : (bz_stride - 14L * S2);
+    const VT *__restrict__ xm = p + dxm;
+    const VT *__restrict__ xp = p + dxp;
+    const VT *__restrict__ ym = p + dym;
+    const VT *__restrict__ yp = p + dyp;
+    const VT *__restrict__ zm = p + dzm;
+    const VT *__restrict__ zp = p + dzp;
+    // x taps: voxels x-1 and x+2 over (dy, dz)
+    const float xm00 = (float)xm[0], xm10 = (float)xm[S], xm01 = (float)xm[S2], xm11 = (float)xm[S2 + S];
+    const float xp00 = (float)xp[0], xp10 = (float)xp[S], xp01 = (float)xp[S2], xp11 = (float)xp[S2 + S];
+    // y taps: voxels y-1 and y+2 over (dx, dz)
+    const float ym00 = (float)ym[0], ym10 = (float)ym[1], ym01 = (float)ym[S2], ym11 = (float)ym[S2 + 1];
+    const float yp00 = (float)yp[0], yp10 = (float)yp[1], yp01 = (float)yp[S2], yp11 = (float)yp[S2 + 1];
+    // z taps: voxels z-1 and z+2 over (dx, dy)
+    const float zm00 = (float)zm[0], zm10 = (float)zm[1], zm01 = (float)zm[S], zm11 = (float)zm[S + 1];
+    const float zp00 = (float)zp[0], zp10 = (float)zp[1], zp01 = (float)zp[S], zp11 = (float)zp[S + 1];
+    const float *v = c.v;
+    // cell(i+1) uses x = {1, 2}; cell(i-1) uses x = {-1, 0}
+    gx = tri8(v[1], xp00, v[3], xp10, v[5], xp01, v[7], xp11, ax, ay, az) -
+         tri8(xm00, v[0], xm10, v[2], xm01, v[4], xm11, v[6], ax, ay, az);
+    gy = tri8(v[2], v[3], yp00, yp10, v[6], v[7], yp01, yp11, ax, ay, az) -
+         tri8(ym00, ym10, v[0], v[1], ym01, ym11, v[4], v[5], ax, ay, az);
+    gz = tri8(v[4], v[5], v[6], v[7], zp00, zp10, zp01, zp11, ax, ay, az) -
+         tri8(zm00, zm10, zm01, zm11, v[0], v[1], v[2], v[3], ax, ay, az);
 }
 
 __device__ __forceinline__ void texel_coord(float p, float n, int &i, float &a)
@@ -162,7 +225,8 @@ __global__ __launch_bounds__(kThreads) void march_kernel(const MarchParams P)
     if (tf_in_lds)
         for (int i = tid; i < P.tf_n; i += kThreads) s_tf[i] = P.tf[i];
     __syncthreads();
-    const float4 *lut = tf_in_lds ? s_tf : P.tf;
+    const long by_stride = (long)P.nbx * kBrickVoxels;
+    const long bz_stride = (long)P.nbx * P.nby * kBrickVoxels;
 
     // XCD-aware, bijective block -> tile remap (blocks b and b+8 share an XCD's L2: give
     // each such group a contiguous band of tiles in raster order).
@@ -200,17 +264,18 @@ __global__ __launch_bounds__(kThreads) void march_kernel(const MarchParams P)
             texel_coord(p1, P.fny, j, ay);
             texel_coord(p2, P.fnz, k, az);
             const int pi = i + kPad, pj = j + kPad, pk = k + kPad;
-            const float d = cell(vol + cell_offset(pi, pj, pk, P.nbx, P.nby), ax, ay, az);
+            const VT *__restrict__ cp = vol + cell_offset(pi, pj, pk, P.nbx, P.nby);
+            Cell8<VT> c;
+            c.load(cp);
+            const float d = c.tri(ax, ay, az);
             const float tt = (d - P.vmin) / P.range;
-            float4 s = tf_lookup(lut, P.tf_n, P.tf_nf, tt);
+            float4 s = tf_in_lds ? tf_lookup(s_tf, P.tf_n, P.tf_nf, tt)
+                                 : tf_lookup(P.tf, P.tf_n, P.tf_nf, tt);
             if (COUNT) ++n_samples;
             if (SHADE && s.w > 0.0f) {
-                const float gx = cell(vol + cell_offset(pi + 1, pj, pk, P.nbx, P.nby), ax, ay, az) -
-                                 cell(vol + cell_offset(pi - 1, pj, pk, P.nbx, P.nby), ax, ay, az);
-                const float gy_ = cell(vol + cell_offset(pi, pj + 1, pk, P.nbx, P.nby), ax, ay, az) -
-                                  cell(vol + cell_offset(pi, pj - 1, pk, P.nbx, P.nby), ax, ay, az);
-                const float gz = cell(vol + cell_offset(pi, pj, pk + 1, P.nbx, P.nby), ax, ay, az) -
-                                 cell(vol + cell_offset(pi, pj, pk - 1, P.nbx, P.nby), ax, ay, az);
+                float gx, gy_, gz;
+                gradient(cp, c, pi & 15, pj & 15, pk & 15, by_stride, bz_stride, ax, ay, az, gx,
+                         gy_, gz);
                 if (COUNT) ++n_shaded;
                 const float wx = gx * P.fnx, wy = gy_ * P.fny, wz = gz * P.fnz;
                 const float g2 = wx * wx + wy * wy + wz * wz;
