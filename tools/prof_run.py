@@ -1,0 +1,53 @@
+"""Minimal profiling workload (no torch): one configuration, K frames through the C ABI.
+
+Used under rocprofv3 (--kernel-trace --stats, or one --pmc group per run) so that every
+counter pass replays a short process.  Prints the in-process HIP-event kernel time so the
+profile's per-dispatch durations can be matched.
+  python tools/prof_run.py [--n 512] [--dtype float32] [--size 1920x1080] [--cam fill]
+                           [--tf tf2] [--shading 1] [--ert 1e-5] [--frames 10] [--tile-order 0]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for sub in ("volumetric-renderer_amd", "tools"):
+    sys.path.insert(0, os.path.join(ROOT, sub))
+
+import numpy as np  # noqa: E402
+
+import synth  # noqa: E402
+import vr_amd  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=512)
+    ap.add_argument("--dtype", default="float32")
+    ap.add_argument("--size", default="1920x1080")
+    ap.add_argument("--cam", default="fill")
+    ap.add_argument("--tf", default="tf2")
+    ap.add_argument("--shading", type=int, default=1)
+    ap.add_argument("--ert", type=float, default=1e-5)
+    ap.add_argument("--frames", type=int, default=10)
+    ap.add_argument("--tile-order", type=int, default=0)
+    a = ap.parse_args()
+    W, H = (int(x) for x in a.size.split("x"))
+    rp = vr_amd.OffscreenPass(W, H)
+    rp.generate_volume((a.n,) * 3, np.dtype(a.dtype), seed=2024)
+    rp.transfer_function_changed(synth.TFS[a.tf]())
+    cam = synth.camera(a.cam).to_vr_camera()
+    p = vr_amd.default_params(shading=a.shading, ert_eps=a.ert, tile_order=a.tile_order)
+    rp.render(cam, p, vr_amd.OUT_RGBA8)
+    rp.timing_enable(True)
+    for _ in range(a.frames):
+        rp.render(cam, p, vr_amd.OUT_RGBA8)
+    ms, n = rp.timing_read()
+    st = rp.count_work(cam, p)
+    print(json.dumps(dict(args=vars(a), kernel=rp.kernel_name(p), kernel_ms=ms / n, stats=st,
+                          gsamples_s=st["samples"] / (ms / n * 1e-3) / 1e9)))
+
+
+if __name__ == "__main__":
+    main()

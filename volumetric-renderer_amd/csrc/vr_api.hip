@@ -346,6 +346,9 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.local_rows = vr_shard_rows(c->height, row_block, nranks);
     P.tiles_x = (c->width + 15) / 16;
     P.tiles_y = (P.local_rows + 15) / 16;
+    P.tile_order = p->tile_order >= 1 && p->tile_order <= 3 ? (uint32_t)p->tile_order : 3u;
+    P.supers_x = (P.tiles_x + 3) / 4;
+    P.supers_total = P.supers_x * ((P.tiles_y + 3) / 4);
     P.out_format = out_format;
     return VR_OK;
 }

@@ -68,6 +68,8 @@ struct MarchParams {
     uint32_t W, H;
     uint32_t row_block, rank, nranks, local_rows;
     uint32_t tiles_x, tiles_y;
+    uint32_t tile_order;    // 1 raster, 2 XCD bands, 3 XCD-interleaved super-tiles
+    uint32_t supers_x, supers_total;  // super-tile grid (tile_order 3)
     int32_t out_format;
 };
 

@@ -12,8 +12,8 @@
 //  * bricked native-dtype volume (vr_internal.h): one brick base address + 7 immediate
 //    offsets per sample, zero apron = CLAMP_TO_BORDER without bounds tests;
 //  * TF decoded to linear float4 once per frame on the host and staged in LDS;
-//  * XCD-aware tile order: workgroups that share an XCD's L2 get a contiguous band of tiles,
-//    so the volume region behind that band stays in that L2;
+//  * XCD-aware tile order (march_kernel head): tiles grouped in 64x64-pixel super-tiles, each
+//    super-tile's workgroups on one XCD (L2 locality), super-tiles dealt over all XCDs (balance);
 //  * fp contraction is OFF (pragma below + -ffp-contract=off): every fused multiply-add is
 //    an explicit fmaf(), matching the CPU oracle's operation order bit for bit.
 #include "vr_internal.h"
@@ -221,6 +221,32 @@ __global__ __launch_bounds__(kThreads) void march_kernel(const MarchParams P)
 {
     __shared__ float4 s_tf[kTfLds];
     const int tid = threadIdx.x;
+
+    // Block -> 16x16 tile.  Workgroups b and b+8 run on the same XCD (round-robin dispatch;
+    // speed only, never correctness).  Orders: 1 raster; 2 each XCD a contiguous band of
+    // tiles (bijective remap); 3 each XCD every 8th 4x4-tile super-tile (64x64 px) in raster
+    // order, its tiles consecutive on that XCD: L2 locality inside a super-tile, every XCD
+    // sampling the whole frame (load balance when the volume covers part of it).
+    uint32_t tile_x, tile_y;
+    {
+        const uint32_t nwg = gridDim.x, b = blockIdx.x;
+        if (P.tile_order == 3) {
+            const uint32_t k = b >> 3, w = k & 15;
+            const uint32_t s = (b & 7u) + 8u * (k >> 4);
+            tile_x = (s % P.supers_x) * 4 + (w & 3);
+            tile_y = (s / P.supers_x) * 4 + (w >> 2);
+            if (s >= P.supers_total || tile_x >= P.tiles_x || tile_y >= P.tiles_y) return;
+        } else if (P.tile_order == 2) {
+            const uint32_t xcd = b & 7u, q = nwg >> 3, r = nwg & 7u;
+            const uint32_t t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+            tile_x = t % P.tiles_x;
+            tile_y = t / P.tiles_x;
+        } else {
+            tile_x = b % P.tiles_x;
+            tile_y = b / P.tiles_x;
+        }
+    }
+
     const bool tf_in_lds = P.tf_n <= kTfLds;
     if (tf_in_lds)
         for (int i = tid; i < P.tf_n; i += kThreads) s_tf[i] = P.tf[i];
@@ -228,12 +254,6 @@ __global__ __launch_bounds__(kThreads) void march_kernel(const MarchParams P)
     const long by_stride = (long)P.nbx * kBrickVoxels;
     const long bz_stride = (long)P.nbx * P.nby * kBrickVoxels;
 
-    // XCD-aware, bijective block -> tile remap (blocks b and b+8 share an XCD's L2: give
-    // each such group a contiguous band of tiles in raster order).
-    const uint32_t nwg = gridDim.x, b = blockIdx.x;
-    const uint32_t xcd = b & 7u, q = nwg >> 3, r = nwg & 7u;
-    const uint32_t t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-    const uint32_t tile_x = t % P.tiles_x, tile_y = t / P.tiles_x;
     const int wave = tid >> 6, lane = tid & 63;
     const uint32_t px = tile_x * kTile + (wave & 1) * 8 + (lane & 7);
     const uint32_t ly = tile_y * kTile + (wave >> 1) * 8 + (lane >> 3);
@@ -479,8 +499,9 @@ __global__ __launch_bounds__(256) void assemble_kernel(const PixT *__restrict__ 
 template <typename VT, bool SHADE, bool COUNT>
 hipError_t launch_march_t(const MarchParams &p, hipStream_t stream)
 {
-    const uint32_t nblocks = p.tiles_x * p.tiles_y;
-    if (nblocks == 0) return hipSuccess;
+    const uint32_t nblocks = p.tile_order == 3 ? ((p.supers_total + 7) / 8) * 8 * 16
+                                               : p.tiles_x * p.tiles_y;
+    if (p.tiles_x * p.tiles_y == 0) return hipSuccess;
     hipLaunchKernelGGL((march_kernel<VT, SHADE, COUNT>), dim3(nblocks), dim3(kThreads), 0,
                        stream, p);
     return hipGetLastError();

@@ -44,7 +44,8 @@ class vr_params(C.Structure):
     _fields_ = [("step", C.c_float), ("ray_dist", C.c_float), ("ert_eps", C.c_float),
                 ("shading", C.c_int32), ("clear_color", C.c_float * 4),
                 ("ambient", C.c_float), ("diffuse", C.c_float), ("specular", C.c_float),
-                ("spec_power", C.c_int32), ("reserved", C.c_int32 * 4)]
+                ("spec_power", C.c_int32), ("tile_order", C.c_int32),
+                ("reserved", C.c_int32 * 3)]
 
 
 class vr_stats(C.Structure):
