@@ -1,0 +1,61 @@
+"""Aggregate rocprofv3 --pmc passes (tools/pmc_passes.sh output) for one kernel and derive
+the figures DESIGN.md uses.  Usage: python tools/pmc_report.py gpurun_out/<tag> [kernel-substr]
+
+Units (MI355X_MICROARCH.md): SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles;
+FETCH_SIZE / WRITE_SIZE are KB; on gfx950 FETCH_SIZE reads 1/2 of the bytes of wide
+coalesced streaming reads (TCC_EA0_RDREQ x 64 B with 128-B requests), so HBM read bytes are
+reported both as FETCH_SIZE and as the corrected 2 x FETCH_SIZE (the guide's prescription).
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def load(d, kname):
+    agg = collections.defaultdict(list)
+    durs = []
+    for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"]
+            if kname not in k or "true>" in k.split(",")[-1]:  # skip the COUNT variant
+                continue
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+    return {k: sum(v) / len(v) for k, v in agg.items()}, (sum(durs) / len(durs) if durs else None)
+
+
+def main():
+    d = sys.argv[1]
+    kname = sys.argv[2] if len(sys.argv) > 2 else "march_kernel"
+    c, dur = load(d, kname)
+    out = {"kernel_substr": kname, "counters": c, "profiled_dispatch_s": dur}
+    g = lambda k: c.get(k)
+    der = {}
+    if g("SQ_WAVE_CYCLES"):
+        wc = g("SQ_WAVE_CYCLES")
+        for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
+                  "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_LDS"):
+            if g(k) is not None:
+                der[k + "_frac_of_wave_cycles"] = round(g(k) / wc, 4)
+    if g("TCP_TOTAL_CACHE_ACCESSES_sum") and g("SQ_INSTS_VMEM_RD"):
+        der["tcp_accesses_per_vmem_rd"] = round(g("TCP_TOTAL_CACHE_ACCESSES_sum") / g("SQ_INSTS_VMEM_RD"), 2)
+    if g("TCP_TOTAL_CACHE_ACCESSES_sum") and g("TCP_TCC_READ_REQ_sum"):
+        der["l1_hit_rate"] = round(1 - g("TCP_TCC_READ_REQ_sum") / g("TCP_TOTAL_CACHE_ACCESSES_sum"), 4)
+    if g("TCC_HIT_sum") is not None and g("TCC_MISS_sum"):
+        der["l2_hit_rate"] = round(g("TCC_HIT_sum") / (g("TCC_HIT_sum") + g("TCC_MISS_sum")), 4)
+    if g("FETCH_SIZE") is not None:
+        der["hbm_read_bytes_fetch_size"] = g("FETCH_SIZE") * 1024
+        der["hbm_read_bytes_corrected_x2"] = 2 * g("FETCH_SIZE") * 1024
+    if g("GRBM_GUI_ACTIVE") and dur:
+        der["effective_clock_ghz"] = round(g("GRBM_GUI_ACTIVE") / 8 / dur / 1e9, 3)
+    if g("SQ_LDS_BANK_CONFLICT") is not None and g("SQ_LDS_IDX_ACTIVE"):
+        der["lds_conflict_frac"] = round(g("SQ_LDS_BANK_CONFLICT") / g("SQ_LDS_IDX_ACTIVE"), 4)
+    out["derived"] = der
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -240,7 +240,7 @@ struct SplitMix {
 int set_bricks(vr_ctx *c, int storage, uint32_t nx, uint32_t ny, uint32_t nz, void **out)
 {
     const size_t bytes = (size_t)bricks_for(nx) * bricks_for(ny) * bricks_for(nz) *
-                         kBrickVoxels * storage_size(storage);
+                         kBrickElems * element_size(storage);
     if (c->bricks && c->brick_bytes == bytes) {
         *out = c->bricks;
         return VR_OK;
@@ -545,25 +545,41 @@ int vr_generate_volume(vr_ctx *c, int kind, int dtype, uint32_t nx, uint32_t ny,
         q[3] = 1.0f / (2.0f * sigma * sigma);
         q[4] = 0.3f + 0.7f * rng.uniform();
     }
+    // generate into a linear staging buffer of the storage type, then brick it like an
+    // uploaded volume (vr_set_volume_device path)
+    const size_t count = (size_t)nx * ny * nz;
     float *prm_dev = nullptr;
+    void *lin = nullptr;
     HIP_TRY(c, hipMalloc(&prm_dev, prm.size() * sizeof(float) + 2 * sizeof(uint32_t)),
             "hipMalloc(generator params)");
-    void *dst = nullptr;
-    int rc = set_bricks(c, st, nx, ny, nz, &dst);
-    if (rc) {
+    hipError_t e = hipMalloc(&lin, count * storage_size(st));
+    if (e != hipSuccess) {
         hipFree(prm_dev);
-        return rc;
+        return hip_fail(c, e, "hipMalloc(generator staging)");
     }
     uint32_t *mm = reinterpret_cast<uint32_t *>(prm_dev + prm.size());
     const uint32_t mm_init[2] = {0xFFFFFFFFu, 0u};
-    hipError_t e = hipMemcpy(prm_dev, prm.data(), prm.size() * sizeof(float), hipMemcpyHostToDevice);
+    e = hipMemcpy(prm_dev, prm.data(), prm.size() * sizeof(float), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(mm, mm_init, sizeof(mm_init), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = launch_generate(kind, st, dst, nx, ny, nz, prm_dev, (int)prm.size(), nullptr);
-    if (e == hipSuccess) e = launch_minmax(st, dst, nx, ny, nz, reinterpret_cast<float *>(mm), nullptr);
+    if (e == hipSuccess) e = launch_generate(kind, st, lin, nx, ny, nz, prm_dev, (int)prm.size(), nullptr);
+    if (e == hipSuccess) e = launch_minmax(st, lin, count, reinterpret_cast<float *>(mm), nullptr);
     uint32_t mm_host[2] = {0, 0};
     if (e == hipSuccess) e = hipMemcpy(mm_host, mm, sizeof(mm_host), hipMemcpyDeviceToHost);
     hipFree(prm_dev);
-    if (e != hipSuccess) return hip_fail(c, e, "generate volume");
+    if (e != hipSuccess) {
+        hipFree(lin);
+        return hip_fail(c, e, "generate volume");
+    }
+    const int src_dtype = st == ST_U8 ? VR_DTYPE_U8 : (st == ST_U16 ? VR_DTYPE_U16 : VR_DTYPE_F32);
+    void *dst = nullptr;
+    int rc = set_bricks(c, st, nx, ny, nz, &dst);
+    if (rc == VR_OK) {
+        e = launch_brick_from_linear(src_dtype, lin, dst, nx, ny, nz, st, nullptr);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        if (e != hipSuccess) rc = hip_fail(c, e, "brick generated volume");
+    }
+    hipFree(lin);
+    if (rc) return rc;
     auto unorder = [](uint32_t o) {
         const uint32_t u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
         float f;
@@ -591,14 +607,16 @@ int vr_debug_read_volume(vr_ctx *c, float *out)
     HIP_TRY(c, hipMemcpy(host.data(), c->bricks, c->brick_bytes, hipMemcpyDeviceToHost),
             "hipMemcpy(bricks)");
     const uint32_t nbx = bricks_for(c->nx), nby = bricks_for(c->ny);
-    const size_t es = storage_size(c->storage);
+    const size_t es = element_size(c->storage);  // component 0 of element (x,y,z) is v(x,y,z)
     for (uint32_t z = 0; z < c->nz; ++z)
         for (uint32_t y = 0; y < c->ny; ++y)
             for (uint32_t x = 0; x < c->nx; ++x) {
                 const uint32_t pi = x + kPad, pj = y + kPad, pk = z + kPad;
-                const size_t b = ((size_t)(pk >> 4) * nby + (pj >> 4)) * nbx + (pi >> 4);
-                const size_t l = ((size_t)(pk & 15) * kStore + (pj & 15)) * kStore + (pi & 15);
-                const unsigned char *src = host.data() + (b * kBrickVoxels + l) * es;
+                const size_t b = ((size_t)(pk >> kBrickShift) * nby + (pj >> kBrickShift)) * nbx +
+                                 (pi >> kBrickShift);
+                const size_t l = ((size_t)(pk & (kBrick - 1)) * kStore + (pj & (kBrick - 1))) * kStore +
+                                 (pi & (kBrick - 1));
+                const unsigned char *src = host.data() + (b * kBrickElems + l) * es;
                 float v;
                 switch (c->storage) {
                     case ST_U8: v = (float)*(const uint8_t *)src; break;

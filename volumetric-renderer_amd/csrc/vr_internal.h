@@ -8,26 +8,32 @@
 
 namespace vr {
 
-// ---- Bricked volume layout in HBM -------------------------------------------------------
+// ---- Bricked, paired-element volume layout in HBM --------------------------------------
 // The logical volume (nx, ny, nz) is shifted by kPad = 2 zero voxels on the low side of each
-// axis ("padded index" p = logical + 2) and cut into bricks of kBrick^3 base cells.  Brick b
-// stores padded indices [16 b, 16 b + 16] on each axis (kStore = 17 = 16 + 1-voxel apron), so
-// the 2x2x2 footprint of every trilinear fetch lies in ONE brick: one base address plus the 7
-// immediate offsets {1, 17, 18, 289, 290, 306, 307}.  Voxels outside [0, N) are stored as 0,
-// which realises CLAMP_TO_BORDER/TRANSPARENT_BLACK without a bounds test.  Bricks are ordered
-// x-fastest in the brick grid; the odd 17-voxel strides keep neighbouring rows/slices of a
-// brick out of the same L1/L2 sets (a 512^3 dense f32 volume has 2 KiB / 1 MiB strides).
-constexpr int kBrick = 16;
-constexpr int kStore = 17;
-constexpr int kBrickVoxels = kStore * kStore * kStore;  // 4913
+// axis ("padded index" p = logical + 2) and cut into bricks of kBrick^3 = 8^3 base cells.
+// Brick b stores ELEMENTS for padded indices [8 b, 8 b + 8] on each axis (kStore = 9: a
+// 1-element apron), bricks ordered x-fastest in the brick grid, elements x-fastest in a brick.
+// An element holds more than one voxel, so that one wide load fetches a whole trilinear
+// footprint edge-on (the gather pipeline, not HBM, bounds this kernel: DESIGN.md):
+//   f32   (and 32/64-bit inputs, converted):  "z-pair"  element = {v(x,y,z), v(x,y,z+1)}, 8 B;
+//         a sample = 2 x 16-B loads (elements x, x+1 of rows y and y+1).
+//   8/16-bit integers: "yz-quad" element = {v(y,z), v(y,z+1), v(y+1,z), v(y+1,z+1)} at x,
+//         4 B (u8/i8) or 8 B (u16/i16); a sample = 1 load of elements x, x+1 (8 B / 16 B).
+// Voxels outside [0, N) are stored as 0: CLAMP_TO_BORDER/TRANSPARENT_BLACK without a bounds
+// test.  Memory: 2 x (9/8)^3 = 2.85x the f32 voxels, 4 x (9/8)^3 = 5.7x the 8/16-bit voxels.
+constexpr int kBrick = 8;
+constexpr int kBrickShift = 3;
+constexpr int kStore = 9;
+constexpr int kBrickElems = kStore * kStore * kStore;  // 729
 constexpr int kPad = 2;
 
-// Bricks per axis: base padded indices of every fetch lie in [0, N + 2] (march fetches in
-// [1, N + 1]; gradient taps one further either side).
-inline uint32_t bricks_for(uint32_t n) { return (n + 3 + kBrick - 1) / kBrick; }
+// Bricks per axis: fetch base indices lie in [1, N + 1] (march) and gradient taps reach one
+// element below and (in z-pair x/y) two above, i.e. padded [0, N + 3].
+inline uint32_t bricks_for(uint32_t n) { return (n + 3) / kBrick + 1; }
 
 enum StorageType { ST_U8 = 0, ST_I8 = 1, ST_U16 = 2, ST_I16 = 3, ST_F32 = 4 };
 
+// Bytes of one voxel / of one element of storage type st.
 inline size_t storage_size(int st)
 {
     switch (st) {
@@ -38,6 +44,8 @@ inline size_t storage_size(int st)
         default: return 4;
     }
 }
+inline size_t voxels_per_element(int st) { return st == ST_F32 ? 2 : 4; }
+inline size_t element_size(int st) { return storage_size(st) * voxels_per_element(st); }
 
 // ---- Kernel parameters (one frame) -------------------------------------------------------
 struct MarchParams {
@@ -79,13 +87,15 @@ hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &
 const char *march_kernel_name(int storage, bool shade, bool count);
 hipError_t launch_brick_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,
                                     uint32_t ny, uint32_t nz, int storage, hipStream_t stream);
-hipError_t launch_generate(int kind, int storage, void *dst, uint32_t nx, uint32_t ny,
+// Synthetic volume into a LINEAR buffer of the storage type (then bricked).
+hipError_t launch_generate(int kind, int storage, void *dst_linear, uint32_t nx, uint32_t ny,
                            uint32_t nz, const float *params_dev, int nparams,
                            hipStream_t stream);
 hipError_t launch_assemble(const void *gathered, void *out, int out_format, uint32_t W,
                            uint32_t H, uint32_t row_block, uint32_t nranks,
                            uint32_t shard_rows, hipStream_t stream);
-hipError_t launch_minmax(int storage, const void *bricks, uint32_t nx, uint32_t ny,
-                         uint32_t nz, float *minmax_dev, hipStream_t stream);
+// min/max over a LINEAR buffer of the storage type (ordered-uint encoding in minmax_dev).
+hipError_t launch_minmax(int storage, const void *linear, size_t count, float *minmax_dev,
+                         hipStream_t stream);
 
 }  // namespace vr

@@ -18,6 +18,8 @@
 //    an explicit fmaf(), matching the CPU oracle's operation order bit for bit.
 #include "vr_internal.h"
 
+#include <type_traits>
+
 #pragma clang fp contract(off)
 
 namespace vr {
@@ -29,12 +31,30 @@ constexpr int kTfLds = 256;     // TF texels staged in LDS
 
 __device__ __forceinline__ float lerpf(float a, float b, float w) { return fmaf(w, b - a, a); }
 
-// 64-bit element offset (brick index * 4913 exceeds 2^32 for 2048^3 volumes) of padded cell (pi, pj, pk) in the bricked layout.
+// Unaligned-capable vector types: element pairs are 4- or 8-byte aligned, and gfx950 global
+// loads only need dword alignment, so these compile to single global_load_dwordx2/x4.
+typedef float f2a __attribute__((ext_vector_type(2))) __attribute__((aligned(4)));
+typedef float f4a __attribute__((ext_vector_type(4))) __attribute__((aligned(4)));
+typedef uint32_t u2a __attribute__((ext_vector_type(2))) __attribute__((aligned(4)));
+typedef uint32_t u4a __attribute__((ext_vector_type(4))) __attribute__((aligned(4)));
+
+template <typename VT>
+constexpr bool kZPair = std::is_same<VT, float>::value;
+// bytes per element; 32-bit words per element (quad layouts)
+template <typename VT>
+constexpr int kElemBytes = kZPair<VT> ? 8 : 4 * (int)sizeof(VT);
+template <typename VT>
+constexpr int kQuadWords = sizeof(VT) == 1 ? 1 : 2;
+
+// Element index of padded cell (pi, pj, pk) in the bricked layout (vr_internal.h).  64-bit:
+// a 2048^3 volume has 257^3 x 729 elements.
 __device__ __forceinline__ size_t cell_offset(int pi, int pj, int pk, uint32_t nbx, uint32_t nby)
 {
-    const uint32_t b = ((uint32_t)(pk >> 4) * nby + (uint32_t)(pj >> 4)) * nbx + (uint32_t)(pi >> 4);
-    const uint32_t l = ((uint32_t)(pk & 15) * kStore + (uint32_t)(pj & 15)) * kStore + (uint32_t)(pi & 15);
-    return (size_t)b * (size_t)kBrickVoxels + l;
+    const uint32_t b = ((uint32_t)(pk >> kBrickShift) * nby + (uint32_t)(pj >> kBrickShift)) * nbx +
+                       (uint32_t)(pi >> kBrickShift);
+    const uint32_t l = ((uint32_t)(pk & (kBrick - 1)) * kStore + (uint32_t)(pj & (kBrick - 1))) * kStore +
+                       (uint32_t)(pi & (kBrick - 1));
+    return (size_t)b * (size_t)kBrickElems + l;
 }
 
 // Trilinear filter of a 2x2x2 cell given its voxels v[dz][dy][dx]: lerp x, then y, then z
@@ -52,22 +72,92 @@ __device__ __forceinline__ float tri8(float v000, float v100, float v010, float 
     return lerpf(c0, c1, az);
 }
 
-// The 8 voxels of the cell whose low corner is at p (x-pairs are adjacent: the compiler
-// fuses each pair into one global_load_dwordx2 for f32).
+// Component c of a yz-quad element held in 32-bit words w (c: 0 (y,z), 1 (y,z+1), 2 (y+1,z),
+// 3 (y+1,z+1)); float(v) is exact for 8/16-bit voxels.
+template <typename VT>
+__device__ __forceinline__ float qc(const uint32_t *w, int c)
+{
+    if constexpr (sizeof(VT) == 1) {
+        const uint32_t b = (w[0] >> (8 * c)) & 0xFFu;
+        if constexpr (std::is_signed<VT>::value) return (float)(int)(int8_t)b;
+        return (float)b;
+    } else {
+        const uint32_t h = (w[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
+        if constexpr (std::is_signed<VT>::value) return (float)(int)(int16_t)h;
+        return (float)h;
+    }
+}
+
+// Load the elements at e and e + 1 (one 8-B or 16-B load) / the element at e alone.
+template <typename VT>
+__device__ __forceinline__ void quad_load2(const char *__restrict__ base, size_t e, uint32_t *w)
+{
+    const char *p = base + e * kElemBytes<VT>;
+    if constexpr (sizeof(VT) == 1) {
+        const u2a r = *reinterpret_cast<const u2a *>(p);
+        w[0] = r.x;
+        w[1] = r.y;
+    } else {
+        const u4a r = *reinterpret_cast<const u4a *>(p);
+        w[0] = r.x;
+        w[1] = r.y;
+        w[2] = r.z;
+        w[3] = r.w;
+    }
+}
+template <typename VT>
+__device__ __forceinline__ void quad_load1(const char *__restrict__ base, size_t e, uint32_t *w)
+{
+    const char *p = base + e * kElemBytes<VT>;
+    if constexpr (sizeof(VT) == 1) {
+        w[0] = *reinterpret_cast<const uint32_t *>(p);
+    } else {
+        const u2a r = *reinterpret_cast<const u2a *>(p);
+        w[0] = r.x;
+        w[1] = r.y;
+    }
+}
+__device__ __forceinline__ f4a zpair_load2(const char *__restrict__ base, size_t e)
+{
+    return *reinterpret_cast<const f4a *>(base + e * 8);
+}
+__device__ __forceinline__ f2a zpair_load1(const char *__restrict__ base, size_t e)
+{
+    return *reinterpret_cast<const f2a *>(base + e * 8);
+}
+
+// The 8 voxels of the cell whose low corner element is e:
+//   f32 z-pair: rows y and y+1, elements x and x+1 -> 2 x 16-B loads;
+//   8/16-bit yz-quad: elements x and x+1 -> 1 x 8-B (u8) / 16-B (u16) load.
 template <typename VT>
 struct Cell8 {
     float v[8];  // index dx + 2 dy + 4 dz
-    __device__ __forceinline__ void load(const VT *__restrict__ p)
+    __device__ __forceinline__ void load(const char *__restrict__ base, size_t e)
     {
-        constexpr int S = kStore, S2 = kStore * kStore;
-        v[0] = (float)p[0];
-        v[1] = (float)p[1];
-        v[2] = (float)p[S];
-        v[3] = (float)p[S + 1];
-        v[4] = (float)p[S2];
-        v[5] = (float)p[S2 + 1];
-        v[6] = (float)p[S2 + S];
-        v[7] = (float)p[S2 + S + 1];
+        if constexpr (kZPair<VT>) {
+            const f4a r0 = zpair_load2(base, e);
+            const f4a r1 = zpair_load2(base, e + kStore);
+            v[0] = r0.x;
+            v[4] = r0.y;
+            v[1] = r0.z;
+            v[5] = r0.w;
+            v[2] = r1.x;
+            v[6] = r1.y;
+            v[3] = r1.z;
+            v[7] = r1.w;
+        } else {
+            constexpr int QW = kQuadWords<VT>;
+            uint32_t w[2 * QW];
+            quad_load2<VT>(base, e, w);
+            v[0] = qc<VT>(w, 0);
+            v[4] = qc<VT>(w, 1);
+            v[2] = qc<VT>(w, 2);
+            v[6] = qc<VT>(w, 3);
+            v[1] = qc<VT>(w + QW, 0);
+            v[5] = qc<VT>(w + QW, 1);
+            v[3] = qc<VT>(w + QW, 2);
+            v[7] = qc<VT>(w + QW, 3);
+        }
     }
     __device__ __forceinline__ float tri(float ax, float ay, float az) const
     {
@@ -75,47 +165,59 @@ struct Cell8 {
     }
 };
 
-// Central-difference gradient (extension): cells one texel either side along each axis
-// share the centre cell's weights, so only 24 new voxels are needed (a 4-wide stencil per
-// axis).  The voxel one below / two above the cell may sit in the neighbouring brick (the
-// 1-voxel apron covers only +1): the per-axis deltas below pick the right brick.
-// Result is bit-identical to six independent trilinear fetches (same voxels, same ops).
+// Central-difference gradient (extension): the cells one texel either side along each axis
+// share the centre cell's weights, so only the 4-wide stencil's outer voxels are new
+// (24 voxels: 10 loads for z-pair f32, 6 for yz-quads).  Taps one element below, or two
+// above in z-pair x/y, may sit in the neighbouring brick (the apron covers +1): the per-axis
+// deltas pick that brick.  Bit-identical to six independent trilinear fetches (same voxels,
+// same operations), which is what the oracle computes.
 template <typename VT>
-__device__ __forceinline__ void gradient(const VT *__restrict__ p, const Cell8<VT> &c,
-                                         int lx, int ly, int lz, long by_stride, long bz_stride,
-                                         float ax, float ay, float az, float &gx, float &gy,
-                                         float &gz)
+__device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e,
+                                         const Cell8<VT> &c, int lx, int ly, int lz,
+                                         long by_stride, long bz_stride, float ax, float ay,
+                                         float az, float &gx, float &gy, float &gz)
 {
-    constexpr int S = kStore, S2 = kStore * kStore, B = kBrickVoxels;
-    const long dxm = lx > 0 ? -1 : (15 - B);
-    const long dxp = lx < 15 ? 2 : (B - 14);
-    const long dym = ly > 0 ? -S : (15 * S - by_stride);
-    const long dyp = ly < 15 ? 2 * S : (by_stride - 14 * S);
-    const long dzm = lz > 0 ? -S2 : (15L * S2 - bz_stride);
-    const long dzp = lz < 15 ? 2 * S2 : (bz_stride - 14L * S2);
-    const VT *__restrict__ xm = p + dxm;
-    const VT *__restrict__ xp = p + dxp;
-    const VT *__restrict__ ym = p + dym;
-    const VT *__restrict__ yp = p + dyp;
-    const VT *__restrict__ zm = p + dzm;
-    const VT *__restrict__ zp = p + dzp;
-    // x taps: voxels x-1 and x+2 over (dy, dz)
-    const float xm00 = (float)xm[0], xm10 = (float)xm[S], xm01 = (float)xm[S2], xm11 = (float)xm[S2 + S];
-    const float xp00 = (float)xp[0], xp10 = (float)xp[S], xp01 = (float)xp[S2], xp11 = (float)xp[S2 + S];
-    // y taps: voxels y-1 and y+2 over (dx, dz)
-    const float ym00 = (float)ym[0], ym10 = (float)ym[1], ym01 = (float)ym[S2], ym11 = (float)ym[S2 + 1];
-    const float yp00 = (float)yp[0], yp10 = (float)yp[1], yp01 = (float)yp[S2], yp11 = (float)yp[S2 + 1];
-    // z taps: voxels z-1 and z+2 over (dx, dy)
-    const float zm00 = (float)zm[0], zm10 = (float)zm[1], zm01 = (float)zm[S], zm11 = (float)zm[S + 1];
-    const float zp00 = (float)zp[0], zp10 = (float)zp[1], zp01 = (float)zp[S], zp11 = (float)zp[S + 1];
+    constexpr long S = kStore, S2 = (long)kStore * kStore, B = kBrickElems, L = kBrick - 1;
+    const long dxm = lx > 0 ? -1 : (L - B);
+    const long dxp = lx < L ? 2 : (B - (L - 1));
+    const long dym = ly > 0 ? -S : (L * S - by_stride);
+    const long dzm = lz > 0 ? -S2 : (L * S2 - bz_stride);
     const float *v = c.v;
-    // cell(i+1) uses x = {1, 2}; cell(i-1) uses x = {-1, 0}
-    gx = tri8(v[1], xp00, v[3], xp10, v[5], xp01, v[7], xp11, ax, ay, az) -
-         tri8(xm00, v[0], xm10, v[2], xm01, v[4], xm11, v[6], ax, ay, az);
-    gy = tri8(v[2], v[3], yp00, yp10, v[6], v[7], yp01, yp11, ax, ay, az) -
-         tri8(ym00, ym10, v[0], v[1], ym01, ym11, v[4], v[5], ax, ay, az);
-    gz = tri8(v[4], v[5], v[6], v[7], zp00, zp10, zp01, zp11, ax, ay, az) -
-         tri8(zm00, zm10, zm01, zm11, v[0], v[1], v[2], v[3], ax, ay, az);
+    if constexpr (kZPair<VT>) {
+        const long dyp = ly < L ? 2 * S : (by_stride - (L - 1) * S);
+        const f2a xm0 = zpair_load1(base, e + dxm), xm1 = zpair_load1(base, e + dxm + S);
+        const f2a xp0 = zpair_load1(base, e + dxp), xp1 = zpair_load1(base, e + dxp + S);
+        const f4a ym = zpair_load2(base, e + dym), yp = zpair_load2(base, e + dyp);
+        const f4a zm0 = zpair_load2(base, e + dzm), zm1 = zpair_load2(base, e + dzm + S);
+        const f4a zp0 = zpair_load2(base, e + S2), zp1 = zpair_load2(base, e + S2 + S);
+        gx = tri8(v[1], xp0.x, v[3], xp1.x, v[5], xp0.y, v[7], xp1.y, ax, ay, az) -
+             tri8(xm0.x, v[0], xm1.x, v[2], xm0.y, v[4], xm1.y, v[6], ax, ay, az);
+        gy = tri8(v[2], v[3], yp.x, yp.z, v[6], v[7], yp.y, yp.w, ax, ay, az) -
+             tri8(ym.x, ym.z, v[0], v[1], ym.y, ym.w, v[4], v[5], ax, ay, az);
+        gz = tri8(v[4], v[5], v[6], v[7], zp0.y, zp0.w, zp1.y, zp1.w, ax, ay, az) -
+             tri8(zm0.x, zm0.z, zm1.x, zm1.z, v[0], v[1], v[2], v[3], ax, ay, az);
+    } else {
+        constexpr int QW = kQuadWords<VT>;
+        uint32_t xm[QW], xp[QW], ym[2 * QW], yp[2 * QW], zm[2 * QW], zp[2 * QW];
+        quad_load1<VT>(base, e + dxm, xm);
+        quad_load1<VT>(base, e + dxp, xp);
+        quad_load2<VT>(base, e + dym, ym);  // elements (x, y-1), (x+1, y-1)
+        quad_load2<VT>(base, e + S, yp);    // elements (x, y+1), (x+1, y+1): comps 2,3 = y+2
+        quad_load2<VT>(base, e + dzm, zm);  // elements (x, y, z-1), (x+1, y, z-1)
+        quad_load2<VT>(base, e + S2, zp);   // elements (x, y, z+1), (x+1, ...): comps 1,3 = z+2
+        gx = tri8(v[1], qc<VT>(xp, 0), v[3], qc<VT>(xp, 2), v[5], qc<VT>(xp, 1), v[7], qc<VT>(xp, 3),
+                  ax, ay, az) -
+             tri8(qc<VT>(xm, 0), v[0], qc<VT>(xm, 2), v[2], qc<VT>(xm, 1), v[4], qc<VT>(xm, 3), v[6],
+                  ax, ay, az);
+        gy = tri8(v[2], v[3], qc<VT>(yp, 2), qc<VT>(yp + QW, 2), v[6], v[7], qc<VT>(yp, 3),
+                  qc<VT>(yp + QW, 3), ax, ay, az) -
+             tri8(qc<VT>(ym, 0), qc<VT>(ym + QW, 0), v[0], v[1], qc<VT>(ym, 1), qc<VT>(ym + QW, 1),
+                  v[4], v[5], ax, ay, az);
+        gz = tri8(v[4], v[5], v[6], v[7], qc<VT>(zp, 1), qc<VT>(zp + QW, 1), qc<VT>(zp, 3),
+                  qc<VT>(zp + QW, 3), ax, ay, az) -
+             tri8(qc<VT>(zm, 0), qc<VT>(zm + QW, 0), qc<VT>(zm, 2), qc<VT>(zm + QW, 2), v[0], v[1],
+                  v[2], v[3], ax, ay, az);
+    }
 }
 
 __device__ __forceinline__ void texel_coord(float p, float n, int &i, float &a)
@@ -251,8 +353,8 @@ __global__ __launch_bounds__(kThreads) void march_kernel(const MarchParams P)
     if (tf_in_lds)
         for (int i = tid; i < P.tf_n; i += kThreads) s_tf[i] = P.tf[i];
     __syncthreads();
-    const long by_stride = (long)P.nbx * kBrickVoxels;
-    const long bz_stride = (long)P.nbx * P.nby * kBrickVoxels;
+    const long by_stride = (long)P.nbx * kBrickElems;  // elements between brick rows/slabs
+    const long bz_stride = (long)P.nbx * P.nby * kBrickElems;
 
     const int wave = tid >> 6, lane = tid & 63;
     const uint32_t px = tile_x * kTile + (wave & 1) * 8 + (lane & 7);
@@ -267,7 +369,7 @@ __global__ __launch_bounds__(kThreads) void march_kernel(const MarchParams P)
 
     float T = 1.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f;
     unsigned long long n_samples = 0, n_shaded = 0, n_steps = 0;
-    const VT *__restrict__ vol = static_cast<const VT *>(P.vol);
+    const char *__restrict__ vol = static_cast<const char *>(P.vol);
     const int nsteps = covered ? P.nsteps : 0;
     float p0 = tex[0], p1 = tex[1], p2 = tex[2];
     const float d0 = dir[0], d1 = dir[1], d2 = dir[2];
@@ -284,9 +386,9 @@ __global__ __launch_bounds__(kThreads) void march_kernel(const MarchParams P)
             texel_coord(p1, P.fny, j, ay);
             texel_coord(p2, P.fnz, k, az);
             const int pi = i + kPad, pj = j + kPad, pk = k + kPad;
-            const VT *__restrict__ cp = vol + cell_offset(pi, pj, pk, P.nbx, P.nby);
+            const size_t ce = cell_offset(pi, pj, pk, P.nbx, P.nby);
             Cell8<VT> c;
-            c.load(cp);
+            c.load(vol, ce);
             const float d = c.tri(ax, ay, az);
             const float tt = (d - P.vmin) / P.range;
             float4 s = tf_in_lds ? tf_lookup(s_tf, P.tf_n, P.tf_nf, tt)
@@ -294,7 +396,8 @@ __global__ __launch_bounds__(kThreads) void march_kernel(const MarchParams P)
             if (COUNT) ++n_samples;
             if (SHADE && s.w > 0.0f) {
                 float gx, gy_, gz;
-                gradient(cp, c, pi & 15, pj & 15, pk & 15, by_stride, bz_stride, ax, ay, az, gx,
+                gradient<VT>(vol, ce, c, pi & (kBrick - 1), pj & (kBrick - 1), pk & (kBrick - 1),
+                             by_stride, bz_stride, ax, ay, az, gx,
                          gy_, gz);
                 if (COUNT) ++n_shaded;
                 const float wx = gx * P.fnx, wy = gy_ * P.fny, wz = gz * P.fnz;
@@ -355,32 +458,45 @@ __global__ __launch_bounds__(kThreads) void march_kernel(const MarchParams P)
     }
 }
 
-// ---- volume ingest: linear (any NRRD element type) -> bricked storage ----------------------
+// ---- volume ingest: linear (any NRRD element type) -> bricked paired elements -------------
 
+// One thread per stored element: padded element coordinates -> the 2 (z-pair) or 4 (yz-quad)
+// voxels it holds, 0 outside the logical volume (border).
 template <typename SrcT, typename DstT>
 __global__ __launch_bounds__(256) void brick_kernel(const SrcT *__restrict__ src,
                                                     DstT *__restrict__ dst, uint32_t nx,
                                                     uint32_t ny, uint32_t nz, uint32_t nbx,
                                                     uint32_t nby, size_t total)
 {
+    constexpr bool zpair = std::is_same<DstT, float>::value;
     for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
          g += (size_t)gridDim.x * blockDim.x) {
-        const size_t bidx = g / kBrickVoxels;
-        const uint32_t l = (uint32_t)(g - bidx * kBrickVoxels);
+        const size_t bidx = g / kBrickElems;
+        const uint32_t l = (uint32_t)(g - bidx * kBrickElems);
         const uint32_t lx = l % kStore, lyz = l / kStore, lyy = lyz % kStore, lz = lyz / kStore;
         const uint32_t bx = (uint32_t)(bidx % nbx), byz = (uint32_t)(bidx / nbx);
         const uint32_t by = byz % nby, bz = byz / nby;
         const long x = (long)bx * kBrick + lx - kPad;
         const long y = (long)by * kBrick + lyy - kPad;
         const long z = (long)bz * kBrick + lz - kPad;
-        DstT v = (DstT)0;
-        if (x >= 0 && y >= 0 && z >= 0 && x < (long)nx && y < (long)ny && z < (long)nz)
-            v = (DstT)src[(size_t)x + (size_t)nx * ((size_t)y + (size_t)ny * (size_t)z)];
-        dst[g] = v;
+        auto at = [&](long xx, long yy, long zz) -> DstT {
+            if (xx < 0 || yy < 0 || zz < 0 || xx >= (long)nx || yy >= (long)ny || zz >= (long)nz)
+                return (DstT)0;
+            return (DstT)src[(size_t)xx + (size_t)nx * ((size_t)yy + (size_t)ny * (size_t)zz)];
+        };
+        if constexpr (zpair) {
+            dst[2 * g + 0] = at(x, y, z);
+            dst[2 * g + 1] = at(x, y, z + 1);
+        } else {
+            dst[4 * g + 0] = at(x, y, z);
+            dst[4 * g + 1] = at(x, y, z + 1);
+            dst[4 * g + 2] = at(x, y + 1, z);
+            dst[4 * g + 3] = at(x, y + 1, z + 1);
+        }
     }
 }
 
-// ---- synthetic volumes generated in place (multi-GiB configs) ------------------------------
+// ---- synthetic volumes (multi-GiB configs): generated linear, then bricked --------------------
 
 __device__ __forceinline__ float hash01(uint32_t x, uint32_t y, uint32_t z)
 {
@@ -408,39 +524,29 @@ __device__ __forceinline__ DstT to_storage(float v)
 // value = out_scale * (sum_g amp exp(-k |x - c|^2) + noise_amp * hash01(x,y,z)).
 template <typename DstT>
 __global__ __launch_bounds__(256) void generate_kernel(DstT *__restrict__ dst, uint32_t nx,
-                                                       uint32_t ny, uint32_t nz, uint32_t nbx,
-                                                       uint32_t nby, size_t total,
+                                                       uint32_t ny, size_t total,
                                                        const float *__restrict__ prm)
 {
     const int ng = (int)prm[0];
     const float noise = prm[1], scale = prm[2];
     for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
          g += (size_t)gridDim.x * blockDim.x) {
-        const size_t bidx = g / kBrickVoxels;
-        const uint32_t l = (uint32_t)(g - bidx * kBrickVoxels);
-        const uint32_t lx = l % kStore, lyz = l / kStore, lyy = lyz % kStore, lz = lyz / kStore;
-        const uint32_t bx = (uint32_t)(bidx % nbx), byz = (uint32_t)(bidx / nbx);
-        const uint32_t by = byz % nby, bz = byz / nby;
-        const long x = (long)bx * kBrick + lx - kPad;
-        const long y = (long)by * kBrick + lyy - kPad;
-        const long z = (long)bz * kBrick + lz - kPad;
-        DstT v = (DstT)0;
-        if (x >= 0 && y >= 0 && z >= 0 && x < (long)nx && y < (long)ny && z < (long)nz) {
-            const float fx = (float)x, fy = (float)y, fz = (float)z;
-            float acc = 0.0f;
-            for (int q = 0; q < ng; ++q) {
-                const float *c = prm + 3 + 5 * q;
-                const float dx = fx - c[0], dy = fy - c[1], dz = fz - c[2];
-                acc += c[4] * __expf(-c[3] * (dx * dx + dy * dy + dz * dz));
-            }
-            acc += noise * hash01((uint32_t)x, (uint32_t)y, (uint32_t)z);
-            v = to_storage<DstT>(acc * scale);
+        const uint32_t x = (uint32_t)(g % nx);
+        const size_t yz = g / nx;
+        const uint32_t y = (uint32_t)(yz % ny), z = (uint32_t)(yz / ny);
+        const float fx = (float)x, fy = (float)y, fz = (float)z;
+        float acc = 0.0f;
+        for (int q = 0; q < ng; ++q) {
+            const float *c = prm + 3 + 5 * q;
+            const float dx = fx - c[0], dy = fy - c[1], dz = fz - c[2];
+            acc += c[4] * __expf(-c[3] * (dx * dx + dy * dy + dz * dz));
         }
-        dst[g] = v;
+        acc += noise * hash01(x, y, z);
+        dst[g] = to_storage<DstT>(acc * scale);
     }
 }
 
-// ---- min/max over logical voxels (generated volumes) ----------------------------------------
+// ---- min/max over a linear buffer -------------------------------------------------------------
 
 __device__ __forceinline__ uint32_t ordered(float f)
 {
@@ -449,19 +555,13 @@ __device__ __forceinline__ uint32_t ordered(float f)
 }
 
 template <typename VT>
-__global__ __launch_bounds__(256) void minmax_kernel(const VT *__restrict__ vol, uint32_t nx,
-                                                     uint32_t ny, uint32_t nz, uint32_t nbx,
-                                                     uint32_t nby, uint32_t *out)
+__global__ __launch_bounds__(256) void minmax_kernel(const VT *__restrict__ vol, size_t total,
+                                                     uint32_t *out)
 {
-    const size_t total = (size_t)nx * ny * nz;
     uint32_t lo = 0xFFFFFFFFu, hi = 0u;
     for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
          g += (size_t)gridDim.x * blockDim.x) {
-        const uint32_t x = (uint32_t)(g % nx);
-        const size_t yz = g / nx;
-        const uint32_t y = (uint32_t)(yz % ny), z = (uint32_t)(yz / ny);
-        const float v = (float)vol[cell_offset((int)x + kPad, (int)y + kPad, (int)z + kPad, nbx, nby)];
-        const uint32_t o = ordered(v);
+        const uint32_t o = ordered((float)vol[g]);
         lo = o < lo ? o : lo;
         hi = o > hi ? o : hi;
     }
@@ -525,7 +625,7 @@ hipError_t brick_from(const void *src, void *dst, uint32_t nx, uint32_t ny, uint
                       int storage, hipStream_t s)
 {
     const uint32_t nbx = bricks_for(nx), nby = bricks_for(ny), nbz = bricks_for(nz);
-    const size_t total = (size_t)nbx * nby * nbz * kBrickVoxels;
+    const size_t total = (size_t)nbx * nby * nbz * kBrickElems;  // elements
     const SrcT *sp = static_cast<const SrcT *>(src);
     switch (storage) {
         case ST_U8: hipLaunchKernelGGL((brick_kernel<SrcT, uint8_t>), dim3(grid_for(total)), dim3(256), 0, s, sp, (uint8_t *)dst, nx, ny, nz, nbx, nby, total); break;
@@ -593,30 +693,27 @@ hipError_t launch_generate(int kind, int storage, void *dst, uint32_t nx, uint32
 {
     (void)nparams;
     if (kind != 0) return hipErrorInvalidValue;
-    const uint32_t nbx = bricks_for(nx), nby = bricks_for(ny), nbz = bricks_for(nz);
-    const size_t total = (size_t)nbx * nby * nbz * kBrickVoxels;
+    const size_t total = (size_t)nx * ny * nz;
     switch (storage) {
-        case ST_U8: hipLaunchKernelGGL((generate_kernel<uint8_t>), dim3(grid_for(total)), dim3(256), 0, s, (uint8_t *)dst, nx, ny, nz, nbx, nby, total, params_dev); break;
-        case ST_U16: hipLaunchKernelGGL((generate_kernel<uint16_t>), dim3(grid_for(total)), dim3(256), 0, s, (uint16_t *)dst, nx, ny, nz, nbx, nby, total, params_dev); break;
-        case ST_F32: hipLaunchKernelGGL((generate_kernel<float>), dim3(grid_for(total)), dim3(256), 0, s, (float *)dst, nx, ny, nz, nbx, nby, total, params_dev); break;
+        case ST_U8: hipLaunchKernelGGL((generate_kernel<uint8_t>), dim3(grid_for(total)), dim3(256), 0, s, (uint8_t *)dst, nx, ny, total, params_dev); break;
+        case ST_U16: hipLaunchKernelGGL((generate_kernel<uint16_t>), dim3(grid_for(total)), dim3(256), 0, s, (uint16_t *)dst, nx, ny, total, params_dev); break;
+        case ST_F32: hipLaunchKernelGGL((generate_kernel<float>), dim3(grid_for(total)), dim3(256), 0, s, (float *)dst, nx, ny, total, params_dev); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
-hipError_t launch_minmax(int storage, const void *bricks, uint32_t nx, uint32_t ny, uint32_t nz,
-                         float *minmax_dev, hipStream_t s)
+hipError_t launch_minmax(int storage, const void *linear, size_t count, float *minmax_dev,
+                         hipStream_t s)
 {
     uint32_t *o = reinterpret_cast<uint32_t *>(minmax_dev);
-    const uint32_t nbx = bricks_for(nx), nby = bricks_for(ny);
-    const size_t total = (size_t)nx * ny * nz;
-    const unsigned g = grid_for(total);
+    const unsigned g = grid_for(count);
     switch (storage) {
-        case ST_U8: hipLaunchKernelGGL((minmax_kernel<uint8_t>), dim3(g), dim3(256), 0, s, (const uint8_t *)bricks, nx, ny, nz, nbx, nby, o); break;
-        case ST_I8: hipLaunchKernelGGL((minmax_kernel<int8_t>), dim3(g), dim3(256), 0, s, (const int8_t *)bricks, nx, ny, nz, nbx, nby, o); break;
-        case ST_U16: hipLaunchKernelGGL((minmax_kernel<uint16_t>), dim3(g), dim3(256), 0, s, (const uint16_t *)bricks, nx, ny, nz, nbx, nby, o); break;
-        case ST_I16: hipLaunchKernelGGL((minmax_kernel<int16_t>), dim3(g), dim3(256), 0, s, (const int16_t *)bricks, nx, ny, nz, nbx, nby, o); break;
-        default: hipLaunchKernelGGL((minmax_kernel<float>), dim3(g), dim3(256), 0, s, (const float *)bricks, nx, ny, nz, nbx, nby, o); break;
+        case ST_U8: hipLaunchKernelGGL((minmax_kernel<uint8_t>), dim3(g), dim3(256), 0, s, (const uint8_t *)linear, count, o); break;
+        case ST_I8: hipLaunchKernelGGL((minmax_kernel<int8_t>), dim3(g), dim3(256), 0, s, (const int8_t *)linear, count, o); break;
+        case ST_U16: hipLaunchKernelGGL((minmax_kernel<uint16_t>), dim3(g), dim3(256), 0, s, (const uint16_t *)linear, count, o); break;
+        case ST_I16: hipLaunchKernelGGL((minmax_kernel<int16_t>), dim3(g), dim3(256), 0, s, (const int16_t *)linear, count, o); break;
+        default: hipLaunchKernelGGL((minmax_kernel<float>), dim3(g), dim3(256), 0, s, (const float *)linear, count, o); break;
     }
     return hipGetLastError();
 }
