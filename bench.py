@@ -31,8 +31,9 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-import vr_amd  # noqa: E402
 import synth  # noqa: E402
+import vr_amd  # noqa: E402
+import vr_dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "Gsamples/sec + fps, 512³ NRRD @ 1080p; achieved HBM GB/s vs peak"
@@ -91,7 +92,7 @@ def run_variant(rp, cfg, steps, warmup, rank, world, stream, row_block=16):
     def step():
         rp.render_device(cam, p, local.data_ptr(), vr_amd.OUT_RGBA8, row_block, rank, world, stream)
         if world > 1:
-            dist.gather(local, gathered if rank == 0 else None, dst=0)
+            vr_dist.gather_to_root(local, gathered, rank, dist)
             if rank == 0:
                 rp.assemble_rows(gbuf.data_ptr(), frame.data_ptr(), vr_amd.OUT_RGBA8, row_block, world, stream)
 
