@@ -249,6 +249,10 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_frac": (round(traffic / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                 if traffic else None),
+                "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"
+                                  if traffic else None,
                 "kernel_ms": round(kms, 4),
                 "bytes_model": "8*sizeof(voxel)/sample + 48*sizeof(voxel)/shaded sample + 4 B/pixel (SURVEY.md 8d)",
             },
