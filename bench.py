@@ -48,9 +48,15 @@ CONFIGS = {
                    shading=0, ert=0.0, seed=2024,
                    workload="C3 reference semantics: no shading, no ERT (volume.frag as written)"),
     "c2": dict(dims=(256, 256, 256), dtype=np.uint8, W=1024, H=1024, cam="fill", tf="tf2",
-               shading=0, ert=0.0, seed=1234, workload="C2: 256^3 u8, 1024x1024, trilinear + 1D TF"),
+               shading=0, ert=0.0, seed=1234, source="ct_head",
+               workload="C2: 256^3 u8 synthetic CT head, 1024x1024, trilinear + 1D TF"),
     "c4": dict(dims=(1024, 1024, 1024), dtype=np.uint8, W=2048, H=2048, cam="fill", tf="tf2",
                shading=0, ert=0.0, seed=7, workload="C4: 1024^3 u8, 2048x2048"),
+    "c1": dict(dims=(64, 64, 64), dtype=np.float32, W=256, H=256, cam="fill", tf="tf2",
+               shading=0, ert=0.0, seed=1, workload="C1: 64^3 f32, 256x256 (the CPU plumbing case)"),
+    "c5": dict(dims=(2048, 2048, 2048), dtype=np.uint8, W=4096, H=4096, cam="fill", tf="tf2",
+               shading=0, ert=0.0, seed=11,
+               workload="C5: 2048^3 u8 bricked (49.5 GB resident in HBM), 4096x4096"),
 }
 
 
@@ -63,7 +69,11 @@ def algorithmic_bytes(stats, voxel_bytes, pixels, out_bytes=4):
 
 def setup_pass(cfg, device):
     rp = vr_amd.OffscreenPass(cfg["W"], cfg["H"], device=device)
-    lo, hi = rp.generate_volume(cfg["dims"], cfg["dtype"], seed=cfg["seed"])
+    if cfg.get("source") == "ct_head":
+        # host-generated u8 CT head through the Dataset path (volume_dataset_changed)
+        rp.volume_dataset_changed(synth.dataset(synth.ct_head(cfg["dims"][0], cfg["seed"])))
+    else:
+        rp.generate_volume(cfg["dims"], cfg["dtype"], seed=cfg["seed"])
     rp.transfer_function_changed(synth.TFS[cfg["tf"]]())
     return rp
 
@@ -212,7 +222,8 @@ def main():
             roofline_frac=round(algorithmic_bytes(r2, vbytes, shard_px) / (k2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    small = int(np.prod(cfg["dims"])) <= 512 ** 3  # the oracle needs the volume as host floats
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and small:
         cpu = cpu_baseline(rp, cfg, args.cpu_budget)
 
     if rank == 0:
