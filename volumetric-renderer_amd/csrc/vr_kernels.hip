@@ -319,7 +319,10 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
 }
 
 template <typename VT, bool SHADE, bool COUNT>
-__global__ __launch_bounds__(kThreads) void march_kernel(const MarchParams P)
+#ifndef VR_MARCH_MIN_WAVES
+#define VR_MARCH_MIN_WAVES 1
+#endif
+__global__ __launch_bounds__(kThreads, VR_MARCH_MIN_WAVES) void march_kernel(const MarchParams P)
 {
     __shared__ float4 s_tf[kTfLds];
     const int tid = threadIdx.x;

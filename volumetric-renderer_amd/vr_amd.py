@@ -17,7 +17,8 @@ from typing import Optional, Sequence
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libvr_amd.so")
+# VR_AMD_LIB selects an experiment build (make LIBDIR=... EXTRA=...); default: lib/
+LIB_PATH = os.environ.get("VR_AMD_LIB") or os.path.join(HERE, "lib", "libvr_amd.so")
 
 # enum vr_dtype
 DTYPE_I8, DTYPE_U8, DTYPE_I16, DTYPE_U16, DTYPE_I32, DTYPE_U32 = 1, 2, 3, 4, 5, 6
