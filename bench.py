@@ -35,6 +35,7 @@ import synth  # noqa: E402
 import vr_amd  # noqa: E402
 import vr_dist  # noqa: E402
 
+BACKEND = "nccl"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "Gsamples/sec + fps, 512³ NRRD @ 1080p; achieved HBM GB/s vs peak"
 
@@ -78,36 +79,42 @@ def setup_pass(cfg, device):
     return rp
 
 
-def run_variant(rp, cfg, steps, warmup, rank, world, stream, row_block=16):
-    """Time `steps` frames; returns (max-over-ranks seconds, kernel ms avg, frame stats, rank0 stats)."""
+def run_variant(rp, cfg, steps, warmup, rank, world, stream, row_block=8, overlap=True):
+    """Time `steps` frames; returns (max-over-ranks seconds, avg kernel ms, frame stats,
+    this rank's stats, this rank's shard pixels).  For N > 1 a frame is: render this rank's
+    row blocks -> RCCL gather to rank 0 -> de-interleave on rank 0, with the gather of frame k
+    overlapped with the render of frame k+1 (vr_dist.FramePipeline) unless overlap=False."""
     W, H = cfg["W"], cfg["H"]
     cam = synth.camera(cfg["cam"]).to_vr_camera()
     p = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"])
     sr = vr_amd.shard_rows(H, row_block, world)
-    local = torch.empty((sr, W), dtype=torch.int32, device="cuda")
-    gathered = frame = gbuf = None
+    nbuf = 2 if (world > 1 and overlap) else 1
+    shards = [torch.empty((sr, W), dtype=torch.int32, device="cuda") for _ in range(nbuf)]
+    gbufs = frame = None
     if world > 1 and rank == 0:
-        # RCCL gathers straight into the rank-major buffer the assembly kernel reads
-        gbuf = torch.empty((world, sr, W), dtype=torch.int32, device="cuda")
-        gathered = [gbuf[r] for r in range(world)]
+        # RCCL gathers straight into the rank-major buffers the assembly kernel reads
+        gbufs = [torch.empty((world, sr, W), dtype=torch.int32, device="cuda") for _ in range(nbuf)]
         frame = torch.empty((H, W), dtype=torch.int32, device="cuda")
 
     my_stats = rp.count_work(cam, p, row_block, rank, world)
+    sdev = "cuda" if BACKEND == "nccl" else "cpu"
     tot = torch.tensor([my_stats[k] for k in ("rays", "samples", "shaded_samples", "steps")],
-                       dtype=torch.float64, device="cuda")
+                       dtype=torch.float64, device=sdev)
     if world > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     frame_stats = dict(zip(("rays", "samples", "shaded_samples", "steps"), [int(x) for x in tot.tolist()]))
 
-    def step():
-        rp.render_device(cam, p, local.data_ptr(), vr_amd.OUT_RGBA8, row_block, rank, world, stream)
-        if world > 1:
-            vr_dist.gather_to_root(local, gathered, rank, dist)
-            if rank == 0:
-                rp.assemble_rows(gbuf.data_ptr(), frame.data_ptr(), vr_amd.OUT_RGBA8, row_block, world, stream)
+    pipe = vr_dist.FramePipeline(
+        shards, gbufs, rank, world, dist,
+        render=lambda buf: rp.render_device(cam, p, buf.data_ptr(), vr_amd.OUT_RGBA8, row_block,
+                                            rank, world, stream),
+        assemble=lambda g: rp.assemble_rows(g.data_ptr(), frame.data_ptr(), vr_amd.OUT_RGBA8,
+                                            row_block, world, stream),
+        overlap=overlap, host_staging=(BACKEND != "nccl"))
 
     for _ in range(warmup):
-        step()
+        pipe.step()
+    pipe.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -118,17 +125,25 @@ def run_variant(rp, cfg, steps, warmup, rank, world, stream, row_block=16):
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
-        step()
+        pipe.step()
+    pipe.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     rp.timing_enable(False)
     kms, nl = rp.timing_read()
-    el = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
+    el = torch.tensor([t1 - t0], dtype=torch.float64, device=sdev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    return float(el.item()), kms / max(nl, 1), frame_stats, my_stats, sr * W
+    check = None
+    if world > 1 and rank == 0:
+        # the assembled frame must equal this device's single-rank render of the whole frame
+        full = torch.empty((vr_amd.shard_rows(H, row_block, 1), W), dtype=torch.int32, device="cuda")
+        rp.render_device(cam, p, full.data_ptr(), vr_amd.OUT_RGBA8, row_block, 0, 1, stream)
+        torch.cuda.synchronize()
+        check = bool(torch.equal(full[:H], frame))
+    return float(el.item()), kms / max(nl, 1), frame_stats, my_stats, sr * W, check
 
 
 def cpu_baseline(rp, cfg, budget_s=12.0):
@@ -188,23 +203,33 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--serial-gather", action="store_true",
+                    help="N > 1: wait for each frame's gather before rendering the next")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # VR_DIST_BACKEND=gloo rehearses the N > 1 path with ranks sharing devices (host-staged
+    # gathers); the real multi-GPU run uses "nccl" (RCCL over xGMI), one device per rank.
+    global BACKEND
+    BACKEND = os.environ.get("VR_DIST_BACKEND", "nccl")
+    device = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    else:
-        torch.cuda.set_device(0)
+        if BACKEND == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(BACKEND)
     stream = torch.cuda.current_stream().cuda_stream
 
     cfg = CONFIGS[args.config]
-    rp = setup_pass(cfg, local_rank)
+    rp = setup_pass(cfg, device)
     vbytes = np.dtype(cfg["dtype"]).itemsize
 
-    secs, kms, fstats, r0stats, shard_px = run_variant(rp, cfg, args.steps, args.warmup, rank, world, stream)
+    overlap = not args.serial_gather
+    secs, kms, fstats, r0stats, shard_px, frame_check = run_variant(rp, cfg, args.steps, args.warmup, rank, world,
+                                                       stream, overlap=overlap)
     value = fstats["samples"] * args.steps / secs / 1e9
     fps = args.steps / secs
     achieved = algorithmic_bytes(r0stats, vbytes, shard_px) / (kms * 1e-3) / 1e9
@@ -214,7 +239,8 @@ def main():
     if not args.no_variants and args.config == "c3":
         vcfg = CONFIGS["c3_ref"]
         rp.transfer_function_changed(synth.TFS[vcfg["tf"]]())
-        s2, k2, f2, r2, _ = run_variant(rp, vcfg, args.steps, min(args.warmup, 5), rank, world, stream)
+        s2, k2, f2, r2, _, _ = run_variant(rp, vcfg, args.steps, min(args.warmup, 5), rank, world, stream,
+                                        overlap=overlap)
         variants["reference_semantics_no_shading_no_ert"] = dict(
             value=round(f2["samples"] * args.steps / s2 / 1e9, 3), unit="Gsamples/s",
             fps=round(args.steps / s2, 2), samples_per_frame=f2["samples"],
@@ -247,7 +273,9 @@ def main():
                 "viewport": f"{cfg['W']}x{cfg['H']}",
                 "camera": synth.CAMERAS[cfg["cam"]],
                 "tf": cfg["tf"], "shading": cfg["shading"], "ert_eps": cfg["ert"],
-                "parallelism": f"image row-blocks x{world}" + (" + RCCL gather" if world > 1 else ""),
+                "parallelism": f"image 8-row blocks cyclic x{world}" + (
+                    (" + RCCL gather (overlapped with next frame)" if overlap else " + RCCL gather (serial)")
+                    if world > 1 else ""),
                 "samples_per_frame": fstats["samples"],
                 "shaded_samples_per_frame": fstats["shaded_samples"],
                 "rays_per_frame": fstats["rays"],
@@ -268,6 +296,7 @@ def main():
                 "bytes_model": "8*sizeof(voxel)/sample + 48*sizeof(voxel)/shaded sample + 4 B/pixel (SURVEY.md 8d)",
             },
             "cpu_baseline": cpu,
+            "frame_check": frame_check,  # N > 1: assembled frame == single-GPU frame, bit for bit
             "variants": variants,
         }
         print(json.dumps(out), flush=True)

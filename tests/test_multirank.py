@@ -22,18 +22,18 @@ def _free_port():
     return p
 
 
-def _scene(W, H):
+def _scene(W, H, k=0):
     import pyoracle
     import synth
     import vr_amd
     vol = synth.gaussians_numpy((16, 14, 12), seed=3)
-    cam = synth.camera("rotA").to_vr_camera()
+    cam = vr_amd.make_camera(radius=2.0, rotate=(100.0 + 37.0 * k, 60.0 - 11.0 * k)).to_vr_camera()
     p = vr_amd.default_params(shading=1)
     return pyoracle.Scene.from_params(vol, float(vol.min()), float(vol.max()), synth.tf_color(),
                                       cam, W, H, p)
 
 
-def _worker(rank, world, port, W, H, rb, q):
+def _worker(rank, world, port, W, H, rb, overlap, nframes, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for sub in ("volumetric-renderer_amd", "oracle", "tools"):
@@ -42,42 +42,60 @@ def _worker(rank, world, port, W, H, rb, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        sc = _scene(W, H)
         rows = vr_dist.shard_global_rows(H, rb, rank, world)
-        img, st = sc.render_rows(rows[rows >= 0], nthreads=2)
-        shard = np.zeros((len(rows), W, 4), np.float32)
-        shard[rows >= 0] = img[rows[rows >= 0]]
-        local = torch.from_numpy(shard)
-        views = None
-        if rank == 0:
-            buf = torch.empty((world,) + tuple(local.shape), dtype=local.dtype)
-            views = [buf[r] for r in range(world)]
-        vr_dist.gather_to_root(local, views, rank, dist)
-        samples = torch.tensor([st["samples"]], dtype=torch.int64)
+        sr = len(rows)
+        nbuf = 2 if overlap else 1
+        shards = [torch.zeros((sr, W, 4), dtype=torch.float32) for _ in range(nbuf)]
+        gbufs = [torch.zeros((world, sr, W, 4), dtype=torch.float32) for _ in range(nbuf)] if rank == 0 else None
+        frames, state = [], {"k": 0, "samples": 0}
+
+        def render(buf):
+            img, st = _scene(W, H, state["k"]).render_rows(rows[rows >= 0], nthreads=2)
+            shard = np.zeros((sr, W, 4), np.float32)
+            shard[rows >= 0] = img[rows[rows >= 0]]
+            buf.copy_(torch.from_numpy(shard))
+            state["samples"] += st["samples"]
+            state["k"] += 1
+
+        def assemble(g):
+            frames.append(vr_dist.assemble_numpy(g.numpy().copy(), H, rb, world))
+
+        pipe = vr_dist.FramePipeline(shards, gbufs, rank, world, dist, render, assemble, overlap=overlap)
+        for _ in range(nframes):
+            pipe.step()
+        pipe.drain()
+        samples = torch.tensor([state["samples"]], dtype=torch.int64)
         dist.all_reduce(samples)
         if rank == 0:
-            frame = vr_dist.assemble_numpy(buf.numpy(), H, rb, world)
-            q.put((frame, int(samples.item())))
+            q.put((frames, int(samples.item())))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,rb", [(2, 16), (2, 4), (3, 8)])
-def test_gloo_sharded_frame_matches_single_process(world, rb):
-    W, H = 40, 45
+@pytest.mark.parametrize("world,rb,overlap", [(2, 16, True), (2, 4, False), (3, 8, True)])
+def test_gloo_sharded_frames_match_single_process(world, rb, overlap):
+    """N ranks, 3 frames through vr_dist.FramePipeline (the benchmark's frame loop): every
+    assembled frame equals the single-process oracle frame bit for bit, with and without
+    the gather of frame k overlapped with the render of frame k+1."""
+    W, H, nframes = 40, 45, 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, rb, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, rb, overlap, nframes, q))
+             for r in range(world)]
     for p in procs:
         p.start()
-    frame, samples = q.get(timeout=120)
+    frames, samples = q.get(timeout=180)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    full, st = _scene(W, H).render()
-    assert np.array_equal(frame, full)
-    assert samples == st["samples"]
+    assert len(frames) == nframes
+    total = 0
+    for k in range(nframes):
+        full, st = _scene(W, H, k).render()
+        assert np.array_equal(frames[k], full), k
+        total += st["samples"]
+    assert samples == total
 
 
 def test_shard_layout_is_a_partition():

@@ -21,9 +21,12 @@ namespace vr {
 //         4 B (u8/i8) or 8 B (u16/i16); a sample = 1 load of elements x, x+1 (8 B / 16 B).
 // Voxels outside [0, N) are stored as 0: CLAMP_TO_BORDER/TRANSPARENT_BLACK without a bounds
 // test.  Memory: 2 x (9/8)^3 = 2.85x the f32 voxels, 4 x (9/8)^3 = 5.7x the 8/16-bit voxels.
-constexpr int kBrick = 8;
-constexpr int kBrickShift = 3;
-constexpr int kStore = 9;
+#ifndef VR_BRICK_SHIFT
+#define VR_BRICK_SHIFT 3  // 8^3 bricks (experiment builds may use 4: 16^3)
+#endif
+constexpr int kBrickShift = VR_BRICK_SHIFT;
+constexpr int kBrick = 1 << kBrickShift;
+constexpr int kStore = kBrick + 1;
 constexpr int kBrickElems = kStore * kStore * kStore;  // 729
 constexpr int kPad = 2;
 

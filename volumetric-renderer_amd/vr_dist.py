@@ -37,6 +37,74 @@ def assemble_numpy(gathered: np.ndarray, height: int, row_block: int, nranks: in
     return gathered[rank, ly]
 
 
-def gather_to_root(local, gathered_views, rank: int, dist) -> None:
+def gather_to_root(local, gathered_views, rank: int, dist, async_op: bool = False):
     """One gather per frame of every rank's shard into rank 0's rank-major buffer views."""
-    dist.gather(local, gathered_views if rank == 0 else None, dst=0)
+    return dist.gather(local, gathered_views if rank == 0 else None, dst=0, async_op=async_op)
+
+
+class FramePipeline:
+    """Per-frame render -> gather -> assemble with the gather of frame k overlapped with the
+    render of frame k+1 (double-buffered shards and gather buffers).
+
+    `render(buf)` enqueues this rank's shard of the next frame into `buf`; `assemble(gbuf)`
+    (rank 0) enqueues the de-interleave of a gathered rank-major buffer.  With overlap, the
+    gather is issued async_op=True and only waited for (work.wait(): a stream wait for
+    NCCL/RCCL, a host wait for gloo) one frame later, right before that frame is assembled
+    and before its shard buffer is rendered into again.  overlap=False is the serial form.
+    """
+
+    def __init__(self, shards, gather_bufs, rank, world, dist, render, assemble, overlap=True,
+                 host_staging=False):
+        self.shards = shards            # list of 1 or 2 local shard tensors
+        self.gather_bufs = gather_bufs  # rank 0: list of (world, rows, W) tensors, else None
+        self.rank, self.world, self.dist = rank, world, dist
+        self.render, self.assemble = render, assemble
+        # host_staging: device shards gathered through host copies (gloo rehearsal of the
+        # multi-GPU path on one device); always serial
+        self.host_staging = host_staging
+        self.overlap = overlap and world > 1 and len(shards) > 1 and not host_staging
+        self.k = 0
+        self.pending = None
+
+    def _views(self, i):
+        if self.rank != 0:
+            return None
+        g = self.gather_bufs[i]
+        return [g[r] for r in range(self.world)]
+
+    def _finish(self, work, i):
+        work.wait()
+        if self.rank == 0:
+            self.assemble(self.gather_bufs[i])
+
+    def step(self):
+        i = self.k % len(self.shards)
+        self.k += 1
+        buf = self.shards[i]
+        self.render(buf)
+        if self.world == 1:
+            return
+        gi = i % len(self.gather_bufs) if self.rank == 0 else 0
+        if self.host_staging:
+            host = buf.cpu()
+            hviews = None
+            if self.rank == 0:
+                hg = self.gather_bufs[gi].cpu()
+                hviews = [hg[r] for r in range(self.world)]
+            gather_to_root(host, hviews, self.rank, self.dist)
+            if self.rank == 0:
+                self.gather_bufs[gi].copy_(hg)
+                self.assemble(self.gather_bufs[gi])
+            return
+        work = gather_to_root(buf, self._views(gi), self.rank, self.dist, async_op=True)
+        if not self.overlap:
+            self._finish(work, gi)
+            return
+        if self.pending is not None:
+            self._finish(*self.pending)
+        self.pending = (work, gi)
+
+    def drain(self):
+        if self.pending is not None:
+            self._finish(*self.pending)
+            self.pending = None
