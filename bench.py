@@ -86,7 +86,8 @@ def run_variant(rp, cfg, steps, warmup, rank, world, stream, row_block=8, overla
     overlapped with the render of frame k+1 (vr_dist.FramePipeline) unless overlap=False."""
     W, H = cfg["W"], cfg["H"]
     cam = synth.camera(cfg["cam"]).to_vr_camera()
-    p = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"])
+    p = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"],
+                              skip_empty=cfg.get("skip_empty", 0))
     sr = vr_amd.shard_rows(H, row_block, world)
     nbuf = 2 if (world > 1 and overlap) else 1
     shards = [torch.empty((sr, W), dtype=torch.int32, device="cuda") for _ in range(nbuf)]
@@ -98,11 +99,11 @@ def run_variant(rp, cfg, steps, warmup, rank, world, stream, row_block=8, overla
 
     my_stats = rp.count_work(cam, p, row_block, rank, world)
     sdev = "cuda" if BACKEND == "nccl" else "cpu"
-    tot = torch.tensor([my_stats[k] for k in ("rays", "samples", "shaded_samples", "steps")],
-                       dtype=torch.float64, device=sdev)
+    keys = ("rays", "samples", "shaded_samples", "steps", "skipped_samples")
+    tot = torch.tensor([my_stats[k] for k in keys], dtype=torch.float64, device=sdev)
     if world > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-    frame_stats = dict(zip(("rays", "samples", "shaded_samples", "steps"), [int(x) for x in tot.tolist()]))
+    frame_stats = dict(zip(keys, [int(x) for x in tot.tolist()]))
 
     pipe = vr_dist.FramePipeline(
         shards, gbufs, rank, world, dist,
@@ -246,6 +247,19 @@ def main():
             fps=round(args.steps / s2, 2), samples_per_frame=f2["samples"],
             kernel_ms=round(k2, 4),
             roofline_frac=round(algorithmic_bytes(r2, vbytes, shard_px) / (k2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+        # opt-in empty-space skipping (bit-identical frames): executed samples drop, so it is
+        # reported as fps and as reference-equivalent samples/s, never as the headline value
+        scfg = dict(CONFIGS["c3"], skip_empty=1)
+        rp.transfer_function_changed(synth.TFS[scfg["tf"]]())
+        s3, k3, f3, r3, _, _ = run_variant(rp, scfg, args.steps, min(args.warmup, 5), rank, world, stream,
+                                        overlap=overlap)
+        variants["c3_skip_empty"] = dict(
+            fps=round(args.steps / s3, 2), ms_per_step=round(s3 / args.steps * 1e3, 4),
+            kernel_ms=round(k3, 4),
+            executed_gsamples_per_s=round(f3["samples"] * args.steps / s3 / 1e9, 3),
+            reference_equivalent_gsamples_per_s=round(
+                (f3["samples"] + f3["skipped_samples"]) * args.steps / s3 / 1e9, 3),
+            samples_per_frame=f3["samples"], skipped_samples_per_frame=f3["skipped_samples"])
 
     cpu = None
     small = int(np.prod(cfg["dims"])) <= 512 ** 3  # the oracle needs the volume as host floats

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 1
+#define VR_ABI_VERSION 2
 
 /* ---- status codes (negative errno style) ---- */
 #define VR_OK 0
@@ -101,7 +101,13 @@ typedef struct vr_params {
      * 0 auto, 1 raster (consecutive tiles round-robin over the 8 XCDs), 2 XCD bands (each
      * XCD a contiguous band of rows), 3 XCD-interleaved 64x64-pixel super-tiles. */
     int32_t tile_order;
-    int32_t reserved[3];
+    /* 1: skip the trilinear fetch of samples proven fully transparent: the sample's cell lies
+     * in an 8^3 brick whose stored value range (widened by a rounding margin) maps only to TF
+     * texels with alpha 0.  Such a sample composites to exactly nothing (C += rgb*0*T,
+     * T *= 1 - 0), so the frame is bit-identical to skip_empty = 0 (DESIGN.md "Empty-space
+     * skipping").  The brick classification is rebuilt lazily after a volume or TF change. */
+    int32_t skip_empty;
+    int32_t reserved[2];
 } vr_params;
 
 /* Work counters of one frame (filled by vr_count_work). */
@@ -110,6 +116,8 @@ typedef struct vr_stats {
     uint64_t samples;         /* executed density samples (trilinear fetches in slab) */
     uint64_t shaded_samples;  /* samples that also took the 6-tap gradient            */
     uint64_t steps;           /* loop iterations taken (incl. out-of-slab steps)      */
+    uint64_t skipped_samples; /* in-slab samples not fetched (skip_empty): samples +
+                                 skipped_samples = the reference's sample count          */
 } vr_stats;
 
 /* ---- lifecycle ---- */

@@ -125,7 +125,7 @@ class Scene:
         if rc != 0:
             raise RuntimeError(f"or_render_rows failed ({rc})")
         return out, dict(rays=st.rays, samples=st.samples, shaded_samples=st.shaded_samples,
-                         steps=st.steps)
+                         steps=st.steps, skipped_samples=0)  # the reference never skips
 
     def render_rows(self, rows, out=None, nthreads=0):
         """Render an arbitrary list of rows (OpenMP over the list) into `out` (H, W, 4)."""
@@ -139,7 +139,7 @@ class Scene:
         if rc != 0:
             raise RuntimeError(f"or_render_row_list failed ({rc})")
         return out, dict(rays=st.rays, samples=st.samples, shaded_samples=st.shaded_samples,
-                         steps=st.steps)
+                         steps=st.steps, skipped_samples=0)  # the reference never skips
 
     def pixel_ray(self, px, py):
         tex = np.zeros(3, np.float32)

@@ -149,7 +149,7 @@ def test_row_block_sharding_assembles_exactly(rp):
         torch.cuda.synchronize()
         assert torch.equal(out, full), (nranks, rb)
         # shards' work sums to the frame's work
-        tot = {k: 0 for k in ("rays", "samples", "shaded_samples", "steps")}
+        tot = {k: 0 for k in ("rays", "samples", "shaded_samples", "steps", "skipped_samples")}
         for r in range(nranks):
             for k, v in rp.count_work(cam, p, rb, r, nranks).items():
                 tot[k] += v
@@ -288,3 +288,100 @@ def test_determinism_and_ert_bound(rp):
     assert np.abs(e.astype(np.float64) - a).max() <= 2 * eps * 1.25 + 1e-6
     assert rp.count_work(cam, vr_amd.default_params(shading=1, ert_eps=eps))["samples"] < \
         rp.count_work(cam, p0)["samples"]
+
+
+SKIP_CASES = [
+    # (volume dtype, tf, shading, slice, ert)
+    (np.float32, "tf2", 1, None, 1e-5),
+    (np.float32, "tfband", 0, ((0.2, 0.0, 0.1), (0.8, 1.0, 0.9)), 0.0),
+    (np.uint8, "tf2", 0, None, 0.0),
+    (np.uint16, "tfband", 1, None, 0.0),
+    (np.int16, "tf2", 1, ((0.1, 0.1, 0.1), (0.9, 0.7, 1.0)), 1e-3),
+]
+
+
+def _as_dtype(base, np_dtype):
+    if np_dtype == np.float32:
+        return base.astype(np.float32)
+    info = np.iinfo(np_dtype)
+    lo, hi = max(info.min, -20000), min(info.max, 40000)
+    return (lo + (base / base.max()) * (hi - lo)).round().astype(np_dtype)
+
+
+@pytest.mark.parametrize("case", SKIP_CASES,
+                         ids=[f"{np.dtype(c[0]).name}-{c[1]}-s{c[2]}-e{c[4]}" for c in SKIP_CASES])
+def test_skip_empty_is_bit_identical(rp, case):
+    """skip_empty = 1 leaves every pixel bit-identical (alpha-0 samples composite to nothing)
+    and only moves samples from `samples` to `skipped_samples`; the frame still matches the
+    oracle."""
+    np_dtype, tfname, shading, sl, ert = case
+    vol = _as_dtype(synth.gaussians_numpy((40, 36, 44), seed=5), np_dtype)
+    W, H = 64, 48
+    rp.framebuffer_size_changed(W, H)
+    ds = synth.dataset(vol)
+    rp.volume_dataset_changed(ds)
+    tf = synth.TFS[tfname]()
+    rp.transfer_function_changed(tf)
+    smin, smax = sl if sl else ((0, 0, 0), (1, 1, 1))
+    rp.slicing_changed(smin, smax)
+    for camname in ("rotA", "fill", "fill_oblique"):
+        cam = synth.camera(camname).to_vr_camera()
+        p0 = vr_amd.default_params(shading=shading, ert_eps=ert)
+        p1 = vr_amd.default_params(shading=shading, ert_eps=ert, skip_empty=1)
+        a = rp.render(cam, p0, vr_amd.OUT_RGBA32F)
+        b = rp.render(cam, p1, vr_amd.OUT_RGBA32F)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), camname
+        c0, c1 = rp.count_work(cam, p0), rp.count_work(cam, p1)
+        assert c0["skipped_samples"] == 0
+        assert c1["samples"] + c1["skipped_samples"] == c0["samples"]
+        assert c1["shaded_samples"] == c0["shaded_samples"] and c1["steps"] == c0["steps"]
+        assert c1["skipped_samples"] > 0, camname
+    ref, _ = oracle_render(vol.astype(np.float32), ds.vmin, ds.vmax, tf, cam, W, H, p1, smin, smax)
+    check(b, ref)
+    rp.slicing_changed((0, 0, 0), (1, 1, 1))
+
+
+def test_skip_empty_tracks_tf_and_volume_changes(rp):
+    """The brick classification is rebuilt after a TF change and after a volume change;
+    an all-transparent TF skips every sample; a constant volume (max == min) and a NaN
+    voxel never classify a brick as empty."""
+    W, H = 48, 40
+    rp.framebuffer_size_changed(W, H)
+    cam = synth.camera("fill").to_vr_camera()
+    p0, p1 = vr_amd.default_params(), vr_amd.default_params(skip_empty=1)
+
+    def same():
+        a = rp.render(cam, p0, vr_amd.OUT_RGBA32F)
+        b = rp.render(cam, p1, vr_amd.OUT_RGBA32F)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+        return rp.count_work(cam, p0), rp.count_work(cam, p1)
+
+    vol = synth.gaussians_numpy((30, 30, 30), seed=9)
+    rp.volume_dataset_changed(synth.dataset(vol))
+    for tf in (synth.tf2(), synth.tf_band(), synth.tf_color(), synth.tf2()[::-1].copy()):
+        rp.transfer_function_changed(tf)
+        same()
+    # every texel transparent: nothing is fetched, the frame is the clear colour
+    rp.transfer_function_changed(np.full(256, 0x00FFFFFF, dtype=np.uint32))
+    c0, c1 = same()
+    assert c1["samples"] == 0 and c1["skipped_samples"] == c0["samples"] > 0
+    # new volume under the same TF (tf2): stale masks would mis-skip
+    rp.transfer_function_changed(synth.tf2())
+    rp.render(cam, p1)
+    vol2 = synth.gaussians_numpy((30, 30, 30), seed=21)
+    rp.volume_dataset_changed(synth.dataset(vol2))
+    same()
+    # constant volume: range 0 -> t = NaN / inf; no brick may be skipped
+    rp.volume_dataset_changed(synth.dataset(np.full((9, 9, 9), 3.0, np.float32)))
+    c0, c1 = same()
+    assert c1["skipped_samples"] == 0
+    # a NaN voxel: its brick is never empty, whatever its other values
+    v = vol.copy()
+    v[15, 15, 15] = np.nan
+    ds = synth.dataset(v)
+    ds.vmin, ds.vmax = float(np.nanmin(v)), float(np.nanmax(v))
+    rp.volume_dataset_changed(ds)
+    rp.transfer_function_changed(synth.tf2())
+    a = rp.render(cam, p0, vr_amd.OUT_RGBA8)
+    b = rp.render(cam, p1, vr_amd.OUT_RGBA8)
+    assert np.array_equal(a, b)

@@ -11,7 +11,9 @@ timeout -k 10 400 python -m pytest tests -m gpu -q -x -p no:cacheprovider > $O/t
 timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > $O/bench.json 2> $O/bench.err &&
 timeout -k 10 300 python tools/view_sweep.py > $O/views_f32.txt 2>&1 &&
 timeout -k 10 300 python tools/view_sweep.py --shading 1 --ert 1e-5 > $O/views_f32_shaded.txt 2>&1 &&
-timeout -k 10 300 python tools/view_sweep.py --dtype uint8 --n 256 --size 1024x1024 > $O/views_u8.txt 2>&1
+timeout -k 10 300 python tools/view_sweep.py --dtype uint8 --n 256 --size 1024x1024 > $O/views_u8.txt 2>&1 &&
+timeout -k 10 300 python tools/view_sweep.py --shading 1 --ert 1e-5 --skip-empty 1 > $O/views_f32_shaded_skip.txt 2>&1 &&
+timeout -k 10 300 python tools/view_sweep.py --skip-empty 1 > $O/views_f32_skip.txt 2>&1
 rc=$?
 echo "rc=$rc" > $O/rc.txt
 exit $rc

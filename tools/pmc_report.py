@@ -20,8 +20,12 @@ def load(d, kname):
     for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
-            if kname not in k or "true>" in k.split(",")[-1]:  # skip the COUNT variant
+            if kname not in k:
                 continue
+            if "march_kernel<" in k:  # <VT, SHADE, COUNT, SKIP>: skip the counting variant
+                targs = [t.strip() for t in k.split("march_kernel<", 1)[1].split(">", 1)[0].split(",")]
+                if len(targs) > 2 and targs[2] == "true":
+                    continue
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
             durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
     return {k: sum(v) / len(v) for k, v in agg.items()}, (sum(durs) / len(durs) if durs else None)

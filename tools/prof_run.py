@@ -5,6 +5,7 @@ counter pass replays a short process.  Prints the in-process HIP-event kernel ti
 profile's per-dispatch durations can be matched.
   python tools/prof_run.py [--n 512] [--dtype float32] [--size 1920x1080] [--cam fill]
                            [--tf tf2] [--shading 1] [--ert 1e-5] [--frames 10] [--tile-order 0]
+                           [--skip-empty 0]
 """
 import argparse
 import json
@@ -32,13 +33,15 @@ def main():
     ap.add_argument("--ert", type=float, default=1e-5)
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--tile-order", type=int, default=0)
+    ap.add_argument("--skip-empty", type=int, default=0)
     a = ap.parse_args()
     W, H = (int(x) for x in a.size.split("x"))
     rp = vr_amd.OffscreenPass(W, H)
     rp.generate_volume((a.n,) * 3, np.dtype(a.dtype), seed=2024)
     rp.transfer_function_changed(synth.TFS[a.tf]())
     cam = synth.camera(a.cam).to_vr_camera()
-    p = vr_amd.default_params(shading=a.shading, ert_eps=a.ert, tile_order=a.tile_order)
+    p = vr_amd.default_params(shading=a.shading, ert_eps=a.ert, tile_order=a.tile_order,
+                              skip_empty=a.skip_empty)
     rp.render(cam, p, vr_amd.OUT_RGBA8)
     rp.timing_enable(True)
     for _ in range(a.frames):

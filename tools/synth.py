@@ -146,7 +146,18 @@ def tf_color():
     return g.discretize(256)
 
 
-TFS = {"tf0": tf0, "tf1": tf1, "tf2": tf2, "tfc": tf_color}
+def tf_band(lo=0.3, hi=0.8, n=256):
+    """Coloured TF, opaque only inside [lo, hi] (alpha exactly 0 outside): empty-space skipping
+    has transparent texels on BOTH sides of the visible band."""
+    t = (np.arange(n) + 0.5) / n
+    r = np.round(255 * t).astype(np.uint32)
+    g = np.round(255 * (1 - t)).astype(np.uint32)
+    b = np.full(n, 160, np.uint32)
+    a = np.where((t >= lo) & (t <= hi), np.round(255 * np.sin(np.pi * (t - lo) / (hi - lo)) ** 2), 0)
+    return (r | (g << 8) | (b << 16) | (a.astype(np.uint32) << 24)).astype(np.uint32)
+
+
+TFS = {"tf0": tf0, "tf1": tf1, "tf2": tf2, "tfc": tf_color, "tfband": tf_band}
 
 
 # ---- cameras ----

@@ -16,8 +16,9 @@ def mean_counter(d, name):
     for f in glob.glob(os.path.join(d, "run_counter_collection.csv")) + glob.glob(os.path.join(d, "*", "run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
-            if "march_kernel" in k and not k.rstrip(")").endswith("true>(vr::MarchParams"):
-                if "true>(vr" in k.split(",")[-1]:
+            if "march_kernel<" in k:
+                targs = [t.strip() for t in k.split("march_kernel<", 1)[1].split(">", 1)[0].split(",")]
+                if targs[2] == "true":  # <VT, SHADE, COUNT, SKIP>: the counting kernel is not timed
                     continue
                 if r["Counter_Name"] == name:
                     vals.append(float(r["Counter_Value"]))

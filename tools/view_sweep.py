@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--ert", type=float, default=0.0)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--tile-order", type=int, default=0)
+    ap.add_argument("--skip-empty", type=int, default=0)
     args = ap.parse_args()
     W, H = (int(x) for x in args.size.split("x"))
     rp = vr_amd.OffscreenPass(W, H)
@@ -48,7 +49,8 @@ def main():
     rp.transfer_function_changed(synth.TFS[args.tf]())
     out = torch.empty((H + 16, W), dtype=torch.int32, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
-    p = vr_amd.default_params(shading=args.shading, ert_eps=args.ert, tile_order=args.tile_order)
+    p = vr_amd.default_params(shading=args.shading, ert_eps=args.ert, tile_order=args.tile_order,
+                              skip_empty=args.skip_empty)
     res = {}
     for name, v in VIEWS.items():
         cam = vr_amd.make_camera(**v).to_vr_camera()
@@ -65,7 +67,8 @@ def main():
         kms = ms / n
         res[name] = dict(kernel_ms=round(kms, 4), samples=st["samples"],
                          gsamples_s=round(st["samples"] / (kms * 1e-3) / 1e9, 2),
-                         shaded=st["shaded_samples"])
+                         shaded=st["shaded_samples"], skipped=st["skipped_samples"],
+                         fps=round(1e3 / kms, 1))
         print(name, json.dumps(res[name]), flush=True)
     print(json.dumps(dict(args=vars(args), views=res)))
 

@@ -32,8 +32,15 @@ struct vr_ctx {
     // transfer function (decoded, linear float RGBA)
     float4 *tf = nullptr;
     uint32_t tf_n = 0;
+    uint32_t *tf_nz = nullptr;  // prefix count of nonzero-alpha texels (tf_n + 1)
     float smin[3] = {0.0f, 0.0f, 0.0f};
     float smax[3] = {1.0f, 1.0f, 1.0f};
+    // empty-space classification (skip_empty), built lazily: per-brick value range after a
+    // volume change, the brick distance field after a volume or TF change
+    float2 *brick_range = nullptr;
+    uint8_t *skip_dist = nullptr;  // 2 x nbricks: distance field + pass scratch
+    size_t nbricks_alloc = 0;
+    bool range_valid = false, dist_valid = false;
     // scratch
     unsigned long long *counters = nullptr;
     void *frame_dev = nullptr;
@@ -239,6 +246,7 @@ struct SplitMix {
 
 int set_bricks(vr_ctx *c, int storage, uint32_t nx, uint32_t ny, uint32_t nz, void **out)
 {
+    c->range_valid = c->dist_valid = false;  // the bricks are about to be rewritten
     const size_t bytes = (size_t)bricks_for(nx) * bricks_for(ny) * bricks_for(nz) *
                          kBrickElems * element_size(storage);
     if (c->bricks && c->brick_bytes == bytes) {
@@ -270,12 +278,23 @@ int upload_tf(vr_ctx *c, const uint32_t *tf, uint32_t n)
     }
     if (c->tf && c->tf_n != n) {
         hipFree(c->tf);
+        hipFree(c->tf_nz);
         c->tf = nullptr;
+        c->tf_nz = nullptr;
     }
-    if (!c->tf) HIP_TRY(c, hipMalloc(&c->tf, n * sizeof(float4)), "hipMalloc(TF)");
+    std::vector<uint32_t> nz(n + 1);
+    nz[0] = 0;
+    for (uint32_t i = 0; i < n; ++i) nz[i + 1] = nz[i] + ((tf[i] >> 24) != 0u ? 1u : 0u);
+    if (!c->tf) {
+        HIP_TRY(c, hipMalloc(&c->tf, n * sizeof(float4)), "hipMalloc(TF)");
+        HIP_TRY(c, hipMalloc(&c->tf_nz, (n + 1) * sizeof(uint32_t)), "hipMalloc(TF alpha prefix)");
+    }
     HIP_TRY(c, hipMemcpy(c->tf, lut.data(), n * sizeof(float4), hipMemcpyHostToDevice),
             "hipMemcpy(TF)");
+    HIP_TRY(c, hipMemcpy(c->tf_nz, nz.data(), (n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice),
+            "hipMemcpy(TF alpha prefix)");
     c->tf_n = n;
+    c->dist_valid = false;
     return VR_OK;
 }
 
@@ -350,6 +369,41 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.supers_x = (P.tiles_x + 3) / 4;
     P.supers_total = P.supers_x * ((P.tiles_y + 3) / 4);
     P.out_format = out_format;
+    return VR_OK;
+}
+
+// skip_empty: (re)build the per-brick ranges and the distance field when stale, on `s` ahead of
+// the march that reads them.
+int ensure_skip(vr_ctx *c, MarchParams &P, hipStream_t s)
+{
+    const size_t nb = (size_t)bricks_for(c->nx) * bricks_for(c->ny) * bricks_for(c->nz);
+    if (nb > 0xFFFFFFFFull) return fail(c, VR_EINVAL, "skip_empty: too many bricks");
+    if (c->nbricks_alloc != nb) {
+        if (c->brick_range) hipFree(c->brick_range);
+        if (c->skip_dist) hipFree(c->skip_dist);
+        c->brick_range = nullptr;
+        c->skip_dist = nullptr;
+        c->nbricks_alloc = 0;
+        c->range_valid = c->dist_valid = false;
+        HIP_TRY(c, hipMalloc(&c->brick_range, nb * sizeof(float2)), "hipMalloc(brick ranges)");
+        HIP_TRY(c, hipMalloc(&c->skip_dist, 2 * nb), "hipMalloc(skip distance field)");
+        c->nbricks_alloc = nb;
+    }
+    if (!c->range_valid) {
+        HIP_TRY(c, launch_brick_range(c->storage, c->bricks, (uint32_t)nb, c->brick_range, s),
+                "brick range kernel");
+        c->range_valid = true;
+        c->dist_valid = false;
+    }
+    if (!c->dist_valid) {
+        HIP_TRY(c, launch_skip_dist(c->brick_range, bricks_for(c->nx), bricks_for(c->ny),
+                                    bricks_for(c->nz), c->tf_nz, (int)c->tf_n, c->vmin,
+                                    c->vmax - c->vmin, c->skip_dist, c->skip_dist + nb, s),
+                "skip distance kernels");
+        c->dist_valid = true;
+    }
+    P.skip_dist = c->skip_dist;
+    P.skip_empty = 1;
     return VR_OK;
 }
 
@@ -447,6 +501,9 @@ void vr_destroy(vr_ctx *c)
     for (auto e : c->ev_pool) hipEventDestroy(e);
     if (c->bricks) hipFree(c->bricks);
     if (c->tf) hipFree(c->tf);
+    if (c->tf_nz) hipFree(c->tf_nz);
+    if (c->brick_range) hipFree(c->brick_range);
+    if (c->skip_dist) hipFree(c->skip_dist);
     if (c->counters) hipFree(c->counters);
     if (c->frame_dev) hipFree(c->frame_dev);
     delete c;
@@ -491,6 +548,7 @@ int vr_set_volume_device(vr_ctx *c, const void *data_dev, int dtype, uint32_t nx
     c->nz = nz;
     c->vmin = vmin;  // offscreen_pass.cpp:265-266
     c->vmax = vmax;
+    c->range_valid = c->dist_valid = false;
     return VR_OK;
 }
 
@@ -592,6 +650,7 @@ int vr_generate_volume(vr_ctx *c, int kind, int dtype, uint32_t nx, uint32_t ny,
     c->nz = nz;
     c->vmin = unorder(mm_host[0]);
     c->vmax = unorder(mm_host[1]);
+    c->range_valid = c->dist_valid = false;
     if (vmin_out) *vmin_out = c->vmin;
     if (vmax_out) *vmax_out = c->vmax;
     return VR_OK;
@@ -684,6 +743,10 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     hipStream_t s = static_cast<hipStream_t>(stream);
+    if (p->skip_empty) {
+        rc = ensure_skip(c, P, s);
+        if (rc) return rc;
+    }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing) {
         e0 = pooled_event(c);
@@ -752,14 +815,19 @@ int vr_count_work(vr_ctx *c, const vr_camera *cam, const vr_params *p, uint32_t 
     MarchParams P;
     int rc = build_params(c, cam, p, c->frame_dev, VR_OUT_RGBA8, row_block, rank, nranks, P);
     if (rc) return rc;
+    if (p->skip_empty) {
+        rc = ensure_skip(c, P, nullptr);
+        if (rc) return rc;
+    }
     HIP_TRY(c, hipMemset(c->counters, 0, 8 * sizeof(unsigned long long)), "hipMemset(counters)");
     HIP_TRY(c, launch_march(c->storage, p->shading != 0, true, P, nullptr), "march (count) launch");
-    unsigned long long h[4];
+    unsigned long long h[5];
     HIP_TRY(c, hipMemcpy(h, c->counters, sizeof(h), hipMemcpyDeviceToHost), "hipMemcpy(counters)");
     out->rays = h[0];
     out->samples = h[1];
     out->shaded_samples = h[2];
     out->steps = h[3];
+    out->skipped_samples = h[4];
     return VR_OK;
 }
 
@@ -803,7 +871,7 @@ int vr_timing_reset(vr_ctx *c)
 const char *vr_kernel_name(const vr_ctx *c, const vr_params *p)
 {
     if (!c) return "";
-    return march_kernel_name(c->storage, p && p->shading != 0, false);
+    return march_kernel_name(c->storage, p && p->shading != 0, false, p && p->skip_empty != 0);
 }
 
 }  // extern "C"

@@ -82,12 +82,16 @@ struct MarchParams {
     uint32_t tile_order;    // 1 raster, 2 XCD bands, 3 XCD-interleaved super-tiles
     uint32_t supers_x, supers_total;  // super-tile grid (tile_order 3)
     int32_t out_format;
+    // skip_empty: per brick (index as in cell_offset) the Chebyshev distance in bricks to the
+    // nearest brick that can produce a visible sample, capped at kSkipCap; 0 = not empty
+    const uint8_t *skip_dist;
+    int32_t skip_empty;
 };
 
 // Launchers (vr_kernels.hip).  All asynchronous on `stream`.
 hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &p,
                         hipStream_t stream);
-const char *march_kernel_name(int storage, bool shade, bool count);
+const char *march_kernel_name(int storage, bool shade, bool count, bool skip);
 hipError_t launch_brick_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,
                                     uint32_t ny, uint32_t nz, int storage, hipStream_t stream);
 // Synthetic volume into a LINEAR buffer of the storage type (then bricked).
@@ -100,5 +104,15 @@ hipError_t launch_assemble(const void *gathered, void *out, int out_format, uint
 // min/max over a LINEAR buffer of the storage type (ordered-uint encoding in minmax_dev).
 hipError_t launch_minmax(int storage, const void *linear, size_t count, float *minmax_dev,
                          hipStream_t stream);
+
+// Empty-space skipping (skip_empty): per-brick value range of the stored elements, then per
+// (volume, TF) the capped Chebyshev distance field over the brick grid (1 byte per brick;
+// scratch_dev: the same size, for the separable passes).
+constexpr int kSkipCap = 16;
+hipError_t launch_brick_range(int storage, const void *bricks, uint32_t nbricks,
+                              float2 *range_dev, hipStream_t stream);
+hipError_t launch_skip_dist(const float2 *range_dev, uint32_t nbx, uint32_t nby, uint32_t nbz,
+                            const uint32_t *tf_nz_dev, int tf_n, float vmin, float vrange,
+                            uint8_t *dist_dev, uint8_t *scratch_dev, hipStream_t stream);
 
 }  // namespace vr

@@ -18,7 +18,9 @@
 //    an explicit fmaf(), matching the CPU oracle's operation order bit for bit.
 #include "vr_internal.h"
 
+#include <string>
 #include <type_traits>
+#include <vector>
 
 #pragma clang fp contract(off)
 
@@ -318,7 +320,25 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
     return v;
 }
 
-template <typename VT, bool SHADE, bool COUNT>
+// skip_empty: longest leap in steps (bounds the float drift the leap margin must cover)
+constexpr int kMaxLeap = 256;
+
+// Minimum of k in [0, kMaxLeap] over the ACTIVE lanes (binary search on ballots: a ballot
+// sees only active lanes, where a DPP reduction would read stale values of inactive ones).
+__device__ __forceinline__ int wave_min_leap(int k)
+{
+    int lo = 0, hi = kMaxLeap;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (__ballot(k <= mid) != 0ull)
+            hi = mid;
+        else
+            lo = mid + 1;
+    }
+    return lo;
+}
+
+template <typename VT, bool SHADE, bool COUNT, bool SKIP>
 #ifndef VR_MARCH_MIN_WAVES
 #define VR_MARCH_MIN_WAVES 1
 #endif
@@ -371,11 +391,23 @@ __global__ __launch_bounds__(kThreads, VR_MARCH_MIN_WAVES) void march_kernel(con
     const bool covered = active && pixel_ray(P, px, gy, tex, dir);
 
     float T = 1.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f;
-    unsigned long long n_samples = 0, n_shaded = 0, n_steps = 0;
+    unsigned long long n_samples = 0, n_shaded = 0, n_steps = 0, n_skipped = 0;
+    uint32_t cur_brick = 0xFFFFFFFFu, cur_dist = 0;
     const char *__restrict__ vol = static_cast<const char *>(P.vol);
     const int nsteps = covered ? P.nsteps : 0;
     float p0 = tex[0], p1 = tex[1], p2 = tex[2];
     const float d0 = dir[0], d1 = dir[1], d2 = dir[2];
+    // skip_empty leap constants: steps per cell along each axis, and a margin (cells) covering
+    // the leap's float-accumulation drift (<= kMaxLeap half-ulps of p < 2, times N) + rounding
+    float inv_du[3] = {0.f, 0.f, 0.f}, leap_margin[3] = {0.f, 0.f, 0.f};
+    if (!COUNT && SKIP) {
+        const float dd[3] = {d0, d1, d2}, fn[3] = {P.fnx, P.fny, P.fnz};
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            inv_du[a] = 1.0f / (fabsf(dd[a]) * P.step * fn[a]);
+            leap_margin[a] = 0.5f + (float)kMaxLeap * 1.2e-7f * fn[a];
+        }
+    }
     for (int it = 0; it < nsteps; ++it) {
         // volume.frag:34-37
         if (p0 > 1.0f || p1 > 1.0f || p2 > 1.0f || p0 < 0.0f || p1 < 0.0f || p2 < 0.0f) break;
@@ -389,41 +421,91 @@ __global__ __launch_bounds__(kThreads, VR_MARCH_MIN_WAVES) void march_kernel(con
             texel_coord(p1, P.fny, j, ay);
             texel_coord(p2, P.fnz, k, az);
             const int pi = i + kPad, pj = j + kPad, pk = k + kPad;
-            const size_t ce = cell_offset(pi, pj, pk, P.nbx, P.nby);
-            Cell8<VT> c;
-            c.load(vol, ce);
-            const float d = c.tri(ax, ay, az);
-            const float tt = (d - P.vmin) / P.range;
-            float4 s = tf_in_lds ? tf_lookup(s_tf, P.tf_n, P.tf_nf, tt)
-                                 : tf_lookup(P.tf, P.tf_n, P.tf_nf, tt);
-            if (COUNT) ++n_samples;
-            if (SHADE && s.w > 0.0f) {
-                float gx, gy_, gz;
-                gradient<VT>(vol, ce, c, pi & (kBrick - 1), pj & (kBrick - 1), pk & (kBrick - 1),
-                             by_stride, bz_stride, ax, ay, az, gx,
-                         gy_, gz);
-                if (COUNT) ++n_shaded;
-                const float wx = gx * P.fnx, wy = gy_ * P.fny, wz = gz * P.fnz;
-                const float g2 = wx * wx + wy * wy + wz * wz;
-                if (g2 > 0.0f) {
-                    const float inv = 1.0f / sqrtf(g2);
-                    const float ndl = fabsf((wx * d0 + wy * d1 + wz * d2) * inv);
-                    const float kdiff = P.ka + P.kd * ndl;
-                    float sp = 1.0f;
-                    for (int e = 0; e < P.spec_power; ++e) sp = sp * ndl;
-                    const float spec = P.ks * sp;
-                    s.x = s.x * kdiff + spec;
-                    s.y = s.y * kdiff + spec;
-                    s.z = s.z * kdiff + spec;
+            uint32_t dist = 0;
+            if (SKIP) {
+                // skip_empty: distance (in bricks) from the cell's brick to the nearest brick
+                // that can produce a visible sample (classify_kernel); cached per brick
+                const uint32_t bb = ((uint32_t)(pk >> kBrickShift) * P.nby +
+                                     (uint32_t)(pj >> kBrickShift)) * P.nbx +
+                                    (uint32_t)(pi >> kBrickShift);
+                if (bb != cur_brick) {
+                    cur_brick = bb;
+                    cur_dist = P.skip_dist[bb];
                 }
+                dist = cur_dist;
             }
-            // volume.frag:44-45
-            cr = cr + (s.x * s.w) * T;
-            cg = cg + (s.y * s.w) * T;
-            cb = cb + (s.z * s.w) * T;
-            T = T * (1.0f - s.w);
-            if (T == 0.0f) break;
-            if (T < P.ert_eps) break;
+            // the wavefront leaps only when every lane sampling here is in empty space, and
+            // by the smallest safe leap of its lanes: lanes stay in lock-step (a lane-private
+            // leap desynchronises the wave and multiplies its fetch instructions)
+            const bool wave_empty = SKIP && !COUNT && __all(dist != 0);
+            if (dist != 0) {
+                if (COUNT) {
+                    ++n_skipped;  // the counting kernel walks every step (exact counters)
+                } else if (wave_empty) {
+                    // Leap: every brick within Chebyshev radius dist - 1 of this one is empty.
+                    // Take the steps whose cells provably stay inside that box (cell
+                    // coordinate u = p N - 0.5, brick of u: (floor(u) + 2) >> 3), advancing p
+                    // with the same float additions as the reference loop, so the first
+                    // non-empty sample is reached at the bit-identical position.
+                    const float reach = (float)((int)(dist - 1) * kBrick);
+                    float kf = (float)min(nsteps - 1 - it, kMaxLeap);
+                    const int bi[3] = {pi >> kBrickShift, pj >> kBrickShift, pk >> kBrickShift};
+                    const float pp[3] = {p0, p1, p2}, dd[3] = {d0, d1, d2};
+                    const float fn[3] = {P.fnx, P.fny, P.fnz};
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+                        const float u = pp[a] * fn[a] - 0.5f;
+                        const float room = dd[a] > 0.0f
+                                               ? (float)((bi[a] + 1) * kBrick - kPad) + reach - u
+                                               : u - (float)(bi[a] * kBrick - kPad) + reach;
+                        // NaN (axis not moving) is ignored by fminf
+                        kf = fminf(kf, (room - leap_margin[a]) * inv_du[a]);
+                    }
+                    const int k = wave_min_leap(kf >= 1.0f ? (int)kf : 0);
+                    for (int j = 0; j < k; ++j) {
+                        p0 = p0 + d0 * P.step;
+                        p1 = p1 + d1 * P.step;
+                        p2 = p2 + d2 * P.step;
+                    }
+                    it += k;
+                }
+            } else {
+                const size_t ce = cell_offset(pi, pj, pk, P.nbx, P.nby);
+                Cell8<VT> c;
+                c.load(vol, ce);
+                const float d = c.tri(ax, ay, az);
+                const float tt = (d - P.vmin) / P.range;
+                float4 s = tf_in_lds ? tf_lookup(s_tf, P.tf_n, P.tf_nf, tt)
+                                     : tf_lookup(P.tf, P.tf_n, P.tf_nf, tt);
+                if (COUNT) ++n_samples;
+                if (SHADE && s.w > 0.0f) {
+                    float gx, gy_, gz;
+                    gradient<VT>(vol, ce, c, pi & (kBrick - 1), pj & (kBrick - 1),
+                                 pk & (kBrick - 1), by_stride, bz_stride, ax, ay, az, gx, gy_,
+                                 gz);
+                    if (COUNT) ++n_shaded;
+                    const float wx = gx * P.fnx, wy = gy_ * P.fny, wz = gz * P.fnz;
+                    const float g2 = wx * wx + wy * wy + wz * wz;
+                    if (g2 > 0.0f) {
+                        const float inv = 1.0f / sqrtf(g2);
+                        const float ndl = fabsf((wx * d0 + wy * d1 + wz * d2) * inv);
+                        const float kdiff = P.ka + P.kd * ndl;
+                        float sp = 1.0f;
+                        for (int e = 0; e < P.spec_power; ++e) sp = sp * ndl;
+                        const float spec = P.ks * sp;
+                        s.x = s.x * kdiff + spec;
+                        s.y = s.y * kdiff + spec;
+                        s.z = s.z * kdiff + spec;
+                    }
+                }
+                // volume.frag:44-45
+                cr = cr + (s.x * s.w) * T;
+                cg = cg + (s.y * s.w) * T;
+                cb = cb + (s.z * s.w) * T;
+                T = T * (1.0f - s.w);
+                if (T == 0.0f) break;
+                if (T < P.ert_eps) break;
+            }
         }
         // volume.frag:47
         p0 = p0 + d0 * P.step;
@@ -436,11 +518,13 @@ __global__ __launch_bounds__(kThreads, VR_MARCH_MIN_WAVES) void march_kernel(con
         const unsigned long long sm = wave_sum(n_samples);
         const unsigned long long sh = wave_sum(n_shaded);
         const unsigned long long st = wave_sum(n_steps);
+        const unsigned long long sk = wave_sum(n_skipped);
         if (lane == 0) {
             atomicAdd(&P.counters[0], rays);
             atomicAdd(&P.counters[1], sm);
             atomicAdd(&P.counters[2], sh);
             atomicAdd(&P.counters[3], st);
+            atomicAdd(&P.counters[4], sk);
         }
     }
     if (!active) return;
@@ -580,6 +664,103 @@ __global__ __launch_bounds__(256) void minmax_kernel(const VT *__restrict__ vol,
     }
 }
 
+// ---- empty-space classification (skip_empty) --------------------------------------------------
+
+// One wavefront per brick: min/max over every voxel its stored elements hold (apron and zero
+// border included: exactly the values a sample whose cell lies in the brick can read).  A
+// brick holding a NaN gets (NaN, NaN), which the classifier never calls empty.
+template <typename VT>
+__global__ __launch_bounds__(256) void brick_range_kernel(const VT *__restrict__ bricks,
+                                                          uint32_t nbricks, uint32_t per_brick,
+                                                          float2 *__restrict__ range)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= nbricks) return;  // wave-uniform
+    const VT *src = bricks + (size_t)b * per_brick;
+    float lo = INFINITY, hi = -INFINITY;
+    bool nan = false;
+    for (uint32_t e = lane; e < per_brick; e += 64) {
+        const float v = (float)src[e];
+        nan = nan || v != v;
+        lo = fminf(lo, v);
+        hi = fmaxf(hi, v);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = fminf(lo, __shfl_xor(lo, off, 64));
+        hi = fmaxf(hi, __shfl_xor(hi, off, 64));
+    }
+    const bool any_nan = __ballot(nan) != 0;
+    if (lane == 0) range[b] = any_nan ? make_float2(NAN, NAN) : make_float2(lo, hi);
+}
+
+// One thread per brick: 0 if the brick can produce a visible sample, kSkipCap if EMPTY.
+// Brick b is empty when every density d the trilinear filter can produce from its values maps
+// to TF texels of alpha 0.  d lies in [lo, hi] up to the filter's rounding (3 levels of fmaf
+// lerps: well under 1e-6 |d|), so the bounds are widened by kRangeMargin; t = (d - vmin) /
+// range, u = t * n - 0.5 and floor are monotone, so the texels tf_lookup can touch are
+// [floor(u(lo)), floor(u(hi)) + 1] clamped to [0, n - 1].  tf_nz is the prefix count of
+// nonzero-alpha texels (n + 1 entries).  A sample whose alpha is lerp(0, 0, w) = 0 adds
+// (rgb * 0) * T = +0 to C and leaves T unchanged: skipping it is exact.
+__global__ __launch_bounds__(256) void classify_kernel(const float2 *__restrict__ range,
+                                                       uint32_t nbricks,
+                                                       const uint32_t *__restrict__ tf_nz,
+                                                       int tf_n, float tf_nf, float vmin,
+                                                       float vrange, uint8_t *__restrict__ dist)
+{
+    constexpr float kRangeMargin = 4.0e-6f;
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nbricks) return;
+    bool empty = false;
+    if (vrange > 0.0f) {
+        const float2 r = range[b];
+        if (r.x == r.x && r.y == r.y) {  // no NaN in the brick
+            const float m = (fabsf(r.x) + fabsf(r.y)) * kRangeMargin;
+            const float t0 = ((r.x - m) - vmin) / vrange;
+            const float t1 = ((r.y + m) - vmin) / vrange;
+            float u0 = t0 * tf_nf - 0.5f, u1 = t1 * tf_nf - 0.5f;
+            u0 = fminf(fmaxf(u0, -1.0f), tf_nf);
+            u1 = fminf(fmaxf(u1, -1.0f), tf_nf);
+            int i0 = (int)floorf(u0), i1 = (int)floorf(u1) + 1;
+            i0 = i0 < 0 ? 0 : (i0 > tf_n - 1 ? tf_n - 1 : i0);
+            i1 = i1 < 0 ? 0 : (i1 > tf_n - 1 ? tf_n - 1 : i1);
+            empty = tf_nz[i1 + 1] == tf_nz[i0];
+        }
+    }
+    dist[b] = empty ? (uint8_t)kSkipCap : (uint8_t)0;
+}
+
+// One separable pass of the Chebyshev (L-inf) distance transform of the non-empty bricks,
+// along axis `axis`: out(b) = min over |o| <= kSkipCap of max(|o|, in(b + o e_axis)), capped.
+// Three passes (x, y, z) from the classification give min(kSkipCap, distance in bricks to
+// the nearest non-empty brick); bricks past the grid count as empty (a ray there has left
+// the volume, and the march's bounds test ends it).
+__global__ __launch_bounds__(256) void dist_pass_kernel(const uint8_t *__restrict__ in,
+                                                        uint8_t *__restrict__ out, uint32_t nbx,
+                                                        uint32_t nby, uint32_t nbz, int axis)
+{
+    const uint32_t nb = nbx * nby * nbz;
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const uint32_t bx = b % nbx, by = (b / nbx) % nby, bz = b / (nbx * nby);
+    const int pos = axis == 0 ? (int)bx : (axis == 1 ? (int)by : (int)bz);
+    const int len = axis == 0 ? (int)nbx : (axis == 1 ? (int)nby : (int)nbz);
+    const long stride = axis == 0 ? 1 : (axis == 1 ? (long)nbx : (long)nbx * nby);
+    int best = in[b];
+    for (int o = 1; o < kSkipCap && o < best; ++o) {
+        if (pos - o >= 0) {
+            const int v = in[b - o * stride];
+            best = min(best, max(o, v));
+        }
+        if (pos + o < len) {
+            const int v = in[b + o * stride];
+            best = min(best, max(o, v));
+        }
+    }
+    out[b] = (uint8_t)best;
+}
+
 // ---- rank-0 framebuffer assembly after the RCCL gather ---------------------------------------
 
 template <typename PixT>
@@ -599,13 +780,13 @@ __global__ __launch_bounds__(256) void assemble_kernel(const PixT *__restrict__ 
     }
 }
 
-template <typename VT, bool SHADE, bool COUNT>
+template <typename VT, bool SHADE, bool COUNT, bool SKIP>
 hipError_t launch_march_t(const MarchParams &p, hipStream_t stream)
 {
     const uint32_t nblocks = p.tile_order == 3 ? ((p.supers_total + 7) / 8) * 8 * 16
                                                : p.tiles_x * p.tiles_y;
     if (p.tiles_x * p.tiles_y == 0) return hipSuccess;
-    hipLaunchKernelGGL((march_kernel<VT, SHADE, COUNT>), dim3(nblocks), dim3(kThreads), 0,
+    hipLaunchKernelGGL((march_kernel<VT, SHADE, COUNT, SKIP>), dim3(nblocks), dim3(kThreads), 0,
                        stream, p);
     return hipGetLastError();
 }
@@ -613,8 +794,18 @@ hipError_t launch_march_t(const MarchParams &p, hipStream_t stream)
 template <typename VT>
 hipError_t launch_march_vt(bool shade, bool count, const MarchParams &p, hipStream_t s)
 {
-    if (shade) return count ? launch_march_t<VT, true, true>(p, s) : launch_march_t<VT, true, false>(p, s);
-    return count ? launch_march_t<VT, false, true>(p, s) : launch_march_t<VT, false, false>(p, s);
+    if (p.skip_empty) {
+        if (shade)
+            return count ? launch_march_t<VT, true, true, true>(p, s)
+                         : launch_march_t<VT, true, false, true>(p, s);
+        return count ? launch_march_t<VT, false, true, true>(p, s)
+                     : launch_march_t<VT, false, false, true>(p, s);
+    }
+    if (shade)
+        return count ? launch_march_t<VT, true, true, false>(p, s)
+                     : launch_march_t<VT, true, false, false>(p, s);
+    return count ? launch_march_t<VT, false, true, false>(p, s)
+                 : launch_march_t<VT, false, false, false>(p, s);
 }
 
 inline unsigned grid_for(size_t total)
@@ -655,22 +846,21 @@ hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &
     }
 }
 
-const char *march_kernel_name(int storage, bool shade, bool count)
+const char *march_kernel_name(int storage, bool shade, bool count, bool skip)
 {
-    static const char *names[5][2][2] = {
-        {{"march_kernel<unsigned char, false, false>", "march_kernel<unsigned char, false, true>"},
-         {"march_kernel<unsigned char, true, false>", "march_kernel<unsigned char, true, true>"}},
-        {{"march_kernel<signed char, false, false>", "march_kernel<signed char, false, true>"},
-         {"march_kernel<signed char, true, false>", "march_kernel<signed char, true, true>"}},
-        {{"march_kernel<unsigned short, false, false>", "march_kernel<unsigned short, false, true>"},
-         {"march_kernel<unsigned short, true, false>", "march_kernel<unsigned short, true, true>"}},
-        {{"march_kernel<short, false, false>", "march_kernel<short, false, true>"},
-         {"march_kernel<short, true, false>", "march_kernel<short, true, true>"}},
-        {{"march_kernel<float, false, false>", "march_kernel<float, false, true>"},
-         {"march_kernel<float, true, false>", "march_kernel<float, true, true>"}},
-    };
+    // demangled names as rocprofv3 reports them (kernel-trace "Kernel_Name")
+    static const std::vector<std::string> names = [] {
+        const char *types[5] = {"unsigned char", "signed char", "unsigned short", "short", "float"};
+        std::vector<std::string> v;
+        for (int t = 0; t < 5; ++t)
+            for (int k = 0; k < 8; ++k)
+                v.push_back(std::string("void vr::(anonymous namespace)::march_kernel<") + types[t] +
+                            ((k & 4) ? ", true" : ", false") + ((k & 2) ? ", true" : ", false") +
+                            ((k & 1) ? ", true" : ", false") + ">(vr::MarchParams)");
+        return v;
+    }();
     if (storage < 0 || storage > 4) return "march_kernel<?>";
-    return names[storage][shade ? 1 : 0][count ? 1 : 0];
+    return names[storage * 8 + (shade ? 4 : 0) + (count ? 2 : 0) + (skip ? 1 : 0)].c_str();
 }
 
 hipError_t launch_brick_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,
@@ -733,6 +923,38 @@ hipError_t launch_assemble(const void *gathered, void *out, int out_format, uint
         hipLaunchKernelGGL((assemble_kernel<float4>), dim3(g), dim3(256), 0, s,
                            (const float4 *)gathered, (float4 *)out, W, H, row_block, nranks, shard_rows);
     return hipGetLastError();
+}
+
+hipError_t launch_brick_range(int storage, const void *bricks, uint32_t nbricks,
+                              float2 *range_dev, hipStream_t s)
+{
+    const unsigned g = (nbricks + 3) / 4;
+    const uint32_t per = kBrickElems * (uint32_t)voxels_per_element(storage);
+    switch (storage) {
+        case ST_U8: hipLaunchKernelGGL((brick_range_kernel<uint8_t>), dim3(g), dim3(256), 0, s, (const uint8_t *)bricks, nbricks, per, range_dev); break;
+        case ST_I8: hipLaunchKernelGGL((brick_range_kernel<int8_t>), dim3(g), dim3(256), 0, s, (const int8_t *)bricks, nbricks, per, range_dev); break;
+        case ST_U16: hipLaunchKernelGGL((brick_range_kernel<uint16_t>), dim3(g), dim3(256), 0, s, (const uint16_t *)bricks, nbricks, per, range_dev); break;
+        case ST_I16: hipLaunchKernelGGL((brick_range_kernel<int16_t>), dim3(g), dim3(256), 0, s, (const int16_t *)bricks, nbricks, per, range_dev); break;
+        default: hipLaunchKernelGGL((brick_range_kernel<float>), dim3(g), dim3(256), 0, s, (const float *)bricks, nbricks, per, range_dev); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_skip_dist(const float2 *range_dev, uint32_t nbx, uint32_t nby, uint32_t nbz,
+                            const uint32_t *tf_nz_dev, int tf_n, float vmin, float vrange,
+                            uint8_t *dist_dev, uint8_t *scratch_dev, hipStream_t s)
+{
+    const uint32_t nb = nbx * nby * nbz;
+    const unsigned g = (nb + 255) / 256;
+    hipLaunchKernelGGL(classify_kernel, dim3(g), dim3(256), 0, s, range_dev, nb, tf_nz_dev, tf_n,
+                       (float)tf_n, vmin, vrange, dist_dev);
+    hipLaunchKernelGGL(dist_pass_kernel, dim3(g), dim3(256), 0, s, (const uint8_t *)dist_dev,
+                       scratch_dev, nbx, nby, nbz, 0);
+    hipLaunchKernelGGL(dist_pass_kernel, dim3(g), dim3(256), 0, s, (const uint8_t *)scratch_dev,
+                       dist_dev, nbx, nby, nbz, 1);
+    hipLaunchKernelGGL(dist_pass_kernel, dim3(g), dim3(256), 0, s, (const uint8_t *)dist_dev,
+                       scratch_dev, nbx, nby, nbz, 2);
+    return hipMemcpyAsync(dist_dev, scratch_dev, nb, hipMemcpyDeviceToDevice, s);
 }
 
 }  // namespace vr

@@ -46,12 +46,13 @@ class vr_params(C.Structure):
                 ("shading", C.c_int32), ("clear_color", C.c_float * 4),
                 ("ambient", C.c_float), ("diffuse", C.c_float), ("specular", C.c_float),
                 ("spec_power", C.c_int32), ("tile_order", C.c_int32),
-                ("reserved", C.c_int32 * 3)]
+                ("skip_empty", C.c_int32), ("reserved", C.c_int32 * 2)]
 
 
 class vr_stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("samples", C.c_uint64),
-                ("shaded_samples", C.c_uint64), ("steps", C.c_uint64)]
+                ("shaded_samples", C.c_uint64), ("steps", C.c_uint64),
+                ("skipped_samples", C.c_uint64)]
 
 
 class vr_orbit_camera(C.Structure):
@@ -83,6 +84,7 @@ HOST_SYMBOLS = [
     "vr_csv_load", "vr_dataset_free", "vr_host_last_error",
 ]
 
+ABI_VERSION = 2  # include/vr/vr.h VR_ABI_VERSION
 _LIB = None
 
 
@@ -148,6 +150,9 @@ def lib() -> C.CDLL:
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
+    if L.vr_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{LIB_PATH} has ABI {L.vr_abi_version()}, this binding expects "
+                           f"{ABI_VERSION}: rebuild it")
     _LIB = L
     return L
 
@@ -423,7 +428,8 @@ class OffscreenPass:
         st = vr_stats()
         self._check(lib().vr_count_work(self._ctx, C.byref(cam), C.byref(params), row_block, rank,
                                         nranks, C.byref(st)), "count_work")
-        return dict(rays=st.rays, samples=st.samples, shaded_samples=st.shaded_samples, steps=st.steps)
+        return dict(rays=st.rays, samples=st.samples, shaded_samples=st.shaded_samples,
+                    steps=st.steps, skipped_samples=st.skipped_samples)
 
     def timing_enable(self, on: bool = True):
         self._check(lib().vr_timing_enable(self._ctx, 1 if on else 0), "timing_enable")
