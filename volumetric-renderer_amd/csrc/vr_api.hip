@@ -342,6 +342,10 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.fnz = (float)c->nz;
     P.vmin = c->vmin;
     P.range = c->vmax - c->vmin;
+    // reciprocal division domain (div_by_range in vr_kernels.hip)
+    P.div_fast = P.range >= 0x1p-40f && P.range < 0x1p100f && std::fabs(c->vmin) < 0x1p100f &&
+                 std::fabs(c->vmax) < 0x1p100f;
+    P.inv_range = P.div_fast ? 1.0f / P.range : 0.0f;
     P.tf_n = (int32_t)c->tf_n;
     P.tf_nf = (float)c->tf_n;
     for (int a = 0; a < 3; ++a) {

@@ -86,6 +86,8 @@ struct MarchParams {
     // nearest brick that can produce a visible sample, capped at kSkipCap; 0 = not empty
     const uint8_t *skip_dist;
     int32_t skip_empty;
+    int32_t div_fast;       // density normalisation by reciprocal + fma correction
+    float inv_range;        // RN(1 / range) (div_fast)
 };
 
 // Launchers (vr_kernels.hip).  All asynchronous on `stream`.

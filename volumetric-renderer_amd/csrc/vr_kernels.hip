@@ -33,6 +33,15 @@ constexpr int kTfLds = 256;     // TF texels staged in LDS
 
 __device__ __forceinline__ float lerpf(float a, float b, float w) { return fmaf(w, b - a, a); }
 
+// Two independent lerps in one packed-FP32 pair (v_pk_add_f32 + v_pk_fma_f32): the same IEEE
+// operations per element as lerpf, so bit-identical to two scalar lerps.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v lerp2(f2v a, f2v b, float w)
+{
+    const f2v ww = {w, w};
+    return __builtin_elementwise_fma(ww, b - a, a);
+}
+
 // Unaligned-capable vector types: element pairs are 4- or 8-byte aligned, and gfx950 global
 // loads only need dword alignment, so these compile to single global_load_dwordx2/x4.
 typedef float f2a __attribute__((ext_vector_type(2))) __attribute__((aligned(4)));
@@ -49,7 +58,8 @@ template <typename VT>
 constexpr int kQuadWords = sizeof(VT) == 1 ? 1 : 2;
 
 // Element index of padded cell (pi, pj, pk) in the bricked layout (vr_internal.h).  64-bit:
-// a 2048^3 volume has 257^3 x 729 elements.
+// a 2048^3 volume has 257^3 x 729 elements.  (A 32-bit index with SGPR-base loads for
+// volumes < 4 GiB measured slower on the shaded kernel and on the diagonal view.)
 __device__ __forceinline__ size_t cell_offset(int pi, int pj, int pk, uint32_t nbx, uint32_t nby)
 {
     const uint32_t b = ((uint32_t)(pk >> kBrickShift) * nby + (uint32_t)(pj >> kBrickShift)) * nbx +
@@ -60,7 +70,7 @@ __device__ __forceinline__ size_t cell_offset(int pi, int pj, int pk, uint32_t n
 }
 
 // Trilinear filter of a 2x2x2 cell given its voxels v[dz][dy][dx]: lerp x, then y, then z
-// (the oracle's tri_cell operation order).
+// (the oracle's tri_cell operation order).  tri8x2: two independent cells at once (packed).
 __device__ __forceinline__ float tri8(float v000, float v100, float v010, float v110, float v001,
                                       float v101, float v011, float v111, float ax, float ay,
                                       float az)
@@ -72,6 +82,18 @@ __device__ __forceinline__ float tri8(float v000, float v100, float v010, float 
     const float c0 = lerpf(c00, c10, ay);
     const float c1 = lerpf(c01, c11, ay);
     return lerpf(c0, c1, az);
+}
+// element-wise: .x = tri8 of the .x voxels, .y = tri8 of the .y voxels
+__device__ __forceinline__ f2v tri8x2(f2v v000, f2v v100, f2v v010, f2v v110, f2v v001,
+                                      f2v v101, f2v v011, f2v v111, float ax, float ay, float az)
+{
+    const f2v c00 = lerp2(v000, v100, ax);
+    const f2v c10 = lerp2(v010, v110, ax);
+    const f2v c01 = lerp2(v001, v101, ax);
+    const f2v c11 = lerp2(v011, v111, ax);
+    const f2v c0 = lerp2(c00, c10, ay);
+    const f2v c1 = lerp2(c01, c11, ay);
+    return lerp2(c0, c1, az);
 }
 
 // Component c of a yz-quad element held in 32-bit words w (c: 0 (y,z), 1 (y,z+1), 2 (y+1,z),
@@ -169,11 +191,13 @@ struct Cell8 {
 
 // Central-difference gradient (extension): the cells one texel either side along each axis
 // share the centre cell's weights, so only the 4-wide stencil's outer voxels are new
-// (24 voxels: 10 loads for z-pair f32, 6 for yz-quads).  Taps one element below, or two
+// (24 voxels: 10 loads for z-pair f32, 6 for yz-quads).  PACKED: each axis' +1/-1 pair of
+// trilinears as one packed-FP32 trilinear (half the VALU, more VGPRs; the z-pair scalar form
+// is kept for the register-tight skip-empty kernel).  Taps one element below, or two
 // above in z-pair x/y, may sit in the neighbouring brick (the apron covers +1): the per-axis
 // deltas pick that brick.  Bit-identical to six independent trilinear fetches (same voxels,
 // same operations), which is what the oracle computes.
-template <typename VT>
+template <typename VT, bool PACKED>
 __device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e,
                                          const Cell8<VT> &c, int lx, int ly, int lz,
                                          long by_stride, long bz_stride, float ax, float ay,
@@ -192,12 +216,28 @@ __device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e
         const f4a ym = zpair_load2(base, e + dym), yp = zpair_load2(base, e + dyp);
         const f4a zm0 = zpair_load2(base, e + dzm), zm1 = zpair_load2(base, e + dzm + S);
         const f4a zp0 = zpair_load2(base, e + S2), zp1 = zpair_load2(base, e + S2 + S);
-        gx = tri8(v[1], xp0.x, v[3], xp1.x, v[5], xp0.y, v[7], xp1.y, ax, ay, az) -
-             tri8(xm0.x, v[0], xm1.x, v[2], xm0.y, v[4], xm1.y, v[6], ax, ay, az);
-        gy = tri8(v[2], v[3], yp.x, yp.z, v[6], v[7], yp.y, yp.w, ax, ay, az) -
-             tri8(ym.x, ym.z, v[0], v[1], ym.y, ym.w, v[4], v[5], ax, ay, az);
-        gz = tri8(v[4], v[5], v[6], v[7], zp0.y, zp0.w, zp1.y, zp1.w, ax, ay, az) -
-             tri8(zm0.x, zm0.z, zm1.x, zm1.z, v[0], v[1], v[2], v[3], ax, ay, az);
+        if constexpr (!PACKED) {
+            gx = tri8(v[1], xp0.x, v[3], xp1.x, v[5], xp0.y, v[7], xp1.y, ax, ay, az) -
+                 tri8(xm0.x, v[0], xm1.x, v[2], xm0.y, v[4], xm1.y, v[6], ax, ay, az);
+            gy = tri8(v[2], v[3], yp.x, yp.z, v[6], v[7], yp.y, yp.w, ax, ay, az) -
+                 tri8(ym.x, ym.z, v[0], v[1], ym.y, ym.w, v[4], v[5], ax, ay, az);
+            gz = tri8(v[4], v[5], v[6], v[7], zp0.y, zp0.w, zp1.y, zp1.w, ax, ay, az) -
+                 tri8(zm0.x, zm0.z, zm1.x, zm1.z, v[0], v[1], v[2], v[3], ax, ay, az);
+            return;
+        }
+        // .x: the +1 tap's cell, .y: the -1 tap's cell, one packed trilinear per axis
+        const f2v tx = tri8x2(f2v{v[1], xm0.x}, f2v{xp0.x, v[0]}, f2v{v[3], xm1.x}, f2v{xp1.x, v[2]},
+                              f2v{v[5], xm0.y}, f2v{xp0.y, v[4]}, f2v{v[7], xm1.y}, f2v{xp1.y, v[6]},
+                              ax, ay, az);
+        const f2v ty = tri8x2(f2v{v[2], ym.x}, f2v{v[3], ym.z}, f2v{yp.x, v[0]}, f2v{yp.z, v[1]},
+                              f2v{v[6], ym.y}, f2v{v[7], ym.w}, f2v{yp.y, v[4]}, f2v{yp.w, v[5]},
+                              ax, ay, az);
+        const f2v tz = tri8x2(f2v{v[4], zm0.x}, f2v{v[5], zm0.z}, f2v{v[6], zm1.x}, f2v{v[7], zm1.z},
+                              f2v{zp0.y, v[0]}, f2v{zp0.w, v[1]}, f2v{zp1.y, v[2]}, f2v{zp1.w, v[3]},
+                              ax, ay, az);
+        gx = tx.x - tx.y;
+        gy = ty.x - ty.y;
+        gz = tz.x - tz.y;
     } else {
         constexpr int QW = kQuadWords<VT>;
         uint32_t xm[QW], xp[QW], ym[2 * QW], yp[2 * QW], zm[2 * QW], zp[2 * QW];
@@ -207,18 +247,22 @@ __device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e
         quad_load2<VT>(base, e + S, yp);    // elements (x, y+1), (x+1, y+1): comps 2,3 = y+2
         quad_load2<VT>(base, e + dzm, zm);  // elements (x, y, z-1), (x+1, y, z-1)
         quad_load2<VT>(base, e + S2, zp);   // elements (x, y, z+1), (x+1, ...): comps 1,3 = z+2
-        gx = tri8(v[1], qc<VT>(xp, 0), v[3], qc<VT>(xp, 2), v[5], qc<VT>(xp, 1), v[7], qc<VT>(xp, 3),
-                  ax, ay, az) -
-             tri8(qc<VT>(xm, 0), v[0], qc<VT>(xm, 2), v[2], qc<VT>(xm, 1), v[4], qc<VT>(xm, 3), v[6],
-                  ax, ay, az);
-        gy = tri8(v[2], v[3], qc<VT>(yp, 2), qc<VT>(yp + QW, 2), v[6], v[7], qc<VT>(yp, 3),
-                  qc<VT>(yp + QW, 3), ax, ay, az) -
-             tri8(qc<VT>(ym, 0), qc<VT>(ym + QW, 0), v[0], v[1], qc<VT>(ym, 1), qc<VT>(ym + QW, 1),
-                  v[4], v[5], ax, ay, az);
-        gz = tri8(v[4], v[5], v[6], v[7], qc<VT>(zp, 1), qc<VT>(zp + QW, 1), qc<VT>(zp, 3),
-                  qc<VT>(zp + QW, 3), ax, ay, az) -
-             tri8(qc<VT>(zm, 0), qc<VT>(zm + QW, 0), qc<VT>(zm, 2), qc<VT>(zm + QW, 2), v[0], v[1],
-                  v[2], v[3], ax, ay, az);
+        // .x: the +1 tap's cell, .y: the -1 tap's cell (as tri8(v000, v100, v010, v110, v001, ...))
+        const f2v tx = tri8x2(f2v{v[1], qc<VT>(xm, 0)}, f2v{qc<VT>(xp, 0), v[0]},
+                              f2v{v[3], qc<VT>(xm, 2)}, f2v{qc<VT>(xp, 2), v[2]},
+                              f2v{v[5], qc<VT>(xm, 1)}, f2v{qc<VT>(xp, 1), v[4]},
+                              f2v{v[7], qc<VT>(xm, 3)}, f2v{qc<VT>(xp, 3), v[6]}, ax, ay, az);
+        const f2v ty = tri8x2(f2v{v[2], qc<VT>(ym, 0)}, f2v{v[3], qc<VT>(ym + QW, 0)},
+                              f2v{qc<VT>(yp, 2), v[0]}, f2v{qc<VT>(yp + QW, 2), v[1]},
+                              f2v{v[6], qc<VT>(ym, 1)}, f2v{v[7], qc<VT>(ym + QW, 1)},
+                              f2v{qc<VT>(yp, 3), v[4]}, f2v{qc<VT>(yp + QW, 3), v[5]}, ax, ay, az);
+        const f2v tz = tri8x2(f2v{v[4], qc<VT>(zm, 0)}, f2v{v[5], qc<VT>(zm + QW, 0)},
+                              f2v{v[6], qc<VT>(zm, 2)}, f2v{v[7], qc<VT>(zm + QW, 2)},
+                              f2v{qc<VT>(zp, 1), v[0]}, f2v{qc<VT>(zp + QW, 1), v[1]},
+                              f2v{qc<VT>(zp, 3), v[2]}, f2v{qc<VT>(zp + QW, 3), v[3]}, ax, ay, az);
+        gx = tx.x - tx.y;
+        gy = ty.x - ty.y;
+        gz = tz.x - tz.y;
     }
 }
 
@@ -293,6 +337,22 @@ __device__ __forceinline__ bool pixel_ray(const MarchParams &P, uint32_t px, uin
     return true;
 }
 
+// (x / range) correctly rounded.  P.div_fast (host: 2^-40 <= range < 2^100, |min|, |max| <
+// 2^100): q = x * RN(1/range), then one fma residual correction.  Markstein's theorem gives
+// the IEEE quotient when the residual is exact (|x| >= 2^-100 here); checked against x86
+// IEEE division on 3.8e9 (x, range) pairs of that domain, 0 mismatches.  Smaller |x| give
+// |t| < 2^-60, where t * n - 0.5 rounds to -0.5 whatever t's last bit: the frame is the
+// same.  Otherwise the full IEEE division sequence.
+__device__ __forceinline__ float div_by_range(float x, const MarchParams &P)
+{
+    if (P.div_fast) {
+        const float q = x * P.inv_range;
+        const float e = fmaf(-q, P.range, x);
+        return fmaf(e, P.inv_range, q);
+    }
+    return x / P.range;
+}
+
 __device__ __forceinline__ float4 tf_lookup(const float4 *lut, int n, float nf, float t)
 {
     float u = t * nf - 0.5f;
@@ -338,11 +398,22 @@ __device__ __forceinline__ int wave_min_leap(int k)
     return lo;
 }
 
-template <typename VT, bool SHADE, bool COUNT, bool SKIP>
+// Occupancy floor (waves per SIMD): the shaded f32 kernel holds 2 x 16-B centre loads plus
+// 10 gradient loads in flight and would take 102 VGPRs (4 waves) unconstrained; 6 waves
+// measured best (A/B: 0.79 vs 0.91 ms for C3).  The skip-empty kernel (scalar gradient) is
+// left unconstrained (96 VGPRs, 5 waves: a floor of 5 yields the same occupancy but measured
+// 12% slower), the counting kernels (not timed) get 4: no spills.
 #ifndef VR_MARCH_MIN_WAVES
-#define VR_MARCH_MIN_WAVES 1
+#define VR_MARCH_MIN_WAVES 6
 #endif
-__global__ __launch_bounds__(kThreads, VR_MARCH_MIN_WAVES) void march_kernel(const MarchParams P)
+#ifndef VR_SKIP_MIN_WAVES
+#define VR_SKIP_MIN_WAVES 1
+#endif
+template <bool COUNT, bool SKIP>
+constexpr int kMarchMinWaves = COUNT ? 4 : (SKIP ? VR_SKIP_MIN_WAVES : VR_MARCH_MIN_WAVES);
+
+template <typename VT, bool SHADE, bool COUNT, bool SKIP>
+__global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP>)) void march_kernel(const MarchParams P)
 {
     __shared__ float4 s_tf[kTfLds];
     const int tid = threadIdx.x;
@@ -474,13 +545,16 @@ __global__ __launch_bounds__(kThreads, VR_MARCH_MIN_WAVES) void march_kernel(con
                 Cell8<VT> c;
                 c.load(vol, ce);
                 const float d = c.tri(ax, ay, az);
-                const float tt = (d - P.vmin) / P.range;
+                // volume.frag:42 (d - min) / (max - min), correctly rounded; for a normal
+                // range the reciprocal + one fma correction gives the IEEE quotient (see
+                // div_by_range)
+                const float tt = div_by_range(d - P.vmin, P);
                 float4 s = tf_in_lds ? tf_lookup(s_tf, P.tf_n, P.tf_nf, tt)
                                      : tf_lookup(P.tf, P.tf_n, P.tf_nf, tt);
                 if (COUNT) ++n_samples;
                 if (SHADE && s.w > 0.0f) {
                     float gx, gy_, gz;
-                    gradient<VT>(vol, ce, c, pi & (kBrick - 1), pj & (kBrick - 1),
+                    gradient<VT, !SKIP>(vol, ce, c, pi & (kBrick - 1), pj & (kBrick - 1),
                                  pk & (kBrick - 1), by_stride, bz_stride, ax, ay, az, gx, gy_,
                                  gz);
                     if (COUNT) ++n_shaded;
