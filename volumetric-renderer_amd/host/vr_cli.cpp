@@ -7,7 +7,8 @@
 // RGBA8 image as a binary PPM (the presentation shim of SURVEY.md §8f-3, headless form).
 //
 //   vr_cli <file.nhdr|file.nrrd|synthetic:N> <out.ppm> [--size WxH] [--radius R]
-//          [--rotate DX,DY] [--tf default|demo] [--shading] [--ert EPS] [--frames K]
+//          [--rotate DX,DY] [--tf default|demo] [--shading] [--ert EPS] [--skip-empty]
+//          [--frames K]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -22,14 +23,15 @@ int main(int argc, char **argv)
 {
     if (argc < 3) {
         std::fprintf(stderr, "usage: %s <file.nhdr|synthetic:N> <out.ppm> [--size WxH] [--radius R] "
-                             "[--rotate DX,DY] [--tf default|demo] [--shading] [--ert EPS] [--frames K]\n",
+                             "[--rotate DX,DY] [--tf default|demo] [--shading] [--ert EPS] [--skip-empty] "
+                             "[--frames K]\n",
                      argv[0]);
         return 2;
     }
     std::string src = argv[1], out = argv[2];
     uint32_t W = 800, H = 600;
     float radius = 3.0f, rx = 0.0f, ry = 0.0f, ert = 0.0f;
-    int shading = 0, frames = 1;
+    int shading = 0, skip_empty = 0, frames = 1;
     std::string tfname = "default";
     for (int i = 3; i < argc; ++i) {
         std::string a = argv[i];
@@ -38,6 +40,7 @@ int main(int argc, char **argv)
         else if (a == "--rotate" && i + 1 < argc) std::sscanf(argv[++i], "%f,%f", &rx, &ry);
         else if (a == "--tf" && i + 1 < argc) tfname = argv[++i];
         else if (a == "--shading") shading = 1;
+        else if (a == "--skip-empty") skip_empty = 1;
         else if (a == "--ert" && i + 1 < argc) ert = std::strtof(argv[++i], nullptr);
         else if (a == "--frames" && i + 1 < argc) frames = std::atoi(argv[++i]);
         else {
@@ -82,6 +85,7 @@ int main(int argc, char **argv)
         vr_cam_view(&oc, cam.view);
         vr_cam_position(&oc, cam.position);
         pass.params().shading = shading;
+        pass.params().skip_empty = skip_empty;
         pass.params().ert_eps = ert;
 
         auto t0 = std::chrono::steady_clock::now();
