@@ -107,7 +107,10 @@ typedef struct vr_params {
      * T *= 1 - 0), so the frame is bit-identical to skip_empty = 0 (DESIGN.md "Empty-space
      * skipping").  The brick classification is rebuilt lazily after a volume or TF change. */
     int32_t skip_empty;
-    int32_t reserved[2];
+    /* Pixel footprint of one 64-lane wavefront inside the 16x16 workgroup tile (speed only,
+     * never results): 0 auto (16x4), 1 8x8, 2 16x4, 3 4x16. */
+    int32_t wave_shape;
+    int32_t reserved[1];
 } vr_params;
 
 /* Work counters of one frame (filled by vr_count_work). */

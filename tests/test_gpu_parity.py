@@ -385,3 +385,21 @@ def test_skip_empty_tracks_tf_and_volume_changes(rp):
     a = rp.render(cam, p0, vr_amd.OUT_RGBA8)
     b = rp.render(cam, p1, vr_amd.OUT_RGBA8)
     assert np.array_equal(a, b)
+
+
+def test_work_placement_never_changes_results(rp):
+    """tile_order (XCD placement) and wave_shape (wavefront pixel footprint) only move work:
+    every combination gives the same bytes and the same work counters."""
+    W, H = 72, 56
+    rp.framebuffer_size_changed(W, H)
+    rp.volume_dataset_changed(synth.dataset(synth.gaussians_numpy((24, 20, 28), seed=8)))
+    rp.transfer_function_changed(synth.tf_color())
+    cam = synth.camera("rotA").to_vr_camera()
+    base = rp.render(cam, vr_amd.default_params(shading=1), vr_amd.OUT_RGBA32F)
+    cw = rp.count_work(cam, vr_amd.default_params(shading=1))
+    for order in (1, 2, 3):
+        for shape in (1, 2, 3):
+            p = vr_amd.default_params(shading=1, tile_order=order, wave_shape=shape)
+            img = rp.render(cam, p, vr_amd.OUT_RGBA32F)
+            assert np.array_equal(img.view(np.uint32), base.view(np.uint32)), (order, shape)
+            assert rp.count_work(cam, p) == cw, (order, shape)

@@ -101,17 +101,19 @@ def linear(vb, n):
     return fn
 
 
-def simulate(layout, n, vb, view, pos, W=1920, H=1080, ntiles=300, seed=0, line=128):
+def simulate(layout, n, vb, view, pos, W=1920, H=1080, ntiles=300, seed=0, line=128, tile=(8, 8)):
+    """tile: the wavefront's pixel footprint (tw, th), tw * th = 64 lanes."""
     rng = np.random.default_rng(seed)
-    nb = (n + 3 + 15) // 16
+    nb = (n + 3) // 4 + 1  # >= bricks per axis for any brick size >= 4 (indices stay unique)
+    tw, th = tile
     tot_instr = 0
     tot_lines = 0
     samples = 0
     tiles = 0
     while tiles < ntiles:
-        tx = rng.integers(0, W // 8)
-        ty = rng.integers(0, H // 8)
-        px, py = np.meshgrid(np.arange(8) + tx * 8, np.arange(8) + ty * 8)
+        tx = rng.integers(0, W // tw)
+        ty = rng.integers(0, H // th)
+        px, py = np.meshgrid(np.arange(tw) + tx * tw, np.arange(th) + ty * th)
         ok, pos0, dirs = rays(view, pos, W, H, px.ravel().astype(float), py.ravel().astype(float))
         if ok.sum() < 32:
             continue
@@ -136,9 +138,33 @@ def simulate(layout, n, vb, view, pos, W=1920, H=1080, ntiles=300, seed=0, line=
                 lines_per_sample=tot_lines / samples, samples=samples)
 
 
+def tile_shapes(n=512, ntiles=60):
+    """Lines per wave-level load of the shipped layouts for wavefront tile shapes 8x8, 16x4,
+    4x16, 32x2 over the sweep views."""
+    sys.path.insert(0, os.path.join(ROOT, "volumetric-renderer_amd"))
+    import synth
+    cams = {"fill": synth.camera("fill"), "fill_oblique": synth.camera("fill_oblique"),
+            "side_x": synth.vr_amd.make_camera(radius=1.6, rotate=(360.0, 0.0)),
+            "top_z": synth.vr_amd.make_camera(radius=1.6, rotate=(0.0, 360.0)),
+            "diag": synth.vr_amd.make_camera(radius=2.0, rotate=(180.0, 140.0)),
+            "default": synth.camera("default")}
+    layouts = {"f32 zpair": (brick_apron_zpair(8, 4), 4), "u8 yzquad": (brick_apron_yzquad(8, 1), 1)}
+    for cname, cam in cams.items():
+        vc = cam.to_vr_camera()
+        for lname, (fn, vb) in layouts.items():
+            row = []
+            for t in ((8, 8), (16, 4), (4, 16), (32, 2)):
+                r = simulate(fn, n, vb, list(vc.view), list(vc.position), ntiles=ntiles, tile=t)
+                row.append(f"{t[0]}x{t[1]} {r['lines_per_sample']:.3f}")
+            print(f"{cname:13s} {lname:10s} lines/sample: " + "  ".join(row), flush=True)
+
+
 if __name__ == "__main__":
     sys.path.insert(0, os.path.join(ROOT, "volumetric-renderer_amd"))
     import synth
+    if len(sys.argv) > 1 and sys.argv[1] == "tiles":
+        tile_shapes()
+        sys.exit(0)
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
     cams = {"fill": synth.camera("fill"), "fill_oblique": synth.camera("fill_oblique"),
             "side_x": synth.vr_amd.make_camera(radius=1.6, rotate=(360.0, 0.0)),

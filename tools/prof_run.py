@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--tile-order", type=int, default=0)
     ap.add_argument("--skip-empty", type=int, default=0)
+    ap.add_argument("--wave-shape", type=int, default=0)
     a = ap.parse_args()
     W, H = (int(x) for x in a.size.split("x"))
     rp = vr_amd.OffscreenPass(W, H)
@@ -41,7 +42,7 @@ def main():
     rp.transfer_function_changed(synth.TFS[a.tf]())
     cam = synth.camera(a.cam).to_vr_camera()
     p = vr_amd.default_params(shading=a.shading, ert_eps=a.ert, tile_order=a.tile_order,
-                              skip_empty=a.skip_empty)
+                              skip_empty=a.skip_empty, wave_shape=a.wave_shape)
     rp.render(cam, p, vr_amd.OUT_RGBA8)
     rp.timing_enable(True)
     for _ in range(a.frames):

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--tile-order", type=int, default=0)
     ap.add_argument("--skip-empty", type=int, default=0)
+    ap.add_argument("--wave-shape", type=int, default=0)
     args = ap.parse_args()
     W, H = (int(x) for x in args.size.split("x"))
     rp = vr_amd.OffscreenPass(W, H)
@@ -50,7 +51,7 @@ def main():
     out = torch.empty((H + 16, W), dtype=torch.int32, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
     p = vr_amd.default_params(shading=args.shading, ert_eps=args.ert, tile_order=args.tile_order,
-                              skip_empty=args.skip_empty)
+                              skip_empty=args.skip_empty, wave_shape=args.wave_shape)
     res = {}
     for name, v in VIEWS.items():
         cam = vr_amd.make_camera(**v).to_vr_camera()

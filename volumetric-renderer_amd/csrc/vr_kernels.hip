@@ -450,9 +450,12 @@ __global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP>)) void march
     const long by_stride = (long)P.nbx * kBrickElems;  // elements between brick rows/slabs
     const long bz_stride = (long)P.nbx * P.nby * kBrickElems;
 
-    const int wave = tid >> 6, lane = tid & 63;
-    const uint32_t px = tile_x * kTile + (wave & 1) * 8 + (lane & 7);
-    const uint32_t ly = tile_y * kTile + (wave >> 1) * 8 + (lane >> 3);
+    // wavefront -> (ww x wh) pixels, ww = 2^wave_w_shift, the 4 of them tiling the 16x16 tile
+    const uint32_t wave = tid >> 6, lane = tid & 63;
+    const uint32_t ws = P.wave_w_shift, ww = 1u << ws, wh = 64u >> ws;
+    const uint32_t wpr = kTile >> ws;  // wavefronts per tile row
+    const uint32_t px = tile_x * kTile + (wave % wpr) * ww + (lane & (ww - 1));
+    const uint32_t ly = tile_y * kTile + (wave / wpr) * wh + (lane >> ws);
     bool active = px < P.W && ly < P.local_rows;
     const uint32_t blk = ly / P.row_block;
     const uint32_t gy = (blk * P.nranks + P.rank) * P.row_block + (ly - blk * P.row_block);

@@ -46,7 +46,8 @@ class vr_params(C.Structure):
                 ("shading", C.c_int32), ("clear_color", C.c_float * 4),
                 ("ambient", C.c_float), ("diffuse", C.c_float), ("specular", C.c_float),
                 ("spec_power", C.c_int32), ("tile_order", C.c_int32),
-                ("skip_empty", C.c_int32), ("reserved", C.c_int32 * 2)]
+                ("skip_empty", C.c_int32), ("wave_shape", C.c_int32),
+                ("reserved", C.c_int32 * 1)]
 
 
 class vr_stats(C.Structure):
