@@ -239,6 +239,31 @@ static inline float tri_cell(const float *v, int nx, int ny, int nz, int i, int 
     return lerpf(c0, c1, az);
 }
 
+/* Gradient extension: trilinear filter (same cell, weights and lerp order as tri_cell) of
+ * the per-voxel central difference D_e(c) = v(c + e) - v(c - e) along axis e, i.e.
+ * tri(v(. + e)) - tri(v(. - e)) with the subtraction done per voxel: one rounding per
+ * difference, then the filter.  (The device reads D from precomputed arrays for f32 volumes
+ * and forms it from the 4-wide stencil otherwise; same operations either way.) */
+static inline float dvox(const float *v, int nx, int ny, int nz, int x, int y, int z, int axis)
+{
+    const int ex = axis == 0, ey = axis == 1, ez = axis == 2;
+    return voxel(v, nx, ny, nz, x + ex, y + ey, z + ez) - voxel(v, nx, ny, nz, x - ex, y - ey, z - ez);
+}
+static inline float grad_cell(const float *v, int nx, int ny, int nz, int i, int j, int k,
+                              float ax, float ay, float az, int axis)
+{
+    float c00 = lerpf(dvox(v, nx, ny, nz, i, j, k, axis), dvox(v, nx, ny, nz, i + 1, j, k, axis), ax);
+    float c10 = lerpf(dvox(v, nx, ny, nz, i, j + 1, k, axis),
+                      dvox(v, nx, ny, nz, i + 1, j + 1, k, axis), ax);
+    float c01 = lerpf(dvox(v, nx, ny, nz, i, j, k + 1, axis),
+                      dvox(v, nx, ny, nz, i + 1, j, k + 1, axis), ax);
+    float c11 = lerpf(dvox(v, nx, ny, nz, i, j + 1, k + 1, axis),
+                      dvox(v, nx, ny, nz, i + 1, j + 1, k + 1, axis), ax);
+    float c0 = lerpf(c00, c10, ay);
+    float c1 = lerpf(c01, c11, ay);
+    return lerpf(c0, c1, az);
+}
+
 /* Normalised coordinate -> texel space: u = s*N - 0.5 (texel i's centre at (i+0.5)/N). */
 static inline void texel_coord(float p, int n, int *i, float *a)
 {
@@ -348,13 +373,10 @@ static void march_pixel(const or_scene *s, const ray_frame *f, const float *lut,
             tf_lookup(lut, s->tf_n, t, sc); /* :43 */
             st->samples++;
             if (s->shading && sc[3] > 0.0f) {
-                /* extension: central differences one texel apart, same weights */
-                const float gx = tri_cell(s->vol, nx, ny, nz, i + 1, j, k, ax, ay, az) -
-                                 tri_cell(s->vol, nx, ny, nz, i - 1, j, k, ax, ay, az);
-                const float gy = tri_cell(s->vol, nx, ny, nz, i, j + 1, k, ax, ay, az) -
-                                 tri_cell(s->vol, nx, ny, nz, i, j - 1, k, ax, ay, az);
-                const float gz = tri_cell(s->vol, nx, ny, nz, i, j, k + 1, ax, ay, az) -
-                                 tri_cell(s->vol, nx, ny, nz, i, j, k - 1, ax, ay, az);
+                /* extension: central differences one texel apart, same weights (grad_cell) */
+                const float gx = grad_cell(s->vol, nx, ny, nz, i, j, k, ax, ay, az, 0);
+                const float gy = grad_cell(s->vol, nx, ny, nz, i, j, k, ax, ay, az, 1);
+                const float gz = grad_cell(s->vol, nx, ny, nz, i, j, k, ax, ay, az, 2);
                 st->shaded_samples++;
                 const float wx = gx * (float)nx, wy = gy * (float)ny, wz = gz * (float)nz;
                 const float g2 = wx * wx + wy * wy + wz * wz;

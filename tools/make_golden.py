@@ -189,7 +189,12 @@ def nrrd_files():
 
 
 if __name__ == "__main__":
+    # optional argument: only the named parts (scenes, kat_b4, nrrd)
+    parts = sys.argv[1:] or ["scenes", "kat_b4", "nrrd"]
     os.makedirs(GOLD, exist_ok=True)
-    scenes()
-    kat_b4()
-    nrrd_files()
+    if "scenes" in parts:
+        scenes()
+    if "kat_b4" in parts:
+        kat_b4()
+    if "nrrd" in parts:
+        nrrd_files()

@@ -11,6 +11,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -41,6 +42,11 @@ struct vr_ctx {
     uint8_t *skip_dist = nullptr;  // 2 x nbricks: distance field + pass scratch
     size_t nbricks_alloc = 0;
     bool range_valid = false, dist_valid = false;
+    // f32 shading: precomputed central differences (3 x the bricked density), built lazily
+    // on the first shaded frame after a volume change; absent when memory is short
+    float *grad = nullptr;
+    size_t grad_bytes = 0;
+    bool grad_valid = false;
     // scratch
     unsigned long long *counters = nullptr;
     void *frame_dev = nullptr;
@@ -247,6 +253,7 @@ struct SplitMix {
 int set_bricks(vr_ctx *c, int storage, uint32_t nx, uint32_t ny, uint32_t nz, void **out)
 {
     c->range_valid = c->dist_valid = false;  // the bricks are about to be rewritten
+    c->grad_valid = false;
     const size_t bytes = (size_t)bricks_for(nx) * bricks_for(ny) * bricks_for(nz) *
                          kBrickElems * element_size(storage);
     if (c->bricks && c->brick_bytes == bytes) {
@@ -414,6 +421,38 @@ int ensure_skip(vr_ctx *c, MarchParams &P, hipStream_t s)
     return VR_OK;
 }
 
+// Shaded f32 frames: (re)build the gradient field when stale.  It needs 3 x the bricked
+// density; when that does not fit beside a 2 GiB reserve the kernel forms the differences
+// from the 4-wide stencil instead (same values, bit for bit).
+void ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s)
+{
+    if (c->storage != ST_F32) return;
+    if (std::getenv("VR_NO_GRAD_FIELD")) return;  // A/B and tests: the stencil path
+    const size_t bytes = c->brick_bytes / element_size(ST_F32) * kGradElemBytes;
+    if (!c->grad || c->grad_bytes != bytes) {
+        if (c->grad) hipFree(c->grad);
+        c->grad = nullptr;
+        c->grad_bytes = 0;
+        c->grad_valid = false;
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < bytes + (2ull << 30)) return;
+        void *g = nullptr;
+        if (hipMalloc(&g, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            return;
+        }
+        c->grad = static_cast<float *>(g);
+        c->grad_bytes = bytes;
+    }
+    if (!c->grad_valid) {
+        if (launch_grad_field(static_cast<const float *>(c->bricks), c->grad, c->nx, c->ny, c->nz,
+                              s) != hipSuccess)
+            return;
+        c->grad_valid = true;
+    }
+    P.grad = c->grad;
+}
+
 hipEvent_t pooled_event(vr_ctx *c)
 {
     if (!c->ev_pool.empty()) {
@@ -511,6 +550,7 @@ void vr_destroy(vr_ctx *c)
     if (c->tf_nz) hipFree(c->tf_nz);
     if (c->brick_range) hipFree(c->brick_range);
     if (c->skip_dist) hipFree(c->skip_dist);
+    if (c->grad) hipFree(c->grad);
     if (c->counters) hipFree(c->counters);
     if (c->frame_dev) hipFree(c->frame_dev);
     delete c;
@@ -754,6 +794,7 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
         rc = ensure_skip(c, P, s);
         if (rc) return rc;
     }
+    if (p->shading) ensure_grad(c, P, s);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing) {
         e0 = pooled_event(c);
@@ -826,6 +867,7 @@ int vr_count_work(vr_ctx *c, const vr_camera *cam, const vr_params *p, uint32_t 
         rc = ensure_skip(c, P, nullptr);
         if (rc) return rc;
     }
+    if (p->shading) ensure_grad(c, P, nullptr);
     HIP_TRY(c, hipMemset(c->counters, 0, 8 * sizeof(unsigned long long)), "hipMemset(counters)");
     HIP_TRY(c, launch_march(c->storage, p->shading != 0, true, P, nullptr), "march (count) launch");
     unsigned long long h[5];
@@ -878,7 +920,9 @@ int vr_timing_reset(vr_ctx *c)
 const char *vr_kernel_name(const vr_ctx *c, const vr_params *p)
 {
     if (!c) return "";
-    return march_kernel_name(c->storage, p && p->shading != 0, false, p && p->skip_empty != 0);
+    // the variant the next vr_render_device launches (after a shaded frame built the field)
+    const bool gf = p && p->shading && c->storage == ST_F32 && c->grad && c->grad_valid;
+    return march_kernel_name(c->storage, p && p->shading != 0, false, p && p->skip_empty != 0, gf);
 }
 
 }  // extern "C"

@@ -88,13 +88,16 @@ struct MarchParams {
     const uint8_t *skip_dist;
     int32_t skip_empty;
     int32_t div_fast;       // density normalisation by reciprocal + fma correction
+    // f32 shading: precomputed central differences, element e = {Dx, Dy, Dz} x {z, z + 1}
+    // (24 B, same element index as the density); null -> formed from the stencil
+    const float *grad;
     float inv_range;        // RN(1 / range) (div_fast)
 };
 
 // Launchers (vr_kernels.hip).  All asynchronous on `stream`.
 hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &p,
                         hipStream_t stream);
-const char *march_kernel_name(int storage, bool shade, bool count, bool skip);
+const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bool gf);
 hipError_t launch_brick_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,
                                     uint32_t ny, uint32_t nz, int storage, hipStream_t stream);
 // Synthetic volume into a LINEAR buffer of the storage type (then bricked).
@@ -112,6 +115,10 @@ hipError_t launch_minmax(int storage, const void *linear, size_t count, float *m
 // (volume, TF) the capped Chebyshev distance field over the brick grid (1 byte per brick;
 // scratch_dev: the same size, for the separable passes).
 constexpr int kSkipCap = 16;
+// f32 gradient field (see MarchParams::grad) from the bricked density: same brick grid.
+constexpr size_t kGradElemBytes = 24;
+hipError_t launch_grad_field(const float *bricks, float *grad, uint32_t nx, uint32_t ny,
+                             uint32_t nz, hipStream_t stream);
 hipError_t launch_brick_range(int storage, const void *bricks, uint32_t nbricks,
                               float2 *range_dev, hipStream_t stream);
 hipError_t launch_skip_dist(const float2 *range_dev, uint32_t nbx, uint32_t nby, uint32_t nbz,

@@ -189,14 +189,32 @@ struct Cell8 {
     }
 };
 
-// Central-difference gradient (extension): the cells one texel either side along each axis
-// share the centre cell's weights, so only the 4-wide stencil's outer voxels are new
-// (24 voxels: 10 loads for z-pair f32, 6 for yz-quads).  PACKED: each axis' +1/-1 pair of
-// trilinears as one packed-FP32 trilinear (half the VALU, more VGPRs; the z-pair scalar form
-// is kept for the register-tight skip-empty kernel).  Taps one element below, or two
-// above in z-pair x/y, may sit in the neighbouring brick (the apron covers +1): the per-axis
-// deltas pick that brick.  Bit-identical to six independent trilinear fetches (same voxels,
-// same operations), which is what the oracle computes.
+// Central-difference gradient (extension): per axis e, the trilinear filter (the centre
+// cell's weights, tri8's lerp order) of the per-voxel difference D_e(c) = v(c+e) - v(c-e)
+// over the cell's 8 corners -- the oracle's grad_cell.  The differences need the 4-wide
+// stencil's 24 outer voxels (10 loads for z-pair f32, 6 for yz-quads).  Taps one element
+// below, or two above in z-pair x/y, may sit in the neighbouring brick (the apron covers
+// +1): the per-axis deltas pick that brick.  Corner index: dx + 2 dy + 4 dz.
+// PACKED: D_x / D_y and their filters as packed-FP32 pairs (fewer VALU, more VGPRs; the
+// scalar form serves the register-tight skip-empty kernel).
+template <bool PACKED>
+__device__ __forceinline__ void grad_filter(const float *dx, const float *dy, const float *dz,
+                                            float ax, float ay, float az, float &gx, float &gy,
+                                            float &gz)
+{
+    if constexpr (PACKED) {
+        const f2v g = tri8x2(f2v{dx[0], dy[0]}, f2v{dx[1], dy[1]}, f2v{dx[2], dy[2]},
+                             f2v{dx[3], dy[3]}, f2v{dx[4], dy[4]}, f2v{dx[5], dy[5]},
+                             f2v{dx[6], dy[6]}, f2v{dx[7], dy[7]}, ax, ay, az);
+        gx = g.x;
+        gy = g.y;
+    } else {
+        gx = tri8(dx[0], dx[1], dx[2], dx[3], dx[4], dx[5], dx[6], dx[7], ax, ay, az);
+        gy = tri8(dy[0], dy[1], dy[2], dy[3], dy[4], dy[5], dy[6], dy[7], ax, ay, az);
+    }
+    gz = tri8(dz[0], dz[1], dz[2], dz[3], dz[4], dz[5], dz[6], dz[7], ax, ay, az);
+}
+
 template <typename VT, bool PACKED>
 __device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e,
                                          const Cell8<VT> &c, int lx, int ly, int lz,
@@ -209,61 +227,79 @@ __device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e
     const long dym = ly > 0 ? -S : (L * S - by_stride);
     const long dzm = lz > 0 ? -S2 : (L * S2 - bz_stride);
     const float *v = c.v;
+    float Dx[8], Dy[8], Dz[8];
     if constexpr (kZPair<VT>) {
         const long dyp = ly < L ? 2 * S : (by_stride - (L - 1) * S);
+        // z-pairs (.x = z, .y = z + 1) of the x - 1 and x + 2 columns, rows y and y + 1
         const f2a xm0 = zpair_load1(base, e + dxm), xm1 = zpair_load1(base, e + dxm + S);
         const f2a xp0 = zpair_load1(base, e + dxp), xp1 = zpair_load1(base, e + dxp + S);
+        // elements x, x + 1 of rows y - 1 and y + 2: (.x, .y) column x, (.z, .w) column x + 1
         const f4a ym = zpair_load2(base, e + dym), yp = zpair_load2(base, e + dyp);
+        // elements x, x + 1 at z - 1 (pairs z - 1, z) and z + 1 (pairs z + 1, z + 2)
         const f4a zm0 = zpair_load2(base, e + dzm), zm1 = zpair_load2(base, e + dzm + S);
         const f4a zp0 = zpair_load2(base, e + S2), zp1 = zpair_load2(base, e + S2 + S);
-        if constexpr (!PACKED) {
-            gx = tri8(v[1], xp0.x, v[3], xp1.x, v[5], xp0.y, v[7], xp1.y, ax, ay, az) -
-                 tri8(xm0.x, v[0], xm1.x, v[2], xm0.y, v[4], xm1.y, v[6], ax, ay, az);
-            gy = tri8(v[2], v[3], yp.x, yp.z, v[6], v[7], yp.y, yp.w, ax, ay, az) -
-                 tri8(ym.x, ym.z, v[0], v[1], ym.y, ym.w, v[4], v[5], ax, ay, az);
-            gz = tri8(v[4], v[5], v[6], v[7], zp0.y, zp0.w, zp1.y, zp1.w, ax, ay, az) -
-                 tri8(zm0.x, zm0.z, zm1.x, zm1.z, v[0], v[1], v[2], v[3], ax, ay, az);
-            return;
-        }
-        // .x: the +1 tap's cell, .y: the -1 tap's cell, one packed trilinear per axis
-        const f2v tx = tri8x2(f2v{v[1], xm0.x}, f2v{xp0.x, v[0]}, f2v{v[3], xm1.x}, f2v{xp1.x, v[2]},
-                              f2v{v[5], xm0.y}, f2v{xp0.y, v[4]}, f2v{v[7], xm1.y}, f2v{xp1.y, v[6]},
-                              ax, ay, az);
-        const f2v ty = tri8x2(f2v{v[2], ym.x}, f2v{v[3], ym.z}, f2v{yp.x, v[0]}, f2v{yp.z, v[1]},
-                              f2v{v[6], ym.y}, f2v{v[7], ym.w}, f2v{yp.y, v[4]}, f2v{yp.w, v[5]},
-                              ax, ay, az);
-        const f2v tz = tri8x2(f2v{v[4], zm0.x}, f2v{v[5], zm0.z}, f2v{v[6], zm1.x}, f2v{v[7], zm1.z},
-                              f2v{zp0.y, v[0]}, f2v{zp0.w, v[1]}, f2v{zp1.y, v[2]}, f2v{zp1.w, v[3]},
-                              ax, ay, az);
-        gx = tx.x - tx.y;
-        gy = ty.x - ty.y;
-        gz = tz.x - tz.y;
+        Dx[0] = v[1] - xm0.x; Dx[1] = xp0.x - v[0]; Dx[2] = v[3] - xm1.x; Dx[3] = xp1.x - v[2];
+        Dx[4] = v[5] - xm0.y; Dx[5] = xp0.y - v[4]; Dx[6] = v[7] - xm1.y; Dx[7] = xp1.y - v[6];
+        Dy[0] = v[2] - ym.x;  Dy[1] = v[3] - ym.z;  Dy[2] = yp.x - v[0];  Dy[3] = yp.z - v[1];
+        Dy[4] = v[6] - ym.y;  Dy[5] = v[7] - ym.w;  Dy[6] = yp.y - v[4];  Dy[7] = yp.w - v[5];
+        Dz[0] = v[4] - zm0.x; Dz[1] = v[5] - zm0.z; Dz[2] = v[6] - zm1.x; Dz[3] = v[7] - zm1.z;
+        Dz[4] = zp0.y - v[0]; Dz[5] = zp0.w - v[1]; Dz[6] = zp1.y - v[2]; Dz[7] = zp1.w - v[3];
     } else {
         constexpr int QW = kQuadWords<VT>;
         uint32_t xm[QW], xp[QW], ym[2 * QW], yp[2 * QW], zm[2 * QW], zp[2 * QW];
-        quad_load1<VT>(base, e + dxm, xm);
-        quad_load1<VT>(base, e + dxp, xp);
-        quad_load2<VT>(base, e + dym, ym);  // elements (x, y-1), (x+1, y-1)
-        quad_load2<VT>(base, e + S, yp);    // elements (x, y+1), (x+1, y+1): comps 2,3 = y+2
-        quad_load2<VT>(base, e + dzm, zm);  // elements (x, y, z-1), (x+1, y, z-1)
-        quad_load2<VT>(base, e + S2, zp);   // elements (x, y, z+1), (x+1, ...): comps 1,3 = z+2
-        // .x: the +1 tap's cell, .y: the -1 tap's cell (as tri8(v000, v100, v010, v110, v001, ...))
-        const f2v tx = tri8x2(f2v{v[1], qc<VT>(xm, 0)}, f2v{qc<VT>(xp, 0), v[0]},
-                              f2v{v[3], qc<VT>(xm, 2)}, f2v{qc<VT>(xp, 2), v[2]},
-                              f2v{v[5], qc<VT>(xm, 1)}, f2v{qc<VT>(xp, 1), v[4]},
-                              f2v{v[7], qc<VT>(xm, 3)}, f2v{qc<VT>(xp, 3), v[6]}, ax, ay, az);
-        const f2v ty = tri8x2(f2v{v[2], qc<VT>(ym, 0)}, f2v{v[3], qc<VT>(ym + QW, 0)},
-                              f2v{qc<VT>(yp, 2), v[0]}, f2v{qc<VT>(yp + QW, 2), v[1]},
-                              f2v{v[6], qc<VT>(ym, 1)}, f2v{v[7], qc<VT>(ym + QW, 1)},
-                              f2v{qc<VT>(yp, 3), v[4]}, f2v{qc<VT>(yp + QW, 3), v[5]}, ax, ay, az);
-        const f2v tz = tri8x2(f2v{v[4], qc<VT>(zm, 0)}, f2v{v[5], qc<VT>(zm + QW, 0)},
-                              f2v{v[6], qc<VT>(zm, 2)}, f2v{v[7], qc<VT>(zm + QW, 2)},
-                              f2v{qc<VT>(zp, 1), v[0]}, f2v{qc<VT>(zp + QW, 1), v[1]},
-                              f2v{qc<VT>(zp, 3), v[2]}, f2v{qc<VT>(zp + QW, 3), v[3]}, ax, ay, az);
-        gx = tx.x - tx.y;
-        gy = ty.x - ty.y;
-        gz = tz.x - tz.y;
+        quad_load1<VT>(base, e + dxm, xm);  // (x-1): comps (y,z) (y,z+1) (y+1,z) (y+1,z+1)
+        quad_load1<VT>(base, e + dxp, xp);  // (x+2)
+        quad_load2<VT>(base, e + dym, ym);  // (x, y-1), (x+1, y-1): comps 0,1 = y-1
+        quad_load2<VT>(base, e + S, yp);    // (x, y+1), (x+1, y+1): comps 2,3 = y+2
+        quad_load2<VT>(base, e + dzm, zm);  // (x, y, z-1), (x+1, y, z-1): comps 0,2 = z-1
+        quad_load2<VT>(base, e + S2, zp);   // (x, y, z+1), (x+1, y, z+1): comps 1,3 = z+2
+#pragma unroll
+        for (int dz_ = 0; dz_ < 2; ++dz_)
+#pragma unroll
+            for (int dy_ = 0; dy_ < 2; ++dy_) {
+                const int q = dz_ + 2 * dy_, o = 2 * dy_ + 4 * dz_;
+                Dx[o] = v[o + 1] - qc<VT>(xm, q);
+                Dx[o + 1] = qc<VT>(xp, q) - v[o];
+            }
+#pragma unroll
+        for (int dz_ = 0; dz_ < 2; ++dz_)
+#pragma unroll
+            for (int dx_ = 0; dx_ < 2; ++dx_) {
+                const int o = dx_ + 4 * dz_;
+                Dy[o] = v[o + 2] - qc<VT>(ym + dx_ * QW, dz_);
+                Dy[o + 2] = qc<VT>(yp + dx_ * QW, 2 + dz_) - v[o];
+            }
+#pragma unroll
+        for (int dy_ = 0; dy_ < 2; ++dy_)
+#pragma unroll
+            for (int dx_ = 0; dx_ < 2; ++dx_) {
+                const int o = dx_ + 2 * dy_;
+                Dz[o] = v[o + 4] - qc<VT>(zm + dx_ * QW, 2 * dy_);
+                Dz[o + 4] = qc<VT>(zp + dx_ * QW, 2 * dy_ + 1) - v[o];
+            }
     }
+    grad_filter<PACKED>(Dx, Dy, Dz, ax, ay, az, gx, gy, gz);
+}
+
+// Gradient from the precomputed f32 field: the cell's 8 corners of {Dx, Dy, Dz}, rows y and
+// y + 1 of elements x, x + 1 (48 B each: 3 x 16-B loads), filtered as grad_filter.
+template <bool PACKED>
+__device__ __forceinline__ void grad_field(const char *__restrict__ gbase, size_t e, float ax,
+                                           float ay, float az, float &gx, float &gy, float &gz)
+{
+    float Dx[8], Dy[8], Dz[8];
+#pragma unroll
+    for (int dy_ = 0; dy_ < 2; ++dy_) {
+        const char *row = gbase + (e + (size_t)dy_ * kStore) * kGradElemBytes;
+        const f4a r0 = *reinterpret_cast<const f4a *>(row);       // Dx(x) z,z+1  Dy(x) z,z+1
+        const f4a r1 = *reinterpret_cast<const f4a *>(row + 16);  // Dz(x) z,z+1  Dx(x+1) z,z+1
+        const f4a r2 = *reinterpret_cast<const f4a *>(row + 32);  // Dy(x+1) ...  Dz(x+1) ...
+        const int o = 2 * dy_;  // corner dx + 2 dy + 4 dz
+        Dx[o] = r0.x; Dx[o + 4] = r0.y; Dy[o] = r0.z; Dy[o + 4] = r0.w;
+        Dz[o] = r1.x; Dz[o + 4] = r1.y; Dx[o + 1] = r1.z; Dx[o + 5] = r1.w;
+        Dy[o + 1] = r2.x; Dy[o + 5] = r2.y; Dz[o + 1] = r2.z; Dz[o + 5] = r2.w;
+    }
+    grad_filter<PACKED>(Dx, Dy, Dz, ax, ay, az, gx, gy, gz);
 }
 
 __device__ __forceinline__ void texel_coord(float p, float n, int &i, float &a)
@@ -409,11 +445,19 @@ __device__ __forceinline__ int wave_min_leap(int k)
 #ifndef VR_SKIP_MIN_WAVES
 #define VR_SKIP_MIN_WAVES 1
 #endif
-template <bool COUNT, bool SKIP>
-constexpr int kMarchMinWaves = COUNT ? 4 : (SKIP ? VR_SKIP_MIN_WAVES : VR_MARCH_MIN_WAVES);
+template <bool COUNT, bool SKIP, bool GF>
+constexpr int kMarchMinWaves = GF ? 1 : (COUNT ? 4 : (SKIP ? VR_SKIP_MIN_WAVES : VR_MARCH_MIN_WAVES));
 
-template <typename VT, bool SHADE, bool COUNT, bool SKIP>
-__global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP>)) void march_kernel(const MarchParams P)
+#ifndef VR_SKIP_PACKED_GRADIENT
+#define VR_SKIP_PACKED_GRADIENT 0
+#endif
+template <bool SKIP>
+constexpr bool kPackedGradient = !SKIP || VR_SKIP_PACKED_GRADIENT;
+
+// GF: shaded f32 with the precomputed difference field (P.grad); without it the kernel forms
+// the differences from the stencil (60 vs 80 VGPRs: 8 vs 6 waves per SIMD).
+template <typename VT, bool SHADE, bool COUNT, bool SKIP, bool GF>
+__global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP, GF>)) void march_kernel(const MarchParams P)
 {
     __shared__ float4 s_tf[kTfLds];
     const int tid = threadIdx.x;
@@ -557,9 +601,14 @@ __global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP>)) void march
                 if (COUNT) ++n_samples;
                 if (SHADE && s.w > 0.0f) {
                     float gx, gy_, gz;
-                    gradient<VT, !SKIP>(vol, ce, c, pi & (kBrick - 1), pj & (kBrick - 1),
-                                 pk & (kBrick - 1), by_stride, bz_stride, ax, ay, az, gx, gy_,
-                                 gz);
+                    if constexpr (GF) {  // f32: precomputed difference field
+                        grad_field<kPackedGradient<SKIP>>(reinterpret_cast<const char *>(P.grad),
+                                                          ce, ax, ay, az, gx, gy_, gz);
+                    } else {
+                        gradient<VT, kPackedGradient<SKIP>>(
+                            vol, ce, c, pi & (kBrick - 1), pj & (kBrick - 1), pk & (kBrick - 1),
+                            by_stride, bz_stride, ax, ay, az, gx, gy_, gz);
+                    }
                     if (COUNT) ++n_shaded;
                     const float wx = gx * P.fnx, wy = gy_ * P.fny, wz = gz * P.fnz;
                     const float g2 = wx * wx + wy * wy + wz * wz;
@@ -741,6 +790,52 @@ __global__ __launch_bounds__(256) void minmax_kernel(const VT *__restrict__ vol,
     }
 }
 
+// ---- f32 gradient field (shading) ------------------------------------------------------------
+
+// Voxel at padded coordinates (p = logical + kPad) from the bricked z-pair density: component
+// 0 of the element at p in brick p >> kBrickShift; 0 outside the logical volume.
+__device__ __forceinline__ float padded_voxel(const float *__restrict__ bricks, int px, int py,
+                                              int pz, uint32_t nx, uint32_t ny, uint32_t nz,
+                                              uint32_t nbx, uint32_t nby)
+{
+    if (px < kPad || py < kPad || pz < kPad || px >= (int)nx + kPad || py >= (int)ny + kPad ||
+        pz >= (int)nz + kPad)
+        return 0.0f;
+    return bricks[2 * cell_offset(px, py, pz, nbx, nby)];
+}
+
+// One thread per stored element: D_e(p) = v(p + e) - v(p - e) (the oracle's dvox) for the
+// element's two voxels p = (x, y, z) and (x, y, z + 1), written as {Dx, Dx', Dy, Dy', Dz, Dz'}.
+__global__ __launch_bounds__(256) void grad_field_kernel(const float *__restrict__ bricks,
+                                                         float *__restrict__ grad, uint32_t nx,
+                                                         uint32_t ny, uint32_t nz, uint32_t nbx,
+                                                         uint32_t nby, size_t total)
+{
+    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+         g += (size_t)gridDim.x * blockDim.x) {
+        const size_t bidx = g / kBrickElems;
+        const uint32_t l = (uint32_t)(g - bidx * kBrickElems);
+        const uint32_t lx = l % kStore, lyz = l / kStore, lyy = lyz % kStore, lz = lyz / kStore;
+        const uint32_t bx = (uint32_t)(bidx % nbx), byz = (uint32_t)(bidx / nbx);
+        const uint32_t by = byz % nby, bz = byz / nby;
+        const int x = (int)(bx * kBrick + lx), y = (int)(by * kBrick + lyy), z = (int)(bz * kBrick + lz);
+        float out[6];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int zz = z + h;
+            auto V = [&](int dx, int dy, int dz) {
+                return padded_voxel(bricks, x + dx, y + dy, zz + dz, nx, ny, nz, nbx, nby);
+            };
+            out[0 + h] = V(1, 0, 0) - V(-1, 0, 0);
+            out[2 + h] = V(0, 1, 0) - V(0, -1, 0);
+            out[4 + h] = V(0, 0, 1) - V(0, 0, -1);
+        }
+        float *o = grad + 6 * g;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) o[k] = out[k];
+    }
+}
+
 // ---- empty-space classification (skip_empty) --------------------------------------------------
 
 // One wavefront per brick: min/max over every voxel its stored elements hold (apron and zero
@@ -857,13 +952,13 @@ __global__ __launch_bounds__(256) void assemble_kernel(const PixT *__restrict__ 
     }
 }
 
-template <typename VT, bool SHADE, bool COUNT, bool SKIP>
+template <typename VT, bool SHADE, bool COUNT, bool SKIP, bool GF = false>
 hipError_t launch_march_t(const MarchParams &p, hipStream_t stream)
 {
     const uint32_t nblocks = p.tile_order == 3 ? ((p.supers_total + 7) / 8) * 8 * 16
                                                : p.tiles_x * p.tiles_y;
     if (p.tiles_x * p.tiles_y == 0) return hipSuccess;
-    hipLaunchKernelGGL((march_kernel<VT, SHADE, COUNT, SKIP>), dim3(nblocks), dim3(kThreads), 0,
+    hipLaunchKernelGGL((march_kernel<VT, SHADE, COUNT, SKIP, GF>), dim3(nblocks), dim3(kThreads), 0,
                        stream, p);
     return hipGetLastError();
 }
@@ -871,6 +966,15 @@ hipError_t launch_march_t(const MarchParams &p, hipStream_t stream)
 template <typename VT>
 hipError_t launch_march_vt(bool shade, bool count, const MarchParams &p, hipStream_t s)
 {
+    if constexpr (kZPair<VT>) {
+        if (shade && p.grad) {
+            if (p.skip_empty)
+                return count ? launch_march_t<VT, true, true, true, true>(p, s)
+                             : launch_march_t<VT, true, false, true, true>(p, s);
+            return count ? launch_march_t<VT, true, true, false, true>(p, s)
+                         : launch_march_t<VT, true, false, false, true>(p, s);
+        }
+    }
     if (p.skip_empty) {
         if (shade)
             return count ? launch_march_t<VT, true, true, true>(p, s)
@@ -923,21 +1027,23 @@ hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &
     }
 }
 
-const char *march_kernel_name(int storage, bool shade, bool count, bool skip)
+const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bool gf)
 {
     // demangled names as rocprofv3 reports them (kernel-trace "Kernel_Name")
     static const std::vector<std::string> names = [] {
         const char *types[5] = {"unsigned char", "signed char", "unsigned short", "short", "float"};
         std::vector<std::string> v;
         for (int t = 0; t < 5; ++t)
-            for (int k = 0; k < 8; ++k)
+            for (int k = 0; k < 16; ++k)
                 v.push_back(std::string("void vr::(anonymous namespace)::march_kernel<") + types[t] +
-                            ((k & 4) ? ", true" : ", false") + ((k & 2) ? ", true" : ", false") +
-                            ((k & 1) ? ", true" : ", false") + ">(vr::MarchParams)");
+                            ((k & 8) ? ", true" : ", false") + ((k & 4) ? ", true" : ", false") +
+                            ((k & 2) ? ", true" : ", false") + ((k & 1) ? ", true" : ", false") +
+                            ">(vr::MarchParams)");
         return v;
     }();
     if (storage < 0 || storage > 4) return "march_kernel<?>";
-    return names[storage * 8 + (shade ? 4 : 0) + (count ? 2 : 0) + (skip ? 1 : 0)].c_str();
+    return names[storage * 16 + (shade ? 8 : 0) + (count ? 4 : 0) + (skip ? 2 : 0) + (gf ? 1 : 0)]
+        .c_str();
 }
 
 hipError_t launch_brick_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,
@@ -1014,6 +1120,16 @@ hipError_t launch_brick_range(int storage, const void *bricks, uint32_t nbricks,
         case ST_I16: hipLaunchKernelGGL((brick_range_kernel<int16_t>), dim3(g), dim3(256), 0, s, (const int16_t *)bricks, nbricks, per, range_dev); break;
         default: hipLaunchKernelGGL((brick_range_kernel<float>), dim3(g), dim3(256), 0, s, (const float *)bricks, nbricks, per, range_dev); break;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_grad_field(const float *bricks, float *grad, uint32_t nx, uint32_t ny,
+                             uint32_t nz, hipStream_t s)
+{
+    const uint32_t nbx = bricks_for(nx), nby = bricks_for(ny), nbz = bricks_for(nz);
+    const size_t total = (size_t)nbx * nby * nbz * kBrickElems;
+    hipLaunchKernelGGL(grad_field_kernel, dim3(grid_for(total)), dim3(256), 0, s, bricks, grad,
+                       nx, ny, nz, nbx, nby, total);
     return hipGetLastError();
 }
 
