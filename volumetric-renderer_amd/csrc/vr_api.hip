@@ -383,6 +383,8 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.supers_x = (P.tiles_x + 3) / 4;
     P.supers_total = P.supers_x * ((P.tiles_y + 3) / 4);
     P.out_format = out_format;
+    P.slab_default = c->smin[0] == 0.0f && c->smin[1] == 0.0f && c->smin[2] == 0.0f &&
+                     c->smax[0] == 1.0f && c->smax[1] == 1.0f && c->smax[2] == 1.0f;
     return VR_OK;
 }
 

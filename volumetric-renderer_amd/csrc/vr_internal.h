@@ -83,6 +83,7 @@ struct MarchParams {
     uint32_t supers_x, supers_total;  // super-tile grid (tile_order 3)
     uint32_t wave_w_shift;  // wavefront pixel footprint: 2^shift x (64 >> shift) (8x8: 3)
     int32_t out_format;
+    int32_t slab_default;   // slicing is the whole volume (0,0,0)-(1,1,1)
     // skip_empty: per brick (index as in cell_offset) the Chebyshev distance in bricks to the
     // nearest brick that can produce a visible sample, capped at kSkipCap; 0 = not empty
     const uint8_t *skip_dist;

@@ -302,6 +302,30 @@ __device__ __forceinline__ void grad_field(const char *__restrict__ gbase, size_
     grad_filter<PACKED>(Dx, Dy, Dz, ax, ay, az, gx, gy, gz);
 }
 
+// Steps k in [1, K] of a ray whose positions provably stay strictly inside (0, 1)^3, where the
+// reference's bounds test (volume.frag:34-37) never breaks and, with the default slicing, the
+// strict slab test (:39-40) always passes: the loop skips both there.  p_k is p_0 plus k float
+// additions of s = fl(d * step); while |p| < 1 each addition rounds by at most 2^-25, so with
+// delta = 2^-24 per step, p_k lies within p_0 + k s +- k delta.  Each bound is linear in k:
+// f(k) = A + B k > 0 holds on [1, K] iff it holds at both ends.
+__device__ __forceinline__ int interior_steps(const float *p, const float *d, float step,
+                                              int nsteps)
+{
+    constexpr double delta = 0x1p-24;
+    double K = (double)(nsteps - 1);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const double s = (double)(d[a] * step), q = (double)p[a];
+        const double A[2] = {q, 1.0 - q}, B[2] = {s - delta, -(s + delta)};
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (!(A[c] + B[c] > 0.0)) return 0;
+            if (B[c] < 0.0) K = fmin(K, floor(A[c] / -B[c]) - 1.0);
+        }
+    }
+    return K > 0.0 ? (int)K : 0;
+}
+
 __device__ __forceinline__ void texel_coord(float p, float n, int &i, float &a)
 {
     const float u = p * n - 0.5f;
@@ -515,6 +539,8 @@ __global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP, GF>)) void m
     const int nsteps = covered ? P.nsteps : 0;
     float p0 = tex[0], p1 = tex[1], p2 = tex[2];
     const float d0 = dir[0], d1 = dir[1], d2 = dir[2];
+    // steps 1..kin need neither the bounds nor (default slicing) the slab test
+    const int kin = (covered && P.slab_default) ? interior_steps(tex, dir, P.step, nsteps) : 0;
     // skip_empty leap constants: steps per cell along each axis, and a margin (cells) covering
     // the leap's float-accumulation drift (<= kMaxLeap half-ulps of p < 2, times N) + rounding
     float inv_du[3] = {0.f, 0.f, 0.f}, leap_margin[3] = {0.f, 0.f, 0.f};
@@ -527,12 +553,15 @@ __global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP, GF>)) void m
         }
     }
     for (int it = 0; it < nsteps; ++it) {
+        const bool interior = (unsigned)(it - 1) < (unsigned)kin;  // it in [1, kin]
         // volume.frag:34-37
-        if (p0 > 1.0f || p1 > 1.0f || p2 > 1.0f || p0 < 0.0f || p1 < 0.0f || p2 < 0.0f) break;
+        if (!interior &&
+            (p0 > 1.0f || p1 > 1.0f || p2 > 1.0f || p0 < 0.0f || p1 < 0.0f || p2 < 0.0f))
+            break;
         if (COUNT) ++n_steps;
         // volume.frag:39-40 (strict)
-        if (p0 < P.smax[0] && p1 < P.smax[1] && p2 < P.smax[2] && p0 > P.smin[0] &&
-            p1 > P.smin[1] && p2 > P.smin[2]) {
+        if (interior || (p0 < P.smax[0] && p1 < P.smax[1] && p2 < P.smax[2] && p0 > P.smin[0] &&
+                         p1 > P.smin[1] && p2 > P.smin[2])) {
             int i, j, k;
             float ax, ay, az;
             texel_coord(p0, P.fnx, i, ax);
