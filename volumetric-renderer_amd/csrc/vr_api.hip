@@ -276,12 +276,17 @@ int set_bricks(vr_ctx *c, int storage, uint32_t nx, uint32_t ny, uint32_t nz, vo
 
 int upload_tf(vr_ctx *c, const uint32_t *tf, uint32_t n)
 {
-    std::vector<float4> lut(n);
+    // texel i as {c_i, c_(i+1) - c_i} (0 for the last): tf_lookup's one-fma linear filter
+    std::vector<float4> lut(2 * (size_t)n);
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t t = tf[i];
-        lut[i] = make_float4(srgb_to_linear(t & 0xFFu), srgb_to_linear((t >> 8) & 0xFFu),
-                             srgb_to_linear((t >> 16) & 0xFFu),
-                             (float)((t >> 24) & 0xFFu) / 255.0f);
+        lut[2 * i] = make_float4(srgb_to_linear(t & 0xFFu), srgb_to_linear((t >> 8) & 0xFFu),
+                                 srgb_to_linear((t >> 16) & 0xFFu),
+                                 (float)((t >> 24) & 0xFFu) / 255.0f);
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+        const float4 a = lut[2 * i], b = i + 1 < n ? lut[2 * i + 2] : a;
+        lut[2 * i + 1] = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, b.w - a.w);
     }
     if (c->tf && c->tf_n != n) {
         hipFree(c->tf);
@@ -293,10 +298,10 @@ int upload_tf(vr_ctx *c, const uint32_t *tf, uint32_t n)
     nz[0] = 0;
     for (uint32_t i = 0; i < n; ++i) nz[i + 1] = nz[i] + ((tf[i] >> 24) != 0u ? 1u : 0u);
     if (!c->tf) {
-        HIP_TRY(c, hipMalloc(&c->tf, n * sizeof(float4)), "hipMalloc(TF)");
+        HIP_TRY(c, hipMalloc(&c->tf, 2 * (size_t)n * sizeof(float4)), "hipMalloc(TF)");
         HIP_TRY(c, hipMalloc(&c->tf_nz, (n + 1) * sizeof(uint32_t)), "hipMalloc(TF alpha prefix)");
     }
-    HIP_TRY(c, hipMemcpy(c->tf, lut.data(), n * sizeof(float4), hipMemcpyHostToDevice),
+    HIP_TRY(c, hipMemcpy(c->tf, lut.data(), lut.size() * sizeof(float4), hipMemcpyHostToDevice),
             "hipMemcpy(TF)");
     HIP_TRY(c, hipMemcpy(c->tf_nz, nz.data(), (n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice),
             "hipMemcpy(TF alpha prefix)");

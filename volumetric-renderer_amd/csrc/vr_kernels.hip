@@ -413,18 +413,23 @@ __device__ __forceinline__ float div_by_range(float x, const MarchParams &P)
     return x / P.range;
 }
 
+// 1D TF, linear filter, clamp-to-edge (offscreen_pass.cpp:1125-1150).  lut holds texel i as
+// {c_i, c_{i+1} - c_i} (difference 0 for the last texel, computed on the host with the same
+// IEEE subtraction), so lerp(c_i0, c_i1, w) = fma(w, c_i1 - c_i0, c_i0) is one fma per channel:
+// i0 = n - 1 (or u = n) reads difference 0 = the clamped c_(n-1); below the first texel
+// (u < 0) both clamped texels are c_0, so w is taken as 0.
 __device__ __forceinline__ float4 tf_lookup(const float4 *lut, int n, float nf, float t)
 {
     float u = t * nf - 0.5f;
     u = fminf(fmaxf(u, -1.0f), nf);
     const float f = floorf(u);
-    const float w = u - f;
-    int i0 = (int)f, i1 = i0 + 1;
+    float w = u - f;
+    int i0 = (int)f;
+    if (i0 < 0) w = 0.0f;
     i0 = i0 < 0 ? 0 : (i0 > n - 1 ? n - 1 : i0);
-    i1 = i1 < 0 ? 0 : (i1 > n - 1 ? n - 1 : i1);
-    const float4 a = lut[i0], b = lut[i1];
-    return make_float4(lerpf(a.x, b.x, w), lerpf(a.y, b.y, w), lerpf(a.z, b.z, w),
-                       lerpf(a.w, b.w, w));
+    const float4 a = lut[2 * i0], d = lut[2 * i0 + 1];
+    return make_float4(fmaf(w, d.x, a.x), fmaf(w, d.y, a.y), fmaf(w, d.z, a.z),
+                       fmaf(w, d.w, a.w));
 }
 
 __device__ __forceinline__ uint32_t unorm8(float x)
@@ -483,7 +488,7 @@ constexpr bool kPackedGradient = !SKIP || VR_SKIP_PACKED_GRADIENT;
 template <typename VT, bool SHADE, bool COUNT, bool SKIP, bool GF>
 __global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP, GF>)) void march_kernel(const MarchParams P)
 {
-    __shared__ float4 s_tf[kTfLds];
+    __shared__ float4 s_tf[2 * kTfLds];  // {texel, difference to the next} pairs
     const int tid = threadIdx.x;
 
     // Block -> 16x16 tile.  Workgroups b and b+8 run on the same XCD (round-robin dispatch;
@@ -513,7 +518,7 @@ __global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP, GF>)) void m
 
     const bool tf_in_lds = P.tf_n <= kTfLds;
     if (tf_in_lds)
-        for (int i = tid; i < P.tf_n; i += kThreads) s_tf[i] = P.tf[i];
+        for (int i = tid; i < 2 * P.tf_n; i += kThreads) s_tf[i] = P.tf[i];
     __syncthreads();
     const long by_stride = (long)P.nbx * kBrickElems;  // elements between brick rows/slabs
     const long bz_stride = (long)P.nbx * P.nby * kBrickElems;
