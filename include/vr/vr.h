@@ -96,7 +96,7 @@ typedef struct vr_params {
     float ambient;
     float diffuse;
     float specular;
-    int32_t spec_power; /* integer exponent, evaluated by repeated multiplication */
+    int32_t spec_power; /* integer exponent in [0, 256], binary exponentiation */
     /* Work order of the 16x16-pixel tiles over the chip (speed only, never results):
      * 0 auto, 1 raster (consecutive tiles round-robin over the 8 XCDs), 2 XCD bands (each
      * XCD a contiguous band of rows), 3 XCD-interleaved 64x64-pixel super-tiles. */

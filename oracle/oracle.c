@@ -333,10 +333,16 @@ void or_tf_sample(const uint32_t *tf, int n, float t, float out[4])
 /* The ray-march (volume.frag:21-52) + blend (offscreen_pass.cpp:715-725)                */
 /* ------------------------------------------------------------------------------------ */
 
+/* Specular power (extension): binary exponentiation, the kernel's operation sequence --
+ * square the base once per remaining exponent bit, multiply it in for each set bit. */
 static float powi(float x, int p)
 {
     float r = 1.0f;
-    for (int k = 0; k < p; ++k) r = r * x;
+    while (p) {
+        if (p & 1) r = r * x;
+        p >>= 1;
+        if (p) x = x * x;
+    }
     return r;
 }
 

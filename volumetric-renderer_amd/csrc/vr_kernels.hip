@@ -650,8 +650,13 @@ __global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP, GF>)) void m
                         const float inv = 1.0f / sqrtf(g2);
                         const float ndl = fabsf((wx * d0 + wy * d1 + wz * d2) * inv);
                         const float kdiff = P.ka + P.kd * ndl;
-                        float sp = 1.0f;
-                        for (int e = 0; e < P.spec_power; ++e) sp = sp * ndl;
+                        // ndl^p by binary exponentiation (the oracle's powi): p uniform
+                        float sp = 1.0f, b = ndl;
+                        for (int e = P.spec_power; e; ) {
+                            if (e & 1) sp = sp * b;
+                            e >>= 1;
+                            if (e) b = b * b;
+                        }
                         const float spec = P.ks * sp;
                         s.x = s.x * kdiff + spec;
                         s.y = s.y * kdiff + spec;
