@@ -324,6 +324,17 @@ int check_params(vr_ctx *c, const vr_params *p)
     return VR_OK;
 }
 
+// Pipelined march (two samples of a ray in flight, vr_kernels.hip PIPE): always for shaded
+// frames (-6% over the view sweep), and for unshaded launches of fewer than
+// kPipelineMaxWaves wavefronts -- one rank's share of a multi-GPU frame -- where per-ray
+// latency, not the chip's throughput, bounds the kernel (N = 8 rank share: 0.153 -> 0.094 ms;
+// at full-frame size it loses on the diagonal view).  VR_PIPELINE=0/1 overrides (A/B).
+bool use_pipeline(bool shading, uint32_t tiles)
+{
+    if (const char *e = std::getenv("VR_PIPELINE")) return e[0] == '1';
+    return shading || tiles * (kThreadsPerTile / 64) < kPipelineMaxWaves;
+}
+
 int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
                  int out_format, uint32_t row_block, uint32_t rank, uint32_t nranks,
                  MarchParams &P)
@@ -390,6 +401,7 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.out_format = out_format;
     P.slab_default = c->smin[0] == 0.0f && c->smin[1] == 0.0f && c->smin[2] == 0.0f &&
                      c->smax[0] == 1.0f && c->smax[1] == 1.0f && c->smax[2] == 1.0f;
+    P.pipelined = use_pipeline(p->shading != 0, P.tiles_x * P.tiles_y);
     return VR_OK;
 }
 
@@ -929,7 +941,12 @@ const char *vr_kernel_name(const vr_ctx *c, const vr_params *p)
     if (!c) return "";
     // the variant the next vr_render_device launches (after a shaded frame built the field)
     const bool gf = p && p->shading && c->storage == ST_F32 && c->grad && c->grad_valid;
-    return march_kernel_name(c->storage, p && p->shading != 0, false, p && p->skip_empty != 0, gf);
+    // the full frame (row_block 16, one rank), as vr_render launches it
+    const uint32_t tiles = ((c->width + 15) / 16) * ((c->height + 15) / 16);
+    const bool pipe = use_pipeline(p && p->shading, tiles) && !(p && p->skip_empty) &&
+                      c->tf_n <= 256;
+    return march_kernel_name(c->storage, p && p->shading != 0, false, p && p->skip_empty != 0, gf,
+                             pipe);
 }
 
 }  // extern "C"

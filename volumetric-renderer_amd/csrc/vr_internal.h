@@ -84,6 +84,7 @@ struct MarchParams {
     uint32_t wave_w_shift;  // wavefront pixel footprint: 2^shift x (64 >> shift) (8x8: 3)
     int32_t out_format;
     int32_t slab_default;   // slicing is the whole volume (0,0,0)-(1,1,1)
+    int32_t pipelined;      // two samples in flight per ray (few waves per CU: see PIPE)
     // skip_empty: per brick (index as in cell_offset) the Chebyshev distance in bricks to the
     // nearest brick that can produce a visible sample, capped at kSkipCap; 0 = not empty
     const uint8_t *skip_dist;
@@ -98,7 +99,10 @@ struct MarchParams {
 // Launchers (vr_kernels.hip).  All asynchronous on `stream`.
 hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &p,
                         hipStream_t stream);
-const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bool gf);
+const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bool gf, bool pipe);
+// Wavefront count below which a launch uses the pipelined kernel (see build_params).
+constexpr uint32_t kPipelineMaxWaves = 24576;  // between N = 2 (16 K) and N = 1 (33 K) at 1080p
+constexpr uint32_t kThreadsPerTile = 256;  // 16 x 16 pixels
 hipError_t launch_brick_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,
                                     uint32_t ny, uint32_t nz, int storage, hipStream_t stream);
 // Synthetic volume into a LINEAR buffer of the storage type (then bricked).

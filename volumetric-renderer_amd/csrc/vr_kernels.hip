@@ -474,8 +474,10 @@ __device__ __forceinline__ int wave_min_leap(int k)
 #ifndef VR_SKIP_MIN_WAVES
 #define VR_SKIP_MIN_WAVES 1
 #endif
-template <bool COUNT, bool SKIP, bool GF>
-constexpr int kMarchMinWaves = GF ? 1 : (COUNT ? 4 : (SKIP ? VR_SKIP_MIN_WAVES : VR_MARCH_MIN_WAVES));
+// (PIPE launches are small by construction: no floor.)
+template <bool COUNT, bool SKIP, bool GF, bool PIPE>
+constexpr int kMarchMinWaves =
+    (GF || PIPE) ? 1 : (COUNT ? 4 : (SKIP ? VR_SKIP_MIN_WAVES : VR_MARCH_MIN_WAVES));
 
 #ifndef VR_SKIP_PACKED_GRADIENT
 #define VR_SKIP_PACKED_GRADIENT 0
@@ -485,8 +487,49 @@ constexpr bool kPackedGradient = !SKIP || VR_SKIP_PACKED_GRADIENT;
 
 // GF: shaded f32 with the precomputed difference field (P.grad); without it the kernel forms
 // the differences from the stencil (60 vs 80 VGPRs: 8 vs 6 waves per SIMD).
-template <typename VT, bool SHADE, bool COUNT, bool SKIP, bool GF>
-__global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP, GF>)) void march_kernel(const MarchParams P)
+// Gradient Phong extension for one sample with alpha > 0 (s: TF colour in/out): gradient from
+// the difference field (GF) or the stencil, scaled to normalised coordinates, headlight
+// ndl = |n . dir|, rgb' = rgb (ka + kd ndl) + ks ndl^p.  The oracle's march_pixel, same order.
+template <typename VT, bool GF, bool PACKED>
+__device__ __forceinline__ void shade_sample(const MarchParams &P, const char *__restrict__ vol,
+                                             size_t ce, const Cell8<VT> &c, int pi, int pj,
+                                             int pk, long by_stride, long bz_stride, float ax,
+                                             float ay, float az, float d0, float d1, float d2,
+                                             float4 &s)
+{
+    float gx, gy_, gz;
+    if constexpr (GF) {  // f32: precomputed difference field
+        grad_field<PACKED>(reinterpret_cast<const char *>(P.grad), ce, ax, ay, az, gx, gy_, gz);
+    } else {
+        gradient<VT, PACKED>(vol, ce, c, pi & (kBrick - 1), pj & (kBrick - 1), pk & (kBrick - 1),
+                             by_stride, bz_stride, ax, ay, az, gx, gy_, gz);
+    }
+    const float wx = gx * P.fnx, wy = gy_ * P.fny, wz = gz * P.fnz;
+    const float g2 = wx * wx + wy * wy + wz * wz;
+    if (g2 > 0.0f) {
+        const float inv = 1.0f / sqrtf(g2);
+        const float ndl = fabsf((wx * d0 + wy * d1 + wz * d2) * inv);
+        const float kdiff = P.ka + P.kd * ndl;
+        // ndl^p by binary exponentiation (the oracle's powi): p uniform
+        float sp = 1.0f, b = ndl;
+        for (int e = P.spec_power; e;) {
+            if (e & 1) sp = sp * b;
+            e >>= 1;
+            if (e) b = b * b;
+        }
+        const float spec = P.ks * sp;
+        s.x = s.x * kdiff + spec;
+        s.y = s.y * kdiff + spec;
+        s.z = s.z * kdiff + spec;
+    }
+}
+
+// PIPE: the loads of sample k + 1 are issued before sample k is filtered, shaded and
+// composited (two samples of the ray in flight).  For launches with few waves per CU (one
+// rank's share of a multi-GPU frame), where every wave's serial chain of memory round trips,
+// not the chip's throughput, sets the time.  Reference-semantics results are identical.
+template <typename VT, bool SHADE, bool COUNT, bool SKIP, bool GF, bool PIPE>
+__global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP, GF, PIPE>)) void march_kernel(const MarchParams P)
 {
     __shared__ float4 s_tf[2 * kTfLds];  // {texel, difference to the next} pairs
     const int tid = threadIdx.x;
@@ -557,6 +600,67 @@ __global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP, GF>)) void m
             leap_margin[a] = 0.5f + (float)kMaxLeap * 1.2e-7f * fn[a];
         }
     }
+    if constexpr (PIPE) {
+        // Positions, predicates and operations exactly as the loop below.  Loads are
+        // unconditional (a cell of the first brick off-slab) and alpha is 0 off-slab, which
+        // composites +0 and leaves T: no load sits under a data-dependent branch, so the
+        // compiler waits with counted vmcnt(N) and the next sample's loads stay in flight.
+        // The TF is LDS-resident (host guarantees tf_n <= kTfLds for PIPE).
+        struct Stage {
+            Cell8<VT> c;
+            size_t ce;
+            float ax, ay, az;
+            int pi, pj, pk;
+            bool ok, slab;
+        };
+        auto prep = [&](Stage &S, int k) {
+            const bool interior = (unsigned)(k - 1) < (unsigned)kin;
+            S.ok = k < nsteps && (interior || !(p0 > 1.0f || p1 > 1.0f || p2 > 1.0f ||
+                                                p0 < 0.0f || p1 < 0.0f || p2 < 0.0f));
+            S.slab = S.ok && (interior || (p0 < P.smax[0] && p1 < P.smax[1] && p2 < P.smax[2] &&
+                                           p0 > P.smin[0] && p1 > P.smin[1] && p2 > P.smin[2]));
+            int i, j, kk;
+            texel_coord(p0, P.fnx, i, S.ax);
+            texel_coord(p1, P.fny, j, S.ay);
+            texel_coord(p2, P.fnz, kk, S.az);
+            if (!S.slab) i = j = kk = 0;
+            S.pi = i + kPad;
+            S.pj = j + kPad;
+            S.pk = kk + kPad;
+            S.ce = cell_offset(S.pi, S.pj, S.pk, P.nbx, P.nby);
+            S.c.load(vol, S.ce);
+        };
+        auto consume = [&](const Stage &S) -> bool {  // true: the ray ends (T == 0 or ERT)
+            const float d = S.c.tri(S.ax, S.ay, S.az);
+            const float tt = div_by_range(d - P.vmin, P);
+            float4 sm = tf_lookup(s_tf, P.tf_n, P.tf_nf, tt);
+            if (!S.slab) sm.w = 0.0f;
+            if (SHADE && sm.w > 0.0f)
+                shade_sample<VT, GF, true>(P, vol, S.ce, S.c, S.pi, S.pj, S.pk, by_stride,
+                                           bz_stride, S.ax, S.ay, S.az, d0, d1, d2, sm);
+            cr = cr + (sm.x * sm.w) * T;
+            cg = cg + (sm.y * sm.w) * T;
+            cb = cb + (sm.z * sm.w) * T;
+            T = T * (1.0f - sm.w);
+            return T == 0.0f || T < P.ert_eps;
+        };
+        auto advance = [&]() {
+            p0 = p0 + d0 * P.step;
+            p1 = p1 + d1 * P.step;
+            p2 = p2 + d2 * P.step;
+        };
+        Stage A, B;
+        int k = 0;
+        prep(A, k);
+        while (A.ok) {  // ping-pong: no register copies between the two stages
+            advance();
+            prep(B, ++k);
+            if (consume(A) || !B.ok) break;
+            advance();
+            prep(A, ++k);
+            if (consume(B)) break;
+        }
+    } else
     for (int it = 0; it < nsteps; ++it) {
         const bool interior = (unsigned)(it - 1) < (unsigned)kin;  // it in [1, kin]
         // volume.frag:34-37
@@ -634,34 +738,9 @@ __global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP, GF>)) void m
                                      : tf_lookup(P.tf, P.tf_n, P.tf_nf, tt);
                 if (COUNT) ++n_samples;
                 if (SHADE && s.w > 0.0f) {
-                    float gx, gy_, gz;
-                    if constexpr (GF) {  // f32: precomputed difference field
-                        grad_field<kPackedGradient<SKIP>>(reinterpret_cast<const char *>(P.grad),
-                                                          ce, ax, ay, az, gx, gy_, gz);
-                    } else {
-                        gradient<VT, kPackedGradient<SKIP>>(
-                            vol, ce, c, pi & (kBrick - 1), pj & (kBrick - 1), pk & (kBrick - 1),
-                            by_stride, bz_stride, ax, ay, az, gx, gy_, gz);
-                    }
+                    shade_sample<VT, GF, kPackedGradient<SKIP>>(P, vol, ce, c, pi, pj, pk, by_stride,
+                                                                bz_stride, ax, ay, az, d0, d1, d2, s);
                     if (COUNT) ++n_shaded;
-                    const float wx = gx * P.fnx, wy = gy_ * P.fny, wz = gz * P.fnz;
-                    const float g2 = wx * wx + wy * wy + wz * wz;
-                    if (g2 > 0.0f) {
-                        const float inv = 1.0f / sqrtf(g2);
-                        const float ndl = fabsf((wx * d0 + wy * d1 + wz * d2) * inv);
-                        const float kdiff = P.ka + P.kd * ndl;
-                        // ndl^p by binary exponentiation (the oracle's powi): p uniform
-                        float sp = 1.0f, b = ndl;
-                        for (int e = P.spec_power; e; ) {
-                            if (e & 1) sp = sp * b;
-                            e >>= 1;
-                            if (e) b = b * b;
-                        }
-                        const float spec = P.ks * sp;
-                        s.x = s.x * kdiff + spec;
-                        s.y = s.y * kdiff + spec;
-                        s.z = s.z * kdiff + spec;
-                    }
                 }
                 // volume.frag:44-45
                 cr = cr + (s.x * s.w) * T;
@@ -991,13 +1070,13 @@ __global__ __launch_bounds__(256) void assemble_kernel(const PixT *__restrict__ 
     }
 }
 
-template <typename VT, bool SHADE, bool COUNT, bool SKIP, bool GF = false>
+template <typename VT, bool SHADE, bool COUNT, bool SKIP, bool GF = false, bool PIPE = false>
 hipError_t launch_march_t(const MarchParams &p, hipStream_t stream)
 {
     const uint32_t nblocks = p.tile_order == 3 ? ((p.supers_total + 7) / 8) * 8 * 16
                                                : p.tiles_x * p.tiles_y;
     if (p.tiles_x * p.tiles_y == 0) return hipSuccess;
-    hipLaunchKernelGGL((march_kernel<VT, SHADE, COUNT, SKIP, GF>), dim3(nblocks), dim3(kThreads), 0,
+    hipLaunchKernelGGL((march_kernel<VT, SHADE, COUNT, SKIP, GF, PIPE>), dim3(nblocks), dim3(kThreads), 0,
                        stream, p);
     return hipGetLastError();
 }
@@ -1005,6 +1084,12 @@ hipError_t launch_march_t(const MarchParams &p, hipStream_t stream)
 template <typename VT>
 hipError_t launch_march_vt(bool shade, bool count, const MarchParams &p, hipStream_t s)
 {
+    if (p.pipelined && !count && !p.skip_empty && p.tf_n <= kTfLds) {
+        if (!shade) return launch_march_t<VT, false, false, false, false, true>(p, s);
+        if constexpr (kZPair<VT>)
+            if (p.grad) return launch_march_t<VT, true, false, false, true, true>(p, s);
+        return launch_march_t<VT, true, false, false, false, true>(p, s);
+    }
     if constexpr (kZPair<VT>) {
         if (shade && p.grad) {
             if (p.skip_empty)
@@ -1066,23 +1151,23 @@ hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &
     }
 }
 
-const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bool gf)
+const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bool gf, bool pipe)
 {
     // demangled names as rocprofv3 reports them (kernel-trace "Kernel_Name")
     static const std::vector<std::string> names = [] {
         const char *types[5] = {"unsigned char", "signed char", "unsigned short", "short", "float"};
         std::vector<std::string> v;
         for (int t = 0; t < 5; ++t)
-            for (int k = 0; k < 16; ++k)
-                v.push_back(std::string("void vr::(anonymous namespace)::march_kernel<") + types[t] +
-                            ((k & 8) ? ", true" : ", false") + ((k & 4) ? ", true" : ", false") +
-                            ((k & 2) ? ", true" : ", false") + ((k & 1) ? ", true" : ", false") +
-                            ">(vr::MarchParams)");
+            for (int k = 0; k < 32; ++k) {
+                std::string n = std::string("void vr::(anonymous namespace)::march_kernel<") + types[t];
+                for (int bit = 4; bit >= 0; --bit) n += (k >> bit) & 1 ? ", true" : ", false";
+                v.push_back(n + ">(vr::MarchParams)");
+            }
         return v;
     }();
     if (storage < 0 || storage > 4) return "march_kernel<?>";
-    return names[storage * 16 + (shade ? 8 : 0) + (count ? 4 : 0) + (skip ? 2 : 0) + (gf ? 1 : 0)]
-        .c_str();
+    const int k = (shade ? 16 : 0) + (count ? 8 : 0) + (skip ? 4 : 0) + (gf ? 2 : 0) + (pipe ? 1 : 0);
+    return names[storage * 32 + k].c_str();
 }
 
 hipError_t launch_brick_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,
