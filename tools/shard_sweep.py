@@ -29,9 +29,12 @@ def main():
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--wave-shape", type=int, default=0)
     ap.add_argument("--pipeline", default="", help="VR_PIPELINE override: '', 0 or 1")
+    ap.add_argument("--pair", default="", help="VR_PAIR override: '', 0 or 1")
     a = ap.parse_args()
     if a.pipeline:
         os.environ["VR_PIPELINE"] = a.pipeline
+    if a.pair:
+        os.environ["VR_PAIR"] = a.pair
     W, H = 1920, 1080
     rp = vr_amd.OffscreenPass(W, H)
     rp.generate_volume((512, 512, 512), np.float32, seed=2024)

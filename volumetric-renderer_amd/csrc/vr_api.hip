@@ -335,6 +335,19 @@ bool use_pipeline(bool shading, uint32_t tiles)
     return shading || tiles * (kThreadsPerTile / 64) < kPipelineMaxWaves;
 }
 
+// Lane-pair march (two lanes per ray, each lane pipelined) for SHADED launches of fewer than
+// kPairMaxWaves single-lane wavefronts -- a rank's share of a multi-GPU frame, small frames:
+// twice the wavefronts, half of each ray's serial chain per lane.  Measured on the C3 rank
+// share: N = 8 0.190 -> 0.153 ms, N = 4 0.270 -> 0.227 ms; the full frame and unshaded shares
+// stay faster single-lane (tools/shard_sweep.py, profiles/r01/multi_gpu/).  Not for
+// skip-empty frames or TFs beyond the LDS copy.  VR_PAIR=0/1 overrides (A/B).
+bool use_pair(const MarchParams &P, const vr_params *p)
+{
+    if (p->skip_empty || P.tf_n > 256) return false;
+    if (const char *e = std::getenv("VR_PAIR")) return e[0] == '1';
+    return p->shading && P.tiles_x * P.tiles_y * (kThreadsPerTile / 64) < kPairMaxWaves;
+}
+
 int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
                  int out_format, uint32_t row_block, uint32_t rank, uint32_t nranks,
                  MarchParams &P)
@@ -814,6 +827,11 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
         if (rc) return rc;
     }
     if (p->shading) ensure_grad(c, P, s);
+    if (use_pair(P, p)) {  // two lanes per ray on 16x8 tiles (vr_kernels.hip march_pair_kernel)
+        P.pair = 1;
+        P.tiles_y = (P.local_rows + 7) / 8;
+        P.supers_total = P.supers_x * ((P.tiles_y + 3) / 4);
+    }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing) {
         e0 = pooled_event(c);

@@ -85,6 +85,7 @@ struct MarchParams {
     int32_t out_format;
     int32_t slab_default;   // slicing is the whole volume (0,0,0)-(1,1,1)
     int32_t pipelined;      // two samples in flight per ray (few waves per CU: see PIPE)
+    int32_t pair;           // lane-pair march (march_pair_kernel), 16x8-pixel tiles
     // skip_empty: per brick (index as in cell_offset) the Chebyshev distance in bricks to the
     // nearest brick that can produce a visible sample, capped at kSkipCap; 0 = not empty
     const uint8_t *skip_dist;
@@ -103,6 +104,8 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
 // Wavefront count below which a launch uses the pipelined kernel (see build_params).
 constexpr uint32_t kPipelineMaxWaves = 24576;  // between N = 2 (16 K) and N = 1 (33 K) at 1080p
 constexpr uint32_t kThreadsPerTile = 256;  // 16 x 16 pixels
+// Wavefront count (single-lane tiling) below which a launch uses the lane-pair kernel.
+constexpr uint32_t kPairMaxWaves = 24576;
 hipError_t launch_brick_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,
                                     uint32_t ny, uint32_t nz, int storage, hipStream_t stream);
 // Synthetic volume into a LINEAR buffer of the storage type (then bricked).

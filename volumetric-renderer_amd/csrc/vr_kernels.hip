@@ -487,6 +487,34 @@ constexpr bool kPackedGradient = !SKIP || VR_SKIP_PACKED_GRADIENT;
 
 // GF: shaded f32 with the precomputed difference field (P.grad); without it the kernel forms
 // the differences from the stencil (60 vs 80 VGPRs: 8 vs 6 waves per SIMD).
+// Block -> tile.  Workgroups b and b+8 run on the same XCD (round-robin dispatch; speed
+// only, never correctness).  Orders: 1 raster; 2 each XCD a contiguous band of tiles
+// (bijective remap); 3 each XCD every 8th 4x4-tile super-tile in raster order, its tiles
+// consecutive on that XCD: L2 locality inside a super-tile, every XCD sampling the whole
+// frame (load balance when the volume covers part of it).  false: no tile (grid padding).
+__device__ __forceinline__ bool block_tile(const MarchParams &P, uint32_t &tile_x,
+                                           uint32_t &tile_y)
+{
+    const uint32_t nwg = gridDim.x, b = blockIdx.x;
+    if (P.tile_order == 3) {
+        const uint32_t k = b >> 3, w = k & 15;
+        const uint32_t s = (b & 7u) + 8u * (k >> 4);
+        tile_x = (s % P.supers_x) * 4 + (w & 3);
+        tile_y = (s / P.supers_x) * 4 + (w >> 2);
+        return s < P.supers_total && tile_x < P.tiles_x && tile_y < P.tiles_y;
+    }
+    if (P.tile_order == 2) {
+        const uint32_t xcd = b & 7u, q = nwg >> 3, r = nwg & 7u;
+        const uint32_t t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+        tile_x = t % P.tiles_x;
+        tile_y = t / P.tiles_x;
+        return true;
+    }
+    tile_x = b % P.tiles_x;
+    tile_y = b / P.tiles_x;
+    return true;
+}
+
 // Gradient Phong extension for one sample with alpha > 0 (s: TF colour in/out): gradient from
 // the difference field (GF) or the stencil, scaled to normalised coordinates, headlight
 // ndl = |n . dir|, rgb' = rgb (ka + kd ndl) + ks ndl^p.  The oracle's march_pixel, same order.
@@ -534,30 +562,8 @@ __global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP, GF, PIPE>)) 
     __shared__ float4 s_tf[2 * kTfLds];  // {texel, difference to the next} pairs
     const int tid = threadIdx.x;
 
-    // Block -> 16x16 tile.  Workgroups b and b+8 run on the same XCD (round-robin dispatch;
-    // speed only, never correctness).  Orders: 1 raster; 2 each XCD a contiguous band of
-    // tiles (bijective remap); 3 each XCD every 8th 4x4-tile super-tile (64x64 px) in raster
-    // order, its tiles consecutive on that XCD: L2 locality inside a super-tile, every XCD
-    // sampling the whole frame (load balance when the volume covers part of it).
     uint32_t tile_x, tile_y;
-    {
-        const uint32_t nwg = gridDim.x, b = blockIdx.x;
-        if (P.tile_order == 3) {
-            const uint32_t k = b >> 3, w = k & 15;
-            const uint32_t s = (b & 7u) + 8u * (k >> 4);
-            tile_x = (s % P.supers_x) * 4 + (w & 3);
-            tile_y = (s / P.supers_x) * 4 + (w >> 2);
-            if (s >= P.supers_total || tile_x >= P.tiles_x || tile_y >= P.tiles_y) return;
-        } else if (P.tile_order == 2) {
-            const uint32_t xcd = b & 7u, q = nwg >> 3, r = nwg & 7u;
-            const uint32_t t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-            tile_x = t % P.tiles_x;
-            tile_y = t / P.tiles_x;
-        } else {
-            tile_x = b % P.tiles_x;
-            tile_y = b / P.tiles_x;
-        }
-    }
+    if (!block_tile(P, tile_x, tile_y)) return;
 
     const bool tf_in_lds = P.tf_n <= kTfLds;
     if (tf_in_lds)
@@ -775,6 +781,134 @@ __global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP, GF, PIPE>)) 
 
     // volume.frag:50 + blend (offscreen_pass.cpp:715-725); uncovered: T = 1, C = 0 -> clear
     const float A = 1.0f - T;
+    const float omA = 1.0f - A;
+    const float o0 = cr * A + P.clear[0] * omA;
+    const float o1 = cg * A + P.clear[1] * omA;
+    const float o2 = cb * A + P.clear[2] * omA;
+    const float o3 = A * A + P.clear[3] * omA;
+    const size_t idx = (size_t)ly * P.W + px;
+    if (P.out_format == 0) {
+        static_cast<uint32_t *>(P.out)[idx] =
+            unorm8(o0) | (unorm8(o1) << 8) | (unorm8(o2) << 16) | (unorm8(o3) << 24);
+    } else {
+        static_cast<float4 *>(P.out)[idx] = make_float4(o0, o1, o2, o3);
+    }
+}
+
+// ---- lane-pair march (small launches) ----------------------------------------------------------
+// Two lanes per ray: lane 0 of the pair fetches, filters and shades the even samples, lane 1 the
+// odd ones; both keep the ray position with the same float additions (p_(k+1) = p_k + d step,
+// every step), exchange their sample through a lane shuffle, and composite the pair in sample
+// order with identical operations, so C and T are the single-lane march's bit for bit (an
+// off-slab sample composites alpha 0: +0, T unchanged).  Halves each ray's serial chain and
+// doubles the wavefronts of a launch: for a rank's share of a multi-GPU frame.  A workgroup is
+// a 16x8-pixel tile (wavefront: 16x2 pixels); the TF is LDS-resident (host: tf_n <= kTfLds).
+template <typename VT, bool SHADE, bool GF>
+__global__ __launch_bounds__(kThreads) void march_pair_kernel(const MarchParams P)
+{
+    __shared__ float4 s_tf[2 * kTfLds];
+    const int tid = threadIdx.x;
+    uint32_t tile_x, tile_y;
+    if (!block_tile(P, tile_x, tile_y)) return;
+    for (int i = tid; i < 2 * P.tf_n; i += kThreads) s_tf[i] = P.tf[i];
+    __syncthreads();
+    const long by_stride = (long)P.nbx * kBrickElems;
+    const long bz_stride = (long)P.nbx * P.nby * kBrickElems;
+
+    const uint32_t wave = tid >> 6, lane = tid & 63, q = lane >> 1, half = lane & 1;
+    const uint32_t px = tile_x * kTile + (q & 15);
+    const uint32_t ly = tile_y * (kTile / 2) + wave * 2 + (q >> 4);
+    bool active = px < P.W && ly < P.local_rows;
+    const uint32_t blk = ly / P.row_block;
+    const uint32_t gy = (blk * P.nranks + P.rank) * P.row_block + (ly - blk * P.row_block);
+    active = active && gy < P.H;
+
+    float tex[3] = {0.f, 0.f, 0.f}, dir[3] = {0.f, 0.f, 0.f};
+    const bool covered = active && pixel_ray(P, px, gy, tex, dir);
+    const char *__restrict__ vol = static_cast<const char *>(P.vol);
+    const int nsteps = covered ? P.nsteps : 0;
+    float p0 = tex[0], p1 = tex[1], p2 = tex[2];
+    const float d0 = dir[0], d1 = dir[1], d2 = dir[2];
+    const int kin = (covered && P.slab_default) ? interior_steps(tex, dir, P.step, nsteps) : 0;
+    auto advance = [&]() {
+        p0 = p0 + d0 * P.step;
+        p1 = p1 + d1 * P.step;
+        p2 = p2 + d2 * P.step;
+    };
+    float T = 1.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f;
+    // Each lane also runs its own samples software-pipelined (its next sample's loads in
+    // flight while the current one is filtered): unconditional loads (a first-brick cell
+    // off-slab, alpha 0 there), ping-pong stages, as march_kernel's PIPE path.
+    struct Stage {
+        Cell8<VT> c;
+        size_t ce;
+        float ax, ay, az;
+        int pi, pj, pk;
+        bool ok, slab;
+    };
+    auto prep = [&](Stage &S, int k) {
+        const bool interior = (unsigned)(k - 1) < (unsigned)kin;
+        S.ok = k < nsteps && (interior || !(p0 > 1.0f || p1 > 1.0f || p2 > 1.0f || p0 < 0.0f ||
+                                            p1 < 0.0f || p2 < 0.0f));
+        S.slab = S.ok && (interior || (p0 < P.smax[0] && p1 < P.smax[1] && p2 < P.smax[2] &&
+                                       p0 > P.smin[0] && p1 > P.smin[1] && p2 > P.smin[2]));
+        int i, j, kk;
+        texel_coord(p0, P.fnx, i, S.ax);
+        texel_coord(p1, P.fny, j, S.ay);
+        texel_coord(p2, P.fnz, kk, S.az);
+        if (!S.slab) i = j = kk = 0;
+        S.pi = i + kPad;
+        S.pj = j + kPad;
+        S.pk = kk + kPad;
+        S.ce = cell_offset(S.pi, S.pj, S.pk, P.nbx, P.nby);
+        S.c.load(vol, S.ce);
+    };
+    // this lane's sample -> exchange -> the pair's two samples composited in order; true: the
+    // ray ends (bounds, nsteps, T == 0 or ERT), identically in both lanes
+    auto consume = [&](const Stage &S) -> bool {
+        float4 sm = tf_lookup(s_tf, P.tf_n, P.tf_nf,
+                              div_by_range(S.c.tri(S.ax, S.ay, S.az) - P.vmin, P));
+        if (!S.slab) sm.w = 0.0f;
+        if (SHADE && sm.w > 0.0f)
+            shade_sample<VT, GF, true>(P, vol, S.ce, S.c, S.pi, S.pj, S.pk, by_stride, bz_stride,
+                                       S.ax, S.ay, S.az, d0, d1, d2, sm);
+        // the pair's two samples, in order: A = even (lane 0), B = odd (lane 1)
+        const float ox = __shfl_xor(sm.x, 1, 64), oy = __shfl_xor(sm.y, 1, 64);
+        const float oz = __shfl_xor(sm.z, 1, 64), ow = __shfl_xor(sm.w, 1, 64);
+        const int ook = __shfl_xor((int)S.ok, 1, 64);
+        const float4 sa = half ? make_float4(ox, oy, oz, ow) : sm;
+        const float4 sb = half ? sm : make_float4(ox, oy, oz, ow);
+        const bool oka = half ? (ook != 0) : S.ok, okb = half ? S.ok : (ook != 0);
+        if (!oka) return true;
+        cr = cr + (sa.x * sa.w) * T;  // volume.frag:44-45
+        cg = cg + (sa.y * sa.w) * T;
+        cb = cb + (sa.z * sa.w) * T;
+        T = T * (1.0f - sa.w);
+        if (T == 0.0f || T < P.ert_eps || !okb) return true;
+        cr = cr + (sb.x * sb.w) * T;
+        cg = cg + (sb.y * sb.w) * T;
+        cb = cb + (sb.z * sb.w) * T;
+        T = T * (1.0f - sb.w);
+        return T == 0.0f || T < P.ert_eps;
+    };
+    if (half) advance();  // lane 1 starts at sample 1
+    Stage S0, S1;
+    int k = (int)half;
+    prep(S0, k);
+    for (;;) {  // both lanes of a pair leave together (same ok flags and T)
+        advance();
+        advance();
+        k += 2;
+        prep(S1, k);
+        if (consume(S0)) break;
+        advance();
+        advance();
+        k += 2;
+        prep(S0, k);
+        if (consume(S1)) break;
+    }
+    if (!active || half) return;
+    const float A = 1.0f - T;  // volume.frag:50 + blend (offscreen_pass.cpp:715-725)
     const float omA = 1.0f - A;
     const float o0 = cr * A + P.clear[0] * omA;
     const float o1 = cg * A + P.clear[1] * omA;
@@ -1081,9 +1215,26 @@ hipError_t launch_march_t(const MarchParams &p, hipStream_t stream)
     return hipGetLastError();
 }
 
+template <typename VT, bool SHADE, bool GF>
+hipError_t launch_pair_t(const MarchParams &p, hipStream_t stream)
+{
+    const uint32_t nblocks = p.tile_order == 3 ? ((p.supers_total + 7) / 8) * 8 * 16
+                                               : p.tiles_x * p.tiles_y;
+    if (p.tiles_x * p.tiles_y == 0) return hipSuccess;
+    hipLaunchKernelGGL((march_pair_kernel<VT, SHADE, GF>), dim3(nblocks), dim3(kThreads), 0,
+                       stream, p);
+    return hipGetLastError();
+}
+
 template <typename VT>
 hipError_t launch_march_vt(bool shade, bool count, const MarchParams &p, hipStream_t s)
 {
+    if (p.pair) {  // host: not counting, no skip-empty, tf_n <= kTfLds, 16x8 tiles
+        if (!shade) return launch_pair_t<VT, false, false>(p, s);
+        if constexpr (kZPair<VT>)
+            if (p.grad) return launch_pair_t<VT, true, true>(p, s);
+        return launch_pair_t<VT, true, false>(p, s);
+    }
     if (p.pipelined && !count && !p.skip_empty && p.tf_n <= kTfLds) {
         if (!shade) return launch_march_t<VT, false, false, false, false, true>(p, s);
         if constexpr (kZPair<VT>)
