@@ -827,9 +827,12 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
         if (rc) return rc;
     }
     if (p->shading) ensure_grad(c, P, s);
-    if (use_pair(P, p)) {  // two lanes per ray on 16x8 tiles (vr_kernels.hip march_pair_kernel)
-        P.pair = 1;
-        P.tiles_y = (P.local_rows + 7) / 8;
+    if (use_pair(P, p)) {  // L lanes per ray on 16 x (16 / L) tiles (march_pair_kernel)
+        // 4 lanes below kPairQuadMaxWaves (N = 8 C3 share: 0.151 -> 0.144 ms), else 2
+        P.pair = P.tiles_x * P.tiles_y * (kThreadsPerTile / 64) < kPairQuadMaxWaves ? 4 : 2;
+        if (const char *e = std::getenv("VR_PAIR_LANES")) P.pair = e[0] == '4' ? 4 : 2;
+        const uint32_t th = 16 / P.pair;
+        P.tiles_y = (P.local_rows + th - 1) / th;
         P.supers_total = P.supers_x * ((P.tiles_y + 3) / 4);
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;

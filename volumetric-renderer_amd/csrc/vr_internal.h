@@ -106,6 +106,7 @@ constexpr uint32_t kPipelineMaxWaves = 24576;  // between N = 2 (16 K) and N = 1
 constexpr uint32_t kThreadsPerTile = 256;  // 16 x 16 pixels
 // Wavefront count (single-lane tiling) below which a launch uses the lane-pair kernel.
 constexpr uint32_t kPairMaxWaves = 24576;
+constexpr uint32_t kPairQuadMaxWaves = 6144;  // below: 4 lanes per ray
 hipError_t launch_brick_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,
                                     uint32_t ny, uint32_t nz, int storage, hipStream_t stream);
 // Synthetic volume into a LINEAR buffer of the storage type (then bricked).

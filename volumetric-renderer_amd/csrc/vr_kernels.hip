@@ -803,7 +803,7 @@ __global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP, GF, PIPE>)) 
 // off-slab sample composites alpha 0: +0, T unchanged).  Halves each ray's serial chain and
 // doubles the wavefronts of a launch: for a rank's share of a multi-GPU frame.  A workgroup is
 // a 16x8-pixel tile (wavefront: 16x2 pixels); the TF is LDS-resident (host: tf_n <= kTfLds).
-template <typename VT, bool SHADE, bool GF>
+template <typename VT, bool SHADE, bool GF, int L>
 __global__ __launch_bounds__(kThreads) void march_pair_kernel(const MarchParams P)
 {
     __shared__ float4 s_tf[2 * kTfLds];
@@ -815,9 +815,10 @@ __global__ __launch_bounds__(kThreads) void march_pair_kernel(const MarchParams 
     const long by_stride = (long)P.nbx * kBrickElems;
     const long bz_stride = (long)P.nbx * P.nby * kBrickElems;
 
-    const uint32_t wave = tid >> 6, lane = tid & 63, q = lane >> 1, half = lane & 1;
+    // L lanes per ray; wavefront = 16 x (4 / L) pixels; workgroup tile 16 x (16 / L)
+    const uint32_t wave = tid >> 6, lane = tid & 63, q = lane / L, half = lane % L;
     const uint32_t px = tile_x * kTile + (q & 15);
-    const uint32_t ly = tile_y * (kTile / 2) + wave * 2 + (q >> 4);
+    const uint32_t ly = tile_y * (kTile / L) + wave * (4 / L) + (q >> 4);
     bool active = px < P.W && ly < P.local_rows;
     const uint32_t blk = ly / P.row_block;
     const uint32_t gy = (blk * P.nranks + P.rank) * P.row_block + (ly - blk * P.row_block);
@@ -872,38 +873,35 @@ __global__ __launch_bounds__(kThreads) void march_pair_kernel(const MarchParams 
         if (SHADE && sm.w > 0.0f)
             shade_sample<VT, GF, true>(P, vol, S.ce, S.c, S.pi, S.pj, S.pk, by_stride, bz_stride,
                                        S.ax, S.ay, S.az, d0, d1, d2, sm);
-        // the pair's two samples, in order: A = even (lane 0), B = odd (lane 1)
-        const float ox = __shfl_xor(sm.x, 1, 64), oy = __shfl_xor(sm.y, 1, 64);
-        const float oz = __shfl_xor(sm.z, 1, 64), ow = __shfl_xor(sm.w, 1, 64);
-        const int ook = __shfl_xor((int)S.ok, 1, 64);
-        const float4 sa = half ? make_float4(ox, oy, oz, ow) : sm;
-        const float4 sb = half ? sm : make_float4(ox, oy, oz, ow);
-        const bool oka = half ? (ook != 0) : S.ok, okb = half ? S.ok : (ook != 0);
-        if (!oka) return true;
-        cr = cr + (sa.x * sa.w) * T;  // volume.frag:44-45
-        cg = cg + (sa.y * sa.w) * T;
-        cb = cb + (sa.z * sa.w) * T;
-        T = T * (1.0f - sa.w);
-        if (T == 0.0f || T < P.ert_eps || !okb) return true;
-        cr = cr + (sb.x * sb.w) * T;
-        cg = cg + (sb.y * sb.w) * T;
-        cb = cb + (sb.z * sb.w) * T;
-        T = T * (1.0f - sb.w);
-        return T == 0.0f || T < P.ert_eps;
+        // the group's L samples, in sample order (lane j of the group holds sample k0 + j)
+        const int base = (int)(lane - half);
+#pragma unroll
+        for (int j = 0; j < L; ++j) {
+            const float sx = __shfl(sm.x, base + j, 64), sy = __shfl(sm.y, base + j, 64);
+            const float sz = __shfl(sm.z, base + j, 64), sw = __shfl(sm.w, base + j, 64);
+            const int sok = __shfl((int)S.ok, base + j, 64);
+            if (!sok) return true;
+            cr = cr + (sx * sw) * T;  // volume.frag:44-45
+            cg = cg + (sy * sw) * T;
+            cb = cb + (sz * sw) * T;
+            T = T * (1.0f - sw);
+            if (T == 0.0f || T < P.ert_eps) return true;
+        }
+        return false;
     };
-    if (half) advance();  // lane 1 starts at sample 1
+    for (uint32_t j = 0; j < half; ++j) advance();  // lane j of the group starts at sample j
     Stage S0, S1;
     int k = (int)half;
     prep(S0, k);
-    for (;;) {  // both lanes of a pair leave together (same ok flags and T)
-        advance();
-        advance();
-        k += 2;
+    for (;;) {  // the lanes of a group leave together (same ok flags and T)
+#pragma unroll
+        for (int j = 0; j < L; ++j) advance();
+        k += L;
         prep(S1, k);
         if (consume(S0)) break;
-        advance();
-        advance();
-        k += 2;
+#pragma unroll
+        for (int j = 0; j < L; ++j) advance();
+        k += L;
         prep(S0, k);
         if (consume(S1)) break;
     }
@@ -1221,8 +1219,12 @@ hipError_t launch_pair_t(const MarchParams &p, hipStream_t stream)
     const uint32_t nblocks = p.tile_order == 3 ? ((p.supers_total + 7) / 8) * 8 * 16
                                                : p.tiles_x * p.tiles_y;
     if (p.tiles_x * p.tiles_y == 0) return hipSuccess;
-    hipLaunchKernelGGL((march_pair_kernel<VT, SHADE, GF>), dim3(nblocks), dim3(kThreads), 0,
-                       stream, p);
+    if (p.pair == 4)
+        hipLaunchKernelGGL((march_pair_kernel<VT, SHADE, GF, 4>), dim3(nblocks), dim3(kThreads),
+                           0, stream, p);
+    else
+        hipLaunchKernelGGL((march_pair_kernel<VT, SHADE, GF, 2>), dim3(nblocks), dim3(kThreads),
+                           0, stream, p);
     return hipGetLastError();
 }
 
