@@ -288,7 +288,9 @@ def main():
                 "camera": synth.CAMERAS[cfg["cam"]],
                 "tf": cfg["tf"], "shading": cfg["shading"], "ert_eps": cfg["ert"],
                 "parallelism": f"image 8-row blocks cyclic x{world}" + (
-                    (" + RCCL gather (overlapped with next frame)" if overlap else " + RCCL gather (serial)")
+                    (" + gloo host-staged gather (rehearsal, ranks share devices)" if BACKEND != "nccl"
+                     else " + RCCL gather (overlapped with next frame)" if overlap
+                     else " + RCCL gather (serial)")
                     if world > 1 else ""),
                 "samples_per_frame": fstats["samples"],
                 "shaded_samples_per_frame": fstats["shaded_samples"],
