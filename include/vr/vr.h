@@ -98,8 +98,10 @@ typedef struct vr_params {
     float specular;
     int32_t spec_power; /* integer exponent in [0, 256], binary exponentiation */
     /* Work order of the 16x16-pixel tiles over the chip (speed only, never results):
-     * 0 auto, 1 raster (consecutive tiles round-robin over the 8 XCDs), 2 XCD bands (each
-     * XCD a contiguous band of rows), 3 XCD-interleaved 64x64-pixel super-tiles. */
+     * 0 auto (= 4), 1 raster (consecutive tiles round-robin over the 8 XCDs), 2 XCD bands
+     * (each XCD a contiguous band of rows), 3 XCD-interleaved 64x64-pixel super-tiles,
+     * 4 adaptive: as 3, each XCD's tiles dispatched longest first by the durations the
+     * previous launch of the same tile geometry recorded (the first launch runs as 3). */
     int32_t tile_order;
     /* 1: skip the trilinear fetch of samples proven fully transparent: the sample's cell lies
      * in an 8^3 brick whose stored value range (widened by a rounding margin) maps only to TF

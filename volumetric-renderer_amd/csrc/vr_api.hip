@@ -9,6 +9,7 @@
 #include "../../include/vr/vr.h"
 #include "vr_internal.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -47,6 +48,16 @@ struct vr_ctx {
     float *grad = nullptr;
     size_t grad_bytes = 0;
     bool grad_valid = false;
+    // adaptive tile order (tile_order 4): per launch geometry, the last launch's per-tile
+    // durations and the workgroup -> tile permutation built from them
+    struct TileSched {
+        uint32_t tiles_x = 0, tiles_y = 0, supers_x = 0, per_xcd = 0;
+        int pair = 0;
+        uint32_t *cost = nullptr, *perm = nullptr, *lists = nullptr;
+        bool have_perm = false;
+        uint32_t launches = 0;
+    };
+    std::vector<TileSched> sched;
     // scratch
     unsigned long long *counters = nullptr;
     void *frame_dev = nullptr;
@@ -405,7 +416,7 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.local_rows = vr_shard_rows(c->height, row_block, nranks);
     P.tiles_x = (c->width + 15) / 16;
     P.tiles_y = (P.local_rows + 15) / 16;
-    P.tile_order = p->tile_order >= 1 && p->tile_order <= 3 ? (uint32_t)p->tile_order : 3u;
+    P.tile_order = p->tile_order >= 1 && p->tile_order <= 4 ? (uint32_t)p->tile_order : 4u;
     // wavefront footprint: 1 8x8, 2 16x4, 3 4x16; auto = 16x4 (x-contiguous brick rows:
     // fewer cache lines per wave-level load; measured -11% on the r=3 view, even on others)
     P.wave_w_shift = p->wave_shape == 1 ? 3u : (p->wave_shape == 3 ? 2u : 4u);
@@ -483,6 +494,57 @@ void ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s)
         c->grad_valid = true;
     }
     P.grad = c->grad;
+}
+
+// Adaptive tile order (tile_order 4): the schedule entry of this launch geometry (created on
+// first use, at most 8 kept); sets P.tile_cost, and P.tile_perm once a permutation exists.
+vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P)
+{
+    if (P.tile_order != 4) return nullptr;
+    for (auto &t : c->sched)
+        if (t.tiles_x == P.tiles_x && t.tiles_y == P.tiles_y && t.pair == P.pair) {
+            P.tile_cost = t.cost;
+            if (t.have_perm) {
+                P.tile_perm = t.perm;
+                P.nperm = 8 * t.per_xcd;
+            }
+            return &t;
+        }
+    if (c->sched.size() >= 8) {
+        hipFree(c->sched.front().cost);
+        hipFree(c->sched.front().perm);
+        hipFree(c->sched.front().lists);
+        c->sched.erase(c->sched.begin());
+    }
+    vr_ctx::TileSched t;
+    t.tiles_x = P.tiles_x;
+    t.tiles_y = P.tiles_y;
+    t.supers_x = P.supers_x;
+    t.pair = P.pair;
+    // per-XCD tile lists (tile_order 3's super-tile assignment), padded with ~0
+    std::vector<std::vector<uint32_t>> xl(8);
+    for (uint32_t ty = 0; ty < P.tiles_y; ++ty)
+        for (uint32_t tx = 0; tx < P.tiles_x; ++tx)
+            xl[((ty >> 2) * P.supers_x + (tx >> 2)) & 7u].push_back(ty * P.tiles_x + tx);
+    for (int x = 0; x < 8; ++x) t.per_xcd = xl[x].size() > t.per_xcd ? (uint32_t)xl[x].size() : t.per_xcd;
+    std::vector<uint32_t> lists(8 * (size_t)t.per_xcd, 0xFFFFFFFFu);
+    for (int x = 0; x < 8; ++x)
+        std::copy(xl[x].begin(), xl[x].end(), lists.begin() + (size_t)x * t.per_xcd);
+    const size_t nt = (size_t)P.tiles_x * P.tiles_y;
+    if (hipMalloc(&t.cost, nt * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&t.perm, lists.size() * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&t.lists, lists.size() * sizeof(uint32_t)) != hipSuccess ||
+        hipMemcpy(t.lists, lists.data(), lists.size() * sizeof(uint32_t), hipMemcpyHostToDevice) !=
+            hipSuccess) {
+        (void)hipGetLastError();
+        hipFree(t.cost);
+        hipFree(t.perm);
+        hipFree(t.lists);
+        return nullptr;  // no adaptive order (tile_order 3 mapping)
+    }
+    c->sched.push_back(t);
+    P.tile_cost = c->sched.back().cost;
+    return &c->sched.back();
 }
 
 hipEvent_t pooled_event(vr_ctx *c)
@@ -583,6 +645,11 @@ void vr_destroy(vr_ctx *c)
     if (c->brick_range) hipFree(c->brick_range);
     if (c->skip_dist) hipFree(c->skip_dist);
     if (c->grad) hipFree(c->grad);
+    for (auto &t : c->sched) {
+        hipFree(t.cost);
+        hipFree(t.perm);
+        hipFree(t.lists);
+    }
     if (c->counters) hipFree(c->counters);
     if (c->frame_dev) hipFree(c->frame_dev);
     delete c;
@@ -835,6 +902,7 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
         P.tiles_y = (P.local_rows + th - 1) / th;
         P.supers_total = P.supers_x * ((P.tiles_y + 3) / 4);
     }
+    vr_ctx::TileSched *ts = tile_sched(c, P);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing) {
         e0 = pooled_event(c);
@@ -846,6 +914,13 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
     if (c->timing) {
         HIP_TRY(c, hipEventRecord(e1, s), "hipEventRecord");
         c->ev_pending.emplace_back(e0, e1);
+    }
+    // next launches of this geometry: longest tiles first, re-ordered every kReorderEvery
+    // launches (the order kernel runs after the timed march kernel, inside the frame)
+    if (ts && ts->launches++ % kReorderEvery == 0) {
+        HIP_TRY(c, launch_order_tiles(ts->cost, ts->lists, ts->perm, ts->per_xcd, s),
+                "tile order kernel");
+        ts->have_perm = true;
     }
     return VR_OK;
 }
@@ -969,5 +1044,15 @@ const char *vr_kernel_name(const vr_ctx *c, const vr_params *p)
     return march_kernel_name(c->storage, p && p->shading != 0, false, p && p->skip_empty != 0, gf,
                              pipe);
 }
+
+#ifdef VR_WG_TIMES
+// Experiment builds only: per-workgroup (start, end) wall-clock pairs of the march launches
+// since the last reset (tools/wg_timeline.py).
+int vr_debug_wg_times(unsigned long long *out, unsigned int max, unsigned int *count, int reset)
+{
+    if (reset) return debug_wg_times_reset() == hipSuccess ? VR_OK : VR_EIO;
+    return debug_wg_times_read(out, max, count) == hipSuccess ? VR_OK : VR_EIO;
+}
+#endif
 
 }  // extern "C"

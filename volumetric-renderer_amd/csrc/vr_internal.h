@@ -86,6 +86,12 @@ struct MarchParams {
     int32_t slab_default;   // slicing is the whole volume (0,0,0)-(1,1,1)
     int32_t pipelined;      // two samples in flight per ray (few waves per CU: see PIPE)
     int32_t pair;           // lane-pair march (march_pair_kernel), 16x8-pixel tiles
+    // adaptive tile order (tile_order 4): workgroup b renders tile tile_perm[b] (tile id =
+    // ty * tiles_x + tx, ~0 = none; nperm workgroups) and records its duration in
+    // tile_cost[tile id]; null: order by tile_order
+    const uint32_t *tile_perm;
+    uint32_t *tile_cost;
+    uint32_t nperm;
     // skip_empty: per brick (index as in cell_offset) the Chebyshev distance in bricks to the
     // nearest brick that can produce a visible sample, capped at kSkipCap; 0 = not empty
     const uint8_t *skip_dist;
@@ -104,6 +110,16 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
 // Wavefront count below which a launch uses the pipelined kernel (see build_params).
 constexpr uint32_t kPipelineMaxWaves = 24576;  // between N = 2 (16 K) and N = 1 (33 K) at 1080p
 constexpr uint32_t kThreadsPerTile = 256;  // 16 x 16 pixels
+// Adaptive tile order: from the per-tile durations of the last launch with the same tile
+// geometry, the next launch's workgroup -> tile permutation, longest first within each XCD's
+// super-tiles (as tile_order 3 assigns them).
+hipError_t launch_order_tiles(const uint32_t *cost, const uint32_t *lists, uint32_t *perm,
+                              uint32_t per_xcd, hipStream_t stream);
+// launches of one geometry per re-ordering (the order kernel runs on every 4th)
+#ifndef VR_REORDER_EVERY
+#define VR_REORDER_EVERY 4
+#endif
+constexpr uint32_t kReorderEvery = VR_REORDER_EVERY;
 // Wavefront count (single-lane tiling) below which a launch uses the lane-pair kernel.
 constexpr uint32_t kPairMaxWaves = 24576;
 constexpr uint32_t kPairQuadMaxWaves = 6144;  // below: 4 lanes per ray
@@ -133,5 +149,10 @@ hipError_t launch_brick_range(int storage, const void *bricks, uint32_t nbricks,
 hipError_t launch_skip_dist(const float2 *range_dev, uint32_t nbx, uint32_t nby, uint32_t nbz,
                             const uint32_t *tf_nz_dev, int tf_n, float vmin, float vrange,
                             uint8_t *dist_dev, uint8_t *scratch_dev, hipStream_t stream);
+
+#ifdef VR_WG_TIMES
+hipError_t debug_wg_times_reset();
+hipError_t debug_wg_times_read(unsigned long long *out, unsigned int max, unsigned int *count);
+#endif
 
 }  // namespace vr

@@ -463,6 +463,14 @@ __device__ __forceinline__ int wave_min_leap(int k)
     return lo;
 }
 
+#ifdef VR_WG_TIMES
+// Experiment builds: per-workgroup start/end wall clock (100 MHz) of the last march launch,
+// read by vr_debug_wg_times (tools/wg_timeline.py).
+constexpr uint32_t kWgTimesMax = 1u << 17;
+__device__ unsigned long long g_wg_times[2 * kWgTimesMax];
+__device__ unsigned int g_wg_count;
+#endif
+
 // Occupancy floor (waves per SIMD): the shaded f32 kernel holds 2 x 16-B centre loads plus
 // 10 gradient loads in flight and would take 102 VGPRs (4 waves) unconstrained; 6 waves
 // measured best (A/B: 0.79 vs 0.91 ms for C3).  The skip-empty kernel (scalar gradient) is
@@ -496,7 +504,13 @@ __device__ __forceinline__ bool block_tile(const MarchParams &P, uint32_t &tile_
                                            uint32_t &tile_y)
 {
     const uint32_t nwg = gridDim.x, b = blockIdx.x;
-    if (P.tile_order == 3) {
+    if (P.tile_perm) {  // adaptive order (launch_order_tiles)
+        const uint32_t t = P.tile_perm[b];
+        tile_x = t % P.tiles_x;
+        tile_y = t / P.tiles_x;
+        return t != 0xFFFFFFFFu;
+    }
+    if (P.tile_order >= 3) {  // 3, and 4 before its first permutation
         const uint32_t k = b >> 3, w = k & 15;
         const uint32_t s = (b & 7u) + 8u * (k >> 4);
         tile_x = (s % P.supers_x) * 4 + (w & 3);
@@ -564,6 +578,10 @@ __global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP, GF, PIPE>)) 
 
     uint32_t tile_x, tile_y;
     if (!block_tile(P, tile_x, tile_y)) return;
+    const long long wg_start = wall_clock64();
+#ifdef VR_WG_TIMES
+    const unsigned long long wg_t0 = wg_start;
+#endif
 
     const bool tf_in_lds = P.tf_n <= kTfLds;
     if (tf_in_lds)
@@ -777,6 +795,22 @@ __global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP, GF, PIPE>)) 
             atomicAdd(&P.counters[4], sk);
         }
     }
+    if (P.tile_cost) {  // adaptive order: this tile's duration for the next launch
+        __syncthreads();
+        if (tid == 0)
+            P.tile_cost[tile_y * P.tiles_x + tile_x] =
+                (uint32_t)min(wall_clock64() - wg_start, 0x7FFFFFFFLL);
+    }
+#ifdef VR_WG_TIMES
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned int slot = atomicAdd(&g_wg_count, 1u);
+        if (slot < kWgTimesMax) {
+            g_wg_times[2 * slot] = (unsigned long long)wg_t0;
+            g_wg_times[2 * slot + 1] = (unsigned long long)wall_clock64();
+        }
+    }
+#endif
     if (!active) return;
 
     // volume.frag:50 + blend (offscreen_pass.cpp:715-725); uncovered: T = 1, C = 0 -> clear
@@ -812,6 +846,10 @@ __global__ __launch_bounds__(kThreads) void march_pair_kernel(const MarchParams 
     if (!block_tile(P, tile_x, tile_y)) return;
     for (int i = tid; i < 2 * P.tf_n; i += kThreads) s_tf[i] = P.tf[i];
     __syncthreads();
+    const long long wg_start = wall_clock64();
+#ifdef VR_WG_TIMES
+    const unsigned long long wg_t0 = wg_start;
+#endif
     const long by_stride = (long)P.nbx * kBrickElems;
     const long bz_stride = (long)P.nbx * P.nby * kBrickElems;
 
@@ -905,6 +943,22 @@ __global__ __launch_bounds__(kThreads) void march_pair_kernel(const MarchParams 
         prep(S0, k);
         if (consume(S1)) break;
     }
+    if (P.tile_cost) {  // adaptive order: this tile's duration for the next launch
+        __syncthreads();
+        if (tid == 0)
+            P.tile_cost[tile_y * P.tiles_x + tile_x] =
+                (uint32_t)min(wall_clock64() - wg_start, 0x7FFFFFFFLL);
+    }
+#ifdef VR_WG_TIMES
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned int slot = atomicAdd(&g_wg_count, 1u);
+        if (slot < kWgTimesMax) {
+            g_wg_times[2 * slot] = (unsigned long long)wg_t0;
+            g_wg_times[2 * slot + 1] = (unsigned long long)wall_clock64();
+        }
+    }
+#endif
     if (!active || half) return;
     const float A = 1.0f - T;  // volume.frag:50 + blend (offscreen_pass.cpp:715-725)
     const float omA = 1.0f - A;
@@ -919,6 +973,53 @@ __global__ __launch_bounds__(kThreads) void march_pair_kernel(const MarchParams 
     } else {
         static_cast<float4 *>(P.out)[idx] = make_float4(o0, o1, o2, o3);
     }
+}
+
+// ---- adaptive tile order --------------------------------------------------------------------
+
+// One workgroup per XCD x over its tile list (the tiles of the super-tiles s = x (mod 8), as
+// tile_order 3 assigns them; built on the host once per geometry: lists[x * per_xcd + j],
+// ~0 = none): counting-sorted by their last duration into 64 log-scale buckets, longest
+// first, written to perm[x + 8 j] (j = rank), the XCD's remaining slots ~0.  Workgroups are
+// dispatched in index order round-robin over the XCDs, so each XCD starts its longest tiles
+// first and the frame no longer ends on a few long rays.
+__global__ __launch_bounds__(256) void order_tiles_kernel(const uint32_t *__restrict__ cost,
+                                                          const uint32_t *__restrict__ lists,
+                                                          uint32_t *__restrict__ perm,
+                                                          uint32_t per_xcd)
+{
+    __shared__ uint32_t count[64], offset[64], n_tiles;
+    const uint32_t x = blockIdx.x, tid = threadIdx.x;
+    const uint32_t *list = lists + (size_t)x * per_xcd;
+    if (tid < 64) count[tid] = 0;
+    if (tid == 0) n_tiles = 0;
+    __syncthreads();
+    auto bucket = [](uint32_t c) -> uint32_t {  // 4 buckets per octave, 63 = longest
+        if (c < 4) return 0;
+        const uint32_t m = 31 - __clz(c);
+        return min(4 * m + ((c >> (m - 2)) & 3u), 63u);
+    };
+    for (uint32_t j = tid; j < per_xcd; j += blockDim.x) {
+        const uint32_t t = list[j];
+        if (t != 0xFFFFFFFFu) {
+            atomicAdd(&count[bucket(cost[t])], 1u);
+            atomicAdd(&n_tiles, 1u);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t acc = 0;
+        for (int b = 63; b >= 0; --b) {
+            offset[b] = acc;
+            acc += count[b];
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = tid; j < per_xcd; j += blockDim.x) {
+        const uint32_t t = list[j];
+        if (t != 0xFFFFFFFFu) perm[x + 8 * atomicAdd(&offset[bucket(cost[t])], 1u)] = t;
+    }
+    for (uint32_t j = n_tiles + tid; j < per_xcd; j += blockDim.x) perm[x + 8 * j] = 0xFFFFFFFFu;
 }
 
 // ---- volume ingest: linear (any NRRD element type) -> bricked paired elements -------------
@@ -1205,8 +1306,9 @@ __global__ __launch_bounds__(256) void assemble_kernel(const PixT *__restrict__ 
 template <typename VT, bool SHADE, bool COUNT, bool SKIP, bool GF = false, bool PIPE = false>
 hipError_t launch_march_t(const MarchParams &p, hipStream_t stream)
 {
-    const uint32_t nblocks = p.tile_order == 3 ? ((p.supers_total + 7) / 8) * 8 * 16
-                                               : p.tiles_x * p.tiles_y;
+    const uint32_t nblocks = p.tile_perm ? p.nperm
+                             : p.tile_order >= 3 ? ((p.supers_total + 7) / 8) * 8 * 16
+                                                 : p.tiles_x * p.tiles_y;
     if (p.tiles_x * p.tiles_y == 0) return hipSuccess;
     hipLaunchKernelGGL((march_kernel<VT, SHADE, COUNT, SKIP, GF, PIPE>), dim3(nblocks), dim3(kThreads), 0,
                        stream, p);
@@ -1216,8 +1318,9 @@ hipError_t launch_march_t(const MarchParams &p, hipStream_t stream)
 template <typename VT, bool SHADE, bool GF>
 hipError_t launch_pair_t(const MarchParams &p, hipStream_t stream)
 {
-    const uint32_t nblocks = p.tile_order == 3 ? ((p.supers_total + 7) / 8) * 8 * 16
-                                               : p.tiles_x * p.tiles_y;
+    const uint32_t nblocks = p.tile_perm ? p.nperm
+                             : p.tile_order >= 3 ? ((p.supers_total + 7) / 8) * 8 * 16
+                                                 : p.tiles_x * p.tiles_y;
     if (p.tiles_x * p.tiles_y == 0) return hipSuccess;
     if (p.pair == 4)
         hipLaunchKernelGGL((march_pair_kernel<VT, SHADE, GF, 4>), dim3(nblocks), dim3(kThreads),
@@ -1425,6 +1528,32 @@ hipError_t launch_skip_dist(const float2 *range_dev, uint32_t nbx, uint32_t nby,
     hipLaunchKernelGGL(dist_pass_kernel, dim3(g), dim3(256), 0, s, (const uint8_t *)dist_dev,
                        scratch_dev, nbx, nby, nbz, 2);
     return hipMemcpyAsync(dist_dev, scratch_dev, nb, hipMemcpyDeviceToDevice, s);
+}
+
+#ifdef VR_WG_TIMES
+hipError_t debug_wg_times_reset()
+{
+    const unsigned int z = 0;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_wg_count), &z, sizeof(z));
+}
+hipError_t debug_wg_times_read(unsigned long long *out, unsigned int max, unsigned int *count)
+{
+    unsigned int n = 0;
+    hipError_t e = hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_wg_count), sizeof(n));
+    if (e != hipSuccess) return e;
+    n = n < kWgTimesMax ? n : kWgTimesMax;
+    n = n < max ? n : max;
+    *count = n;
+    return n ? hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_times), 2 * n * sizeof(unsigned long long))
+             : hipSuccess;
+}
+#endif
+
+hipError_t launch_order_tiles(const uint32_t *cost, const uint32_t *lists, uint32_t *perm,
+                              uint32_t per_xcd, hipStream_t s)
+{
+    hipLaunchKernelGGL(order_tiles_kernel, dim3(8), dim3(256), 0, s, cost, lists, perm, per_xcd);
+    return hipGetLastError();
 }
 
 }  // namespace vr
