@@ -482,10 +482,13 @@ __device__ unsigned int g_wg_count;
 #ifndef VR_SKIP_MIN_WAVES
 #define VR_SKIP_MIN_WAVES 1
 #endif
-// (PIPE launches are small by construction: no floor.)
+#ifndef VR_PIPE_MIN_WAVES
+#define VR_PIPE_MIN_WAVES 1
+#endif
 template <bool COUNT, bool SKIP, bool GF, bool PIPE>
 constexpr int kMarchMinWaves =
-    (GF || PIPE) ? 1 : (COUNT ? 4 : (SKIP ? VR_SKIP_MIN_WAVES : VR_MARCH_MIN_WAVES));
+    PIPE ? VR_PIPE_MIN_WAVES
+         : (GF ? 1 : (COUNT ? 4 : (SKIP ? VR_SKIP_MIN_WAVES : VR_MARCH_MIN_WAVES)));
 
 #ifndef VR_SKIP_PACKED_GRADIENT
 #define VR_SKIP_PACKED_GRADIENT 0
