@@ -428,3 +428,33 @@ def test_f32_gradient_field_equals_stencil_gradient(rp, monkeypatch):
     ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), synth.tf_band(0.2, 0.9), cam,
                            W, H, vr_amd.default_params(shading=1))
     check(a, ref)
+
+
+@pytest.mark.parametrize("shading", [0, 1])
+def test_kernel_variants_bit_identical(rp, monkeypatch, shading):
+    """Every march kernel a launch can select -- single lane, pipelined (PIPE), lane groups of
+    2 and 4 (march_pair_kernel), with and without the f32 difference field -- renders the
+    same bytes and matches the oracle (forced through the A/B environment overrides)."""
+    W, H = 96, 72
+    rp.framebuffer_size_changed(W, H)
+    vol = synth.gaussians_numpy((33, 27, 40), seed=17).astype(np.float32)
+    rp.volume_dataset_changed(synth.dataset(vol))
+    tf = synth.tf_band(0.15, 0.95)
+    rp.transfer_function_changed(tf)
+    cam = synth.camera("fill_oblique").to_vr_camera()
+    p = vr_amd.default_params(shading=shading, ert_eps=1e-4)
+    combos = [dict(VR_PIPELINE="0", VR_PAIR="0"), dict(VR_PIPELINE="1", VR_PAIR="0"),
+              dict(VR_PAIR="1", VR_PAIR_LANES="2"), dict(VR_PAIR="1", VR_PAIR_LANES="4"),
+              dict(VR_PAIR="1", VR_PAIR_LANES="4", VR_NO_GRAD_FIELD="1"),
+              dict(VR_PIPELINE="1", VR_PAIR="0", VR_NO_GRAD_FIELD="1")]
+    imgs = []
+    for env in combos:
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        imgs.append(rp.render(cam, p, vr_amd.OUT_RGBA32F))
+        for k in env:
+            monkeypatch.delenv(k)
+    for env, img in zip(combos[1:], imgs[1:]):
+        assert np.array_equal(img.view(np.uint32), imgs[0].view(np.uint32)), env
+    ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p)
+    check(imgs[0], ref)
