@@ -336,14 +336,17 @@ int check_params(vr_ctx *c, const vr_params *p)
 }
 
 // Pipelined march (two samples of a ray in flight, vr_kernels.hip PIPE): always for shaded
-// frames (-6% over the view sweep), and for unshaded launches of fewer than
-// kPipelineMaxWaves wavefronts -- one rank's share of a multi-GPU frame -- where per-ray
-// latency, not the chip's throughput, bounds the kernel (N = 8 rank share: 0.153 -> 0.094 ms;
-// at full-frame size it loses on the diagonal view).  VR_PIPELINE=0/1 overrides (A/B).
-bool use_pipeline(bool shading, uint32_t tiles)
+// frames (-6% over the view sweep); for unshaded launches of fewer than kPipelineMaxWaves
+// wavefronts -- one rank's share of a multi-GPU frame -- where per-ray latency, not the
+// chip's throughput, bounds the kernel (N = 8 rank share: 0.153 -> 0.094 ms); and for
+// volumes of >= kPipelineMinBytes bricked bytes, whose gathers miss the caches more
+// (C4 1024^3 u8 -12%, C5 2048^3 u8 -9%; a 256^3 u8 or 512^3 f32 full frame loses).
+// VR_PIPELINE=0/1 overrides (A/B).
+bool use_pipeline(bool shading, uint32_t tiles, size_t volume_bytes)
 {
     if (const char *e = std::getenv("VR_PIPELINE")) return e[0] == '1';
-    return shading || tiles * (kThreadsPerTile / 64) < kPipelineMaxWaves;
+    return shading || tiles * (kThreadsPerTile / 64) < kPipelineMaxWaves ||
+           volume_bytes >= kPipelineMinBytes;
 }
 
 // Lane-pair march (two lanes per ray, each lane pipelined) for SHADED launches of fewer than
@@ -425,7 +428,7 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.out_format = out_format;
     P.slab_default = c->smin[0] == 0.0f && c->smin[1] == 0.0f && c->smin[2] == 0.0f &&
                      c->smax[0] == 1.0f && c->smax[1] == 1.0f && c->smax[2] == 1.0f;
-    P.pipelined = use_pipeline(p->shading != 0, P.tiles_x * P.tiles_y);
+    P.pipelined = use_pipeline(p->shading != 0, P.tiles_x * P.tiles_y, c->brick_bytes);
     return VR_OK;
 }
 
@@ -1039,8 +1042,8 @@ const char *vr_kernel_name(const vr_ctx *c, const vr_params *p)
     const bool gf = p && p->shading && c->storage == ST_F32 && c->grad && c->grad_valid;
     // the full frame (row_block 16, one rank), as vr_render launches it
     const uint32_t tiles = ((c->width + 15) / 16) * ((c->height + 15) / 16);
-    const bool pipe = use_pipeline(p && p->shading, tiles) && !(p && p->skip_empty) &&
-                      c->tf_n <= 256;
+    const bool pipe = use_pipeline(p && p->shading, tiles, c->brick_bytes) &&
+                      !(p && p->skip_empty) && c->tf_n <= 256;
     return march_kernel_name(c->storage, p && p->shading != 0, false, p && p->skip_empty != 0, gf,
                              pipe);
 }

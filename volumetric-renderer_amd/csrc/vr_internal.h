@@ -109,6 +109,7 @@ hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &
 const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bool gf, bool pipe);
 // Wavefront count below which a launch uses the pipelined kernel (see build_params).
 constexpr uint32_t kPipelineMaxWaves = 24576;  // between N = 2 (16 K) and N = 1 (33 K) at 1080p
+constexpr size_t kPipelineMinBytes = 4ull << 30;  // large volumes: always pipelined
 constexpr uint32_t kThreadsPerTile = 256;  // 16 x 16 pixels
 // Adaptive tile order: from the per-tile durations of the last launch with the same tile
 // geometry, the next launch's workgroup -> tile permutation, longest first within each XCD's
