@@ -236,7 +236,24 @@ def main():
     achieved = algorithmic_bytes(r0stats, vbytes, shard_px) / (kms * 1e-3) / 1e9
     traffic = load_traffic(args.config, world)
 
+    # also the reference-equivalent sample count (volume.frag as written: no
+    # ERT, every in-slab step sampled) of the same frame, per second of this configuration
+    ref_cam = synth.camera(cfg["cam"]).to_vr_camera()
+    ref_stats = rp.count_work(ref_cam, vr_amd.default_params(), 8, rank, world)
+    ref_samples = torch.tensor([ref_stats["samples"]], dtype=torch.float64,
+                               device="cuda" if BACKEND == "nccl" else "cpu")
+    if world > 1:
+        dist.all_reduce(ref_samples, op=dist.ReduceOp.SUM)
+    ref_samples = int(ref_samples.item())
+
     variants = {}
+    if world > 1 and not args.no_variants and overlap:
+        # the serial form too (each frame's gather waited before the next render)
+        s4, k4, _, _, _, c4 = run_variant(rp, cfg, max(5, args.steps // 2), min(args.warmup, 5), rank,
+                                          world, stream, overlap=False)
+        variants["serial_gather"] = dict(value=round(fstats["samples"] * max(5, args.steps // 2) / s4 / 1e9, 3),
+                                         unit="Gsamples/s", ms_per_step=round(s4 / max(5, args.steps // 2) * 1e3, 4),
+                                         frame_check=c4)
     if not args.no_variants and args.config == "c3":
         vcfg = CONFIGS["c3_ref"]
         rp.transfer_function_changed(synth.TFS[vcfg["tf"]]())
@@ -276,6 +293,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(secs / args.steps * 1e3, 4),
             "fps": round(fps, 2),
+            "reference_equivalent_gsamples_per_s": round(ref_samples * args.steps / secs / 1e9, 3),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -293,6 +311,7 @@ def main():
                      else " + RCCL gather (serial)")
                     if world > 1 else ""),
                 "samples_per_frame": fstats["samples"],
+                "reference_equivalent_samples_per_frame": ref_samples,
                 "shaded_samples_per_frame": fstats["shaded_samples"],
                 "rays_per_frame": fstats["rays"],
             },
