@@ -11,7 +11,9 @@
  * the last failure is available from vr_last_error().  A context is bound to ONE HIP
  * device and is not thread-safe (one host thread per context, as the reference's single
  * render thread).  Multi-GPU runs use one process (and one context) per GPU; see
- * vr_render_device() row-block sharding and vr_assemble_rows().
+ * vr_render_device() row-block sharding and vr_assemble_rows().  Volume and TF changes wait
+ * for the device first (the reference's vkDeviceWaitIdle before a resource swap), so frames
+ * still in flight on any stream finish on the old data.
  *
  * Mapping to the reference (each function lists the interface it replaces):
  *   vr_create                 OffscreenPass::OffscreenPass(VulkanContext*, w, h)   offscreen_pass.cpp:112-134

@@ -96,6 +96,16 @@ int hip_fail(vr_ctx *c, hipError_t e, const char *what)
         if (_e != hipSuccess) return hip_fail(c, _e, what); \
     } while (0)
 
+// Resource swaps wait for the device first, as the reference does (vkDeviceWaitIdle,
+// offscreen_pass.cpp:242,260,282): a frame still in flight on any stream may read the volume,
+// TF or derived fields that are about to be rewritten or freed.
+int wait_idle(vr_ctx *c)
+{
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    HIP_TRY(c, hipDeviceSynchronize(), "hipDeviceSynchronize (resource swap)");
+    return VR_OK;
+}
+
 int storage_for(int dtype)
 {
     switch (dtype) {
@@ -684,9 +694,10 @@ int vr_set_volume_device(vr_ctx *c, const void *data_dev, int dtype, uint32_t nx
     if (st < 0) return fail(c, VR_EINVAL, "unsupported volume dtype");
     if (nx == 0 || ny == 0 || nz == 0) return fail(c, VR_EINVAL, "volume dims must be non-zero");
     if (nx > 65536 || ny > 65536 || nz > 65536) return fail(c, VR_EINVAL, "volume dim > 65536");
-    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    int rc = wait_idle(c);
+    if (rc) return rc;
     void *dst = nullptr;
-    int rc = set_bricks(c, st, nx, ny, nz, &dst);
+    rc = set_bricks(c, st, nx, ny, nz, &dst);
     if (rc) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
     HIP_TRY(c, launch_brick_from_linear(dtype, data_dev, dst, nx, ny, nz, st, s), "brick kernel");
@@ -708,6 +719,7 @@ int vr_set_volume(vr_ctx *c, const void *data, int dtype, uint32_t nx, uint32_t 
     if (!data) return fail(c, VR_EINVAL, "volume data is NULL");
     if (storage_for(dtype) < 0) return fail(c, VR_EINVAL, "unsupported volume dtype");
     if (nx == 0 || ny == 0 || nz == 0) return fail(c, VR_EINVAL, "volume dims must be non-zero");
+    if (nx > 65536 || ny > 65536 || nz > 65536) return fail(c, VR_EINVAL, "volume dim > 65536");
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     const size_t bytes = (size_t)nx * ny * nz * dtype_size(dtype);
     void *tmp = nullptr;
@@ -736,6 +748,7 @@ int vr_generate_volume(vr_ctx *c, int kind, int dtype, uint32_t nx, uint32_t ny,
         default: return fail(c, VR_EINVAL, "generator supports u8, u16, f32");
     }
     if (nx == 0 || ny == 0 || nz == 0) return fail(c, VR_EINVAL, "volume dims must be non-zero");
+    if (nx > 65536 || ny > 65536 || nz > 65536) return fail(c, VR_EINVAL, "volume dim > 65536");
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     const int ng = 32;
     std::vector<float> prm(3 + 5 * ng);
@@ -755,6 +768,7 @@ int vr_generate_volume(vr_ctx *c, int kind, int dtype, uint32_t nx, uint32_t ny,
     // generate into a linear staging buffer of the storage type, then brick it like an
     // uploaded volume (vr_set_volume_device path)
     const size_t count = (size_t)nx * ny * nz;
+    if (int rc0 = wait_idle(c)) return rc0;
     float *prm_dev = nullptr;
     void *lin = nullptr;
     HIP_TRY(c, hipMalloc(&prm_dev, prm.size() * sizeof(float) + 2 * sizeof(uint32_t)),
@@ -859,7 +873,7 @@ int vr_set_transfer_function(vr_ctx *c, const uint32_t *rgba8_srgb, uint32_t n)
     if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
     if (!rgba8_srgb || n == 0) return fail(c, VR_EINVAL, "transfer function is empty");
     if (n > (1u << 20)) return fail(c, VR_EINVAL, "transfer function too large");
-    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    if (int rc = wait_idle(c)) return rc;
     return upload_tf(c, rgba8_srgb, n);
 }
 
