@@ -36,6 +36,7 @@ import vr_amd  # noqa: E402
 import vr_dist  # noqa: E402
 
 BACKEND = "nccl"
+GATHER = "native"  # N > 1 over RCCL: "native" (vr_dist.h) or "torch" (torch.distributed.gather)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "Gsamples/sec + fps, 512³ NRRD @ 1080p; achieved HBM GB/s vs peak"
 
@@ -79,23 +80,62 @@ def setup_pass(cfg, device):
     return rp
 
 
-def run_variant(rp, cfg, steps, warmup, rank, world, stream, row_block=8, overlap=True):
+_DIST = {}
+
+
+def dist_frames(rp, rank, world, row_block, inflight):
+    """One RCCL communicator per frames-in-flight setting (vr_dist_create), id from rank 0
+    broadcast over the torch.distributed process group."""
+    key = (row_block, inflight)
+    if key not in _DIST:
+        uid = vr_amd.dist_unique_id() if rank == 0 else bytes(vr_amd.DIST_ID_BYTES)
+        t = torch.tensor(list(uid), dtype=torch.uint8, device="cuda")
+        dist.broadcast(t, 0)
+        _DIST[key] = vr_amd.DistFrames(rp, bytes(t.cpu().tolist()), world, rank, row_block, inflight)
+    return _DIST[key]
+
+
+class NativeFrames:
+    """FramePipeline's interface over vr_amd.DistFrames (include/vr/vr_dist.h)."""
+
+    def __init__(self, frames, cam, p, rank, H, W):
+        self.frames, self.cam, self.p, self.rank = frames, cam, p, rank
+        self.stream = torch.cuda.Stream()
+        self.last = vr_dist.Slot(None, frame=torch.empty((H, W), dtype=torch.int32, device="cuda")
+                                 if rank == 0 else None)
+
+    def step(self):
+        self.frames.render(self.cam, self.p, self.last.frame.data_ptr() if self.rank == 0 else 0,
+                           self.stream.cuda_stream)
+
+    def drain(self):
+        self.frames.synchronize()
+        self.stream.synchronize()
+
+
+def run_variant(rp, cfg, steps, warmup, rank, world, inflight, row_block=8):
     """Time `steps` frames; returns (max-over-ranks seconds, avg kernel ms, frame stats,
-    this rank's stats, this rank's shard pixels).  For N > 1 a frame is: render this rank's
-    row blocks -> RCCL gather to rank 0 -> de-interleave on rank 0, with the gather of frame k
-    overlapped with the render of frame k+1 (vr_dist.FramePipeline) unless overlap=False."""
+    this rank's stats, this rank's shard pixels, frame check).  For N > 1 a frame is: render
+    this rank's row blocks -> RCCL gather to rank 0 -> de-interleave on rank 0.  `inflight`
+    frames are in flight (vr_dist.FramePipeline): frame i's work goes to stream i mod
+    inflight, so consecutive frames overlap on the device and a frame's gather overlaps the
+    next frames' renders; inflight = 1 is the serial frame loop."""
     W, H = cfg["W"], cfg["H"]
     cam = synth.camera(cfg["cam"]).to_vr_camera()
     p = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"],
-                              skip_empty=cfg.get("skip_empty", 0))
+                              skip_empty=cfg.get("skip_empty", 0), frames_in_flight=inflight)
     sr = vr_amd.shard_rows(H, row_block, world)
-    nbuf = 2 if (world > 1 and overlap) else 1
-    shards = [torch.empty((sr, W), dtype=torch.int32, device="cuda") for _ in range(nbuf)]
-    gbufs = frame = None
-    if world > 1 and rank == 0:
-        # RCCL gathers straight into the rank-major buffers the assembly kernel reads
-        gbufs = [torch.empty((world, sr, W), dtype=torch.int32, device="cuda") for _ in range(nbuf)]
-        frame = torch.empty((H, W), dtype=torch.int32, device="cuda")
+    if BACKEND != "nccl":
+        inflight = 1  # host-staged gloo rehearsal: serial
+    slots = []
+    for _ in range(inflight):
+        gbuf = frame = None
+        if world > 1 and rank == 0:
+            # RCCL gathers straight into the rank-major buffer the assembly kernel reads
+            gbuf = torch.empty((world, sr, W), dtype=torch.int32, device="cuda")
+            frame = torch.empty((H, W), dtype=torch.int32, device="cuda")
+        slots.append(vr_dist.Slot(torch.empty((sr, W), dtype=torch.int32, device="cuda"), gbuf,
+                                  frame, torch.cuda.Stream()))
 
     my_stats = rp.count_work(cam, p, row_block, rank, world)
     sdev = "cuda" if BACKEND == "nccl" else "cpu"
@@ -105,13 +145,18 @@ def run_variant(rp, cfg, steps, warmup, rank, world, stream, row_block=8, overla
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     frame_stats = dict(zip(keys, [int(x) for x in tot.tolist()]))
 
-    pipe = vr_dist.FramePipeline(
-        shards, gbufs, rank, world, dist,
-        render=lambda buf: rp.render_device(cam, p, buf.data_ptr(), vr_amd.OUT_RGBA8, row_block,
-                                            rank, world, stream),
-        assemble=lambda g: rp.assemble_rows(g.data_ptr(), frame.data_ptr(), vr_amd.OUT_RGBA8,
-                                            row_block, world, stream),
-        overlap=overlap, host_staging=(BACKEND != "nccl"))
+    if world > 1 and BACKEND == "nccl" and GATHER == "native":
+        # the whole frame in the library: render -> ncclGather -> assemble, stream-ordered
+        pipe = NativeFrames(dist_frames(rp, rank, world, row_block, inflight), cam, p, rank, H, W)
+    else:
+        pipe = vr_dist.FramePipeline(
+            slots, rank, world, dist,
+            render=lambda sl: rp.render_device(cam, p, sl.shard.data_ptr(), vr_amd.OUT_RGBA8,
+                                               row_block, rank, world, sl.stream.cuda_stream),
+            assemble=lambda sl: rp.assemble_rows(sl.gbuf.data_ptr(), sl.frame.data_ptr(),
+                                                 vr_amd.OUT_RGBA8, row_block, world,
+                                                 sl.stream.cuda_stream),
+            host_staging=(BACKEND != "nccl"))
 
     for _ in range(warmup):
         pipe.step()
@@ -141,9 +186,10 @@ def run_variant(rp, cfg, steps, warmup, rank, world, stream, row_block=8, overla
     if world > 1 and rank == 0:
         # the assembled frame must equal this device's single-rank render of the whole frame
         full = torch.empty((vr_amd.shard_rows(H, row_block, 1), W), dtype=torch.int32, device="cuda")
-        rp.render_device(cam, p, full.data_ptr(), vr_amd.OUT_RGBA8, row_block, 0, 1, stream)
+        rp.render_device(cam, p, full.data_ptr(), vr_amd.OUT_RGBA8, row_block, 0, 1,
+                         torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
-        check = bool(torch.equal(full[:H], frame))
+        check = bool(torch.equal(full[:H], pipe.last.frame))
     return float(el.item()), kms / max(nl, 1), frame_stats, my_stats, sr * W, check
 
 
@@ -204,8 +250,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--frames-in-flight", type=int, default=3,
+                    help="frames in flight on separate streams (1 = serial frame loop)")
     ap.add_argument("--serial-gather", action="store_true",
-                    help="N > 1: wait for each frame's gather before rendering the next")
+                    help="= --frames-in-flight 1: each frame's gather waited for before the next render")
+    ap.add_argument("--gather", default="native", choices=("native", "torch"),
+                    help="N > 1: the library's RCCL frame path (vr_dist.h) or torch.distributed.gather")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -213,8 +263,9 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # VR_DIST_BACKEND=gloo rehearses the N > 1 path with ranks sharing devices (host-staged
     # gathers); the real multi-GPU run uses "nccl" (RCCL over xGMI), one device per rank.
-    global BACKEND
+    global BACKEND, GATHER
     BACKEND = os.environ.get("VR_DIST_BACKEND", "nccl")
+    GATHER = args.gather
     device = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
     if world > 1:
@@ -222,15 +273,16 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group(BACKEND)
-    stream = torch.cuda.current_stream().cuda_stream
 
     cfg = CONFIGS[args.config]
     rp = setup_pass(cfg, device)
     vbytes = np.dtype(cfg["dtype"]).itemsize
 
-    overlap = not args.serial_gather
+    inflight = 1 if args.serial_gather else max(1, min(16, args.frames_in_flight))
+    if BACKEND != "nccl":
+        inflight = 1
     secs, kms, fstats, r0stats, shard_px, frame_check = run_variant(rp, cfg, args.steps, args.warmup, rank, world,
-                                                       stream, overlap=overlap)
+                                                                    inflight)
     value = fstats["samples"] * args.steps / secs / 1e9
     fps = args.steps / secs
     achieved = algorithmic_bytes(r0stats, vbytes, shard_px) / (kms * 1e-3) / 1e9
@@ -247,18 +299,22 @@ def main():
     ref_samples = int(ref_samples.item())
 
     variants = {}
-    if world > 1 and not args.no_variants and overlap:
-        # the serial form too (each frame's gather waited before the next render)
-        s4, k4, _, _, _, c4 = run_variant(rp, cfg, max(5, args.steps // 2), min(args.warmup, 5), rank,
-                                          world, stream, overlap=False)
-        variants["serial_gather"] = dict(value=round(fstats["samples"] * max(5, args.steps // 2) / s4 / 1e9, 3),
-                                         unit="Gsamples/s", ms_per_step=round(s4 / max(5, args.steps // 2) * 1e3, 4),
-                                         frame_check=c4)
+    if not args.no_variants and inflight > 1:
+        # the serial form too (one frame at a time; for N > 1 each frame's
+        # gather waited for before the next render).  Its kernels run alone on the device,
+        # so their HIP-event durations are the kernel's own (reported beside the roofline).
+        ns = max(5, args.steps // 2)
+        s4, k4, _, r4, _, c4 = run_variant(rp, cfg, ns, min(args.warmup, 5), rank, world, 1)
+        variants["serial_frames"] = dict(
+            value=round(fstats["samples"] * ns / s4 / 1e9, 3), unit="Gsamples/s",
+            ms_per_step=round(s4 / ns * 1e3, 4), fps=round(ns / s4, 2), kernel_ms=round(k4, 4),
+            roofline_frac=round(algorithmic_bytes(r4, vbytes, shard_px) / (k4 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            frame_check=c4)
     if not args.no_variants and args.config == "c3":
         vcfg = CONFIGS["c3_ref"]
         rp.transfer_function_changed(synth.TFS[vcfg["tf"]]())
-        s2, k2, f2, r2, _, _ = run_variant(rp, vcfg, args.steps, min(args.warmup, 5), rank, world, stream,
-                                        overlap=overlap)
+        s2, k2, f2, r2, _, _ = run_variant(rp, vcfg, args.steps, min(args.warmup, 5), rank, world,
+                                           inflight)
         variants["reference_semantics_no_shading_no_ert"] = dict(
             value=round(f2["samples"] * args.steps / s2 / 1e9, 3), unit="Gsamples/s",
             fps=round(args.steps / s2, 2), samples_per_frame=f2["samples"],
@@ -268,8 +324,8 @@ def main():
         # reported as fps and as reference-equivalent samples/s, never as the headline value
         scfg = dict(CONFIGS["c3"], skip_empty=1)
         rp.transfer_function_changed(synth.TFS[scfg["tf"]]())
-        s3, k3, f3, r3, _, _ = run_variant(rp, scfg, args.steps, min(args.warmup, 5), rank, world, stream,
-                                        overlap=overlap)
+        s3, k3, f3, r3, _, _ = run_variant(rp, scfg, args.steps, min(args.warmup, 5), rank, world,
+                                           inflight)
         variants["c3_skip_empty"] = dict(
             fps=round(args.steps / s3, 2), ms_per_step=round(s3 / args.steps * 1e3, 4),
             kernel_ms=round(k3, 4),
@@ -307,9 +363,10 @@ def main():
                 "tf": cfg["tf"], "shading": cfg["shading"], "ert_eps": cfg["ert"],
                 "parallelism": f"image 8-row blocks cyclic x{world}" + (
                     (" + gloo host-staged gather (rehearsal, ranks share devices)" if BACKEND != "nccl"
-                     else " + RCCL gather (overlapped with next frame)" if overlap
-                     else " + RCCL gather (serial)")
-                    if world > 1 else ""),
+                     else " + RCCL ncclGather (vr_dist.h, stream-ordered)" if GATHER == "native"
+                     else " + RCCL gather (torch.distributed)")
+                    if world > 1 else "") + f", {inflight} frames in flight",
+                "frames_in_flight": inflight,
                 "samples_per_frame": fstats["samples"],
                 "reference_equivalent_samples_per_frame": ref_samples,
                 "shaded_samples_per_frame": fstats["shaded_samples"],
@@ -328,6 +385,10 @@ def main():
                 "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"
                                   if traffic else None,
                 "kernel_ms": round(kms, 4),
+                # with frames in flight a kernel shares the device with its neighbours, so its
+                # duration exceeds the frame period; this is the same bytes per frame period
+                "achieved_per_frame_period": round(
+                    algorithmic_bytes(r0stats, vbytes, shard_px) / (secs / args.steps) / 1e9, 1),
                 "bytes_model": "8*sizeof(voxel)/sample + 48*sizeof(voxel)/shaded sample + 4 B/pixel (SURVEY.md 8d)",
             },
             "cpu_baseline": cpu,
@@ -335,6 +396,8 @@ def main():
             "variants": variants,
         }
         print(json.dumps(out), flush=True)
+    for d in _DIST.values():
+        d.close()
     rp.close()
     if world > 1:
         dist.destroy_process_group()

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 2
+#define VR_ABI_VERSION 3
 
 /* ---- status codes (negative errno style) ---- */
 #define VR_OK 0
@@ -114,7 +114,14 @@ typedef struct vr_params {
     /* Pixel footprint of one 64-lane wavefront inside the 16x16 workgroup tile (speed only,
      * never results): 0 auto (16x4), 1 8x8, 2 16x4, 3 4x16. */
     int32_t wave_shape;
-    int32_t reserved[1];
+    /* Frames the caller keeps in flight on different streams (speed only, never results).
+     * 0 or 1: frames are rendered one after another, so a small launch (one rank's share of
+     * a multi-GPU frame) is bound by its longest rays and runs the lane-group kernel that
+     * shortens them.  >= 2: consecutive frames overlap on the device (the reference keeps
+     * MAX_FRAMES_IN_FLIGHT = 2, vulkan_context.h:17), the next frame fills the chip while
+     * this one drains, and every launch runs the single-lane kernels, which do the least
+     * work per sample.  Must be in [0, 16]. */
+    int32_t frames_in_flight;
 } vr_params;
 
 /* Work counters of one frame (filled by vr_count_work). */
@@ -143,6 +150,8 @@ const char *vr_last_error(const vr_ctx *ctx);
 /* framebuffer_size_changed: 0 sizes are ignored (offscreen_pass.cpp:237-239). */
 int vr_resize(vr_ctx *ctx, uint32_t width, uint32_t height);
 int vr_get_size(const vr_ctx *ctx, uint32_t *width, uint32_t *height);
+/* The HIP device index the context renders on (vr_create's `device`). */
+int vr_get_device(const vr_ctx *ctx, int *device);
 
 /* ---- inputs (the callee copies; the caller keeps ownership) ---- */
 

@@ -25,10 +25,10 @@ def exported():
     return {l.split()[-1] for l in out.splitlines() if " T " in l}
 
 
-@pytest.mark.parametrize("header", ["vr.h", "vr_host.h"])
+@pytest.mark.parametrize("header", ["vr.h", "vr_host.h", "vr_dist.h"])
 def test_every_declared_symbol_is_exported(header):
     names = declared(header)
-    assert len(names) > 10
+    assert len(names) >= 6
     missing = names - exported()
     assert not missing, missing
 
@@ -36,11 +36,12 @@ def test_every_declared_symbol_is_exported(header):
 def test_binding_lists_cover_headers():
     assert declared("vr.h") == set(vr_amd.ABI_SYMBOLS)
     assert declared("vr_host.h") == set(vr_amd.HOST_SYMBOLS)
+    assert declared("vr_dist.h") == set(vr_amd.DIST_SYMBOLS)
 
 
 def test_library_loads_and_pure_entry_points():
     L = vr_amd.lib()
-    assert L.vr_abi_version() == 2
+    assert L.vr_abi_version() == 3
     p = vr_amd.default_params()
     assert p.step == pytest.approx(0.005) and p.ray_dist == pytest.approx(1.8)
     assert list(p.clear_color) == pytest.approx([0.11, 0.11, 0.11, 1.0])
@@ -62,8 +63,8 @@ def test_struct_layouts_match_header():
 #include "vr/vr.h"
 #include <stdio.h>
 #include <stddef.h>
-int main(void) { printf("%zu %zu %zu %zu %zu\n", sizeof(vr_camera), sizeof(vr_params),
-  sizeof(vr_stats), offsetof(vr_params, spec_power), offsetof(vr_params, skip_empty)); return 0; }
+int main(void) { printf("%zu %zu %zu %zu %zu %zu\n", sizeof(vr_camera), sizeof(vr_params),
+  sizeof(vr_stats), offsetof(vr_params, spec_power), offsetof(vr_params, skip_empty), offsetof(vr_params, frames_in_flight)); return 0; }
 """
     tmp = os.path.join("/tmp", "vr_abi_layout")
     with open(tmp + ".c", "w") as f:
@@ -72,8 +73,9 @@ int main(void) { printf("%zu %zu %zu %zu %zu\n", sizeof(vr_camera), sizeof(vr_pa
     out = subprocess.run([tmp], capture_output=True, text=True, check=True).stdout.split()
     assert [int(x) for x in out] == [C.sizeof(vr_amd.vr_camera), C.sizeof(vr_amd.vr_params),
                                      C.sizeof(vr_amd.vr_stats), vr_amd.vr_params.spec_power.offset,
-                                     vr_amd.vr_params.skip_empty.offset]
-    assert "VR_ABI_VERSION 2" in src
+                                     vr_amd.vr_params.skip_empty.offset,
+                                     vr_amd.vr_params.frames_in_flight.offset]
+    assert "VR_ABI_VERSION 3" in src
 
 
 def test_create_without_device_fails_cleanly():
@@ -84,10 +86,24 @@ def test_create_without_device_fails_cleanly():
         vr_amd.OffscreenPass(8, 8)
 
 
+def test_dist_entry_points_reject_bad_arguments():
+    """vr_dist.h argument checks (no communicator is created, no device touched)."""
+    L = vr_amd.lib()
+    assert L.vr_dist_create(None, None, 2, 0, 8, 3) is None
+    assert b"NULL" in L.vr_dist_last_error(None)
+    assert L.vr_dist_unique_id(None) == -22
+    p = vr_amd.default_params()
+    cam = vr_amd.make_camera().to_vr_camera()
+    assert L.vr_dist_render(None, C.byref(cam), C.byref(p), None, None) == -22
+    assert L.vr_dist_synchronize(None) == -22
+    L.vr_dist_destroy(None)  # no-op
+
+
 def test_no_cpu_fallback_in_product():
     """The product path never routes through the oracle or any CPU renderer."""
     for path in ("volumetric-renderer_amd/vr_amd.py", "volumetric-renderer_amd/csrc/vr_api.hip",
-                 "volumetric-renderer_amd/csrc/vr_kernels.hip", "volumetric-renderer_amd/host/vr_host.cpp"):
+                 "volumetric-renderer_amd/csrc/vr_kernels.hip", "volumetric-renderer_amd/host/vr_host.cpp",
+                 "volumetric-renderer_amd/csrc/vr_dist.cpp"):
         txt = open(os.path.join(ROOT, path)).read()
         for needle in ("pyoracle", "liboracle", "oracle.h", "import oracle", "ref_numpy", "or_render"):
             assert needle not in txt, (path, needle)

@@ -458,3 +458,43 @@ def test_kernel_variants_bit_identical(rp, monkeypatch, shading):
         assert np.array_equal(img.view(np.uint32), imgs[0].view(np.uint32)), env
     ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p)
     check(imgs[0], ref)
+
+
+def test_frames_in_flight_on_streams_are_identical(rp):
+    """Frames rendered back to back on 3 streams (frames_in_flight = 3, own output buffer per
+    stream, adaptive tile order per stream) equal the serial frame byte for byte.  Right
+    after a volume or TF change the first frame on one stream builds the derived fields (the
+    f32 difference field, the skip-empty classification) and the frames on the other
+    streams must wait for that build (vr_api.hip ensure_derived); the rank shares of a
+    4-way split are rendered the same way."""
+    import torch
+    W, H = 96, 80
+    rp.framebuffer_size_changed(W, H)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    cam = synth.camera("fill_oblique").to_vr_camera()
+    for seed, tf in ((5, synth.tf_band(0.1, 0.9)), (6, synth.tf2())):
+        vol = synth.gaussians_numpy((41, 37, 45), seed=seed).astype(np.float32)
+        for shading, skip in ((1, 0), (0, 1), (1, 1)):
+            for nranks in (1, 4):
+                sr = vr_amd.shard_rows(H, 8, nranks)
+                serial = vr_amd.default_params(shading=shading, skip_empty=skip, ert_eps=1e-5)
+                inflight = vr_amd.default_params(shading=shading, skip_empty=skip, ert_eps=1e-5,
+                                                 frames_in_flight=3)
+                ref = torch.zeros((sr, W), dtype=torch.int32, device="cuda")  # padding rows stay 0
+                outs = [torch.zeros((sr, W), dtype=torch.int32, device="cuda") for _ in range(6)]
+                torch.cuda.synchronize()
+                # fresh volume + TF: no derived field exists yet when the streams start
+                rp.volume_dataset_changed(synth.dataset(vol))
+                rp.transfer_function_changed(tf)
+                for i, o in enumerate(outs):
+                    rp.render_device(cam, inflight, o.data_ptr(), vr_amd.OUT_RGBA8, 8, nranks - 1,
+                                     nranks, streams[i % 3].cuda_stream)
+                torch.cuda.synchronize()
+                rp.render_device(cam, serial, ref.data_ptr(), vr_amd.OUT_RGBA8, 8, nranks - 1,
+                                 nranks, torch.cuda.current_stream().cuda_stream)
+                torch.cuda.synchronize()
+                for i, o in enumerate(outs):
+                    assert torch.equal(o, ref), (seed, shading, skip, nranks, i)
+    bad = vr_amd.default_params(frames_in_flight=17)
+    with pytest.raises(RuntimeError):
+        rp.render(cam, bad)

@@ -33,7 +33,7 @@ def _scene(W, H, k=0):
                                       cam, W, H, p)
 
 
-def _worker(rank, world, port, W, H, rb, overlap, nframes, q):
+def _worker(rank, world, port, W, H, rb, inflight, nframes, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for sub in ("volumetric-renderer_amd", "oracle", "tools"):
@@ -44,12 +44,13 @@ def _worker(rank, world, port, W, H, rb, overlap, nframes, q):
     try:
         rows = vr_dist.shard_global_rows(H, rb, rank, world)
         sr = len(rows)
-        nbuf = 2 if overlap else 1
-        shards = [torch.zeros((sr, W, 4), dtype=torch.float32) for _ in range(nbuf)]
-        gbufs = [torch.zeros((world, sr, W, 4), dtype=torch.float32) for _ in range(nbuf)] if rank == 0 else None
+        slots = [vr_dist.Slot(torch.zeros((sr, W, 4), dtype=torch.float32),
+                              torch.zeros((world, sr, W, 4), dtype=torch.float32) if rank == 0 else None)
+                 for _ in range(inflight)]
         frames, state = [], {"k": 0, "samples": 0}
 
-        def render(buf):
+        def render(slot):
+            buf = slot.shard
             img, st = _scene(W, H, state["k"]).render_rows(rows[rows >= 0], nthreads=2)
             shard = np.zeros((sr, W, 4), np.float32)
             shard[rows >= 0] = img[rows[rows >= 0]]
@@ -57,10 +58,10 @@ def _worker(rank, world, port, W, H, rb, overlap, nframes, q):
             state["samples"] += st["samples"]
             state["k"] += 1
 
-        def assemble(g):
-            frames.append(vr_dist.assemble_numpy(g.numpy().copy(), H, rb, world))
+        def assemble(slot):
+            frames.append(vr_dist.assemble_numpy(slot.gbuf.numpy().copy(), H, rb, world))
 
-        pipe = vr_dist.FramePipeline(shards, gbufs, rank, world, dist, render, assemble, overlap=overlap)
+        pipe = vr_dist.FramePipeline(slots, rank, world, dist, render, assemble)
         for _ in range(nframes):
             pipe.step()
         pipe.drain()
@@ -72,16 +73,18 @@ def _worker(rank, world, port, W, H, rb, overlap, nframes, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,rb,overlap", [(2, 16, True), (2, 4, False), (3, 8, True)])
-def test_gloo_sharded_frames_match_single_process(world, rb, overlap):
-    """N ranks, 3 frames through vr_dist.FramePipeline (the benchmark's frame loop): every
-    assembled frame equals the single-process oracle frame bit for bit, with and without
-    the gather of frame k overlapped with the render of frame k+1."""
-    W, H, nframes = 40, 45, 3
+@pytest.mark.parametrize("world,rb,inflight,nframes",
+                         [(2, 16, 2, 3), (2, 4, 1, 3), (3, 8, 3, 5), (2, 8, 3, 2)])
+def test_gloo_sharded_frames_match_single_process(world, rb, inflight, nframes):
+    """N ranks, several frames through vr_dist.FramePipeline (the benchmark's frame loop):
+    every assembled frame equals the single-process oracle frame bit for bit, in order,
+    serial (1 frame in flight) and with 2-3 frames in flight (gathers waited for only when
+    their slot comes round again; fewer frames than slots too)."""
+    W, H = 40, 45
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, rb, overlap, nframes, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, rb, inflight, nframes, q))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -50,14 +50,22 @@ struct vr_ctx {
     bool grad_valid = false;
     // adaptive tile order (tile_order 4): per launch geometry, the last launch's per-tile
     // durations and the workgroup -> tile permutation built from them
+    // Keyed by the launch stream too: frames in flight on different streams each own their
+    // duration/permutation buffers, so one stream's order kernel never rewrites a permutation
+    // another stream's march kernel is reading.
     struct TileSched {
         uint32_t tiles_x = 0, tiles_y = 0, supers_x = 0, per_xcd = 0;
         int pair = 0;
+        void *stream = nullptr;
         uint32_t *cost = nullptr, *perm = nullptr, *lists = nullptr;
         bool have_perm = false;
         uint32_t launches = 0;
     };
     std::vector<TileSched> sched;
+    // lazily built derived fields (gradient, skip-empty) are produced on the stream of the
+    // frame that first needs them; frames on other streams wait for this event
+    hipEvent_t built_ev = nullptr;
+    bool built_recorded = false;
     // scratch
     unsigned long long *counters = nullptr;
     void *frame_dev = nullptr;
@@ -340,6 +348,8 @@ int check_params(vr_ctx *c, const vr_params *p)
         return fail(c, VR_EINVAL, "params.ray_dist must be finite and >= 0");
     if (p->spec_power < 0 || p->spec_power > 256)
         return fail(c, VR_EINVAL, "params.spec_power must be in [0, 256]");
+    if (p->frames_in_flight < 0 || p->frames_in_flight > 16)
+        return fail(c, VR_EINVAL, "params.frames_in_flight must be in [0, 16]");
     const float n = p->ray_dist / p->step;
     if (n > 1.0e8f) return fail(c, VR_EINVAL, "params.ray_dist / step too large");
     return VR_OK;
@@ -363,12 +373,17 @@ bool use_pipeline(bool shading, uint32_t tiles, size_t volume_bytes)
 // kPairMaxWaves single-lane wavefronts -- a rank's share of a multi-GPU frame, small frames:
 // twice the wavefronts, half of each ray's serial chain per lane.  Measured on the C3 rank
 // share: N = 8 0.190 -> 0.153 ms, N = 4 0.270 -> 0.227 ms; the full frame and unshaded shares
-// stay faster single-lane (tools/shard_sweep.py, profiles/r01/multi_gpu/).  Not for
+// stay faster single-lane (tools/shard_sweep.py, profiles/r01/multi_gpu/).  Serial frames
+// only (vr_params.frames_in_flight <= 1).  Not for
 // skip-empty frames or TFs beyond the LDS copy.  VR_PAIR=0/1 overrides (A/B).
 bool use_pair(const MarchParams &P, const vr_params *p)
 {
     if (p->skip_empty || P.tf_n > 256) return false;
     if (const char *e = std::getenv("VR_PAIR")) return e[0] == '1';
+    // frames overlapping on the device: the next frame hides this one's tail, so throughput
+    // per sample decides and the single-lane kernel wins (N = 8 C3 share with 3 frames in
+    // flight: 0.070 against 0.107 ms per frame, tools/inflight_sweep.py)
+    if (p->frames_in_flight >= 2) return false;
     return p->shading && P.tiles_x * P.tiles_y * (kThreadsPerTile / 64) < kPairMaxWaves;
 }
 
@@ -509,13 +524,38 @@ void ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s)
     P.grad = c->grad;
 }
 
+// The derived fields a frame reads (skip-empty classification, gradient field), built on `s`
+// when stale.  A frame on another stream may follow before that build has run: every frame
+// waits on the event recorded after the last build (a no-op once it has completed).
+int ensure_derived(vr_ctx *c, const vr_params *p, MarchParams &P, hipStream_t s)
+{
+    const bool r0 = c->range_valid, d0 = c->dist_valid, g0 = c->grad_valid;
+    if (p->skip_empty) {
+        int rc = ensure_skip(c, P, s);
+        if (rc) return rc;
+    }
+    if (p->shading) ensure_grad(c, P, s);
+    const bool built = (!r0 && c->range_valid) || (!d0 && c->dist_valid) || (!g0 && c->grad_valid);
+    if (built) {
+        if (!c->built_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->built_ev, hipEventDisableTiming),
+                                  "hipEventCreate");
+        HIP_TRY(c, hipEventRecord(c->built_ev, s), "hipEventRecord(build)");
+        c->built_recorded = true;
+    } else if (c->built_recorded) {
+        HIP_TRY(c, hipStreamWaitEvent(s, c->built_ev, 0), "hipStreamWaitEvent(build)");
+    }
+    return VR_OK;
+}
+
 // Adaptive tile order (tile_order 4): the schedule entry of this launch geometry (created on
-// first use, at most 8 kept); sets P.tile_cost, and P.tile_perm once a permutation exists.
-vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P)
+// first use, at most 16 kept, one per
+// geometry and stream); sets P.tile_cost, and P.tile_perm once a permutation exists.
+vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P, void *stream)
 {
     if (P.tile_order != 4) return nullptr;
     for (auto &t : c->sched)
-        if (t.tiles_x == P.tiles_x && t.tiles_y == P.tiles_y && t.pair == P.pair) {
+        if (t.tiles_x == P.tiles_x && t.tiles_y == P.tiles_y && t.pair == P.pair &&
+            t.stream == stream) {
             P.tile_cost = t.cost;
             if (t.have_perm) {
                 P.tile_perm = t.perm;
@@ -523,7 +563,7 @@ vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P)
             }
             return &t;
         }
-    if (c->sched.size() >= 8) {
+    if (c->sched.size() >= 16) {
         hipFree(c->sched.front().cost);
         hipFree(c->sched.front().perm);
         hipFree(c->sched.front().lists);
@@ -534,6 +574,7 @@ vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P)
     t.tiles_y = P.tiles_y;
     t.supers_x = P.supers_x;
     t.pair = P.pair;
+    t.stream = stream;
     // per-XCD tile lists (tile_order 3's super-tile assignment), padded with ~0
     std::vector<std::vector<uint32_t>> xl(8);
     for (uint32_t ty = 0; ty < P.tiles_y; ++ty)
@@ -652,6 +693,7 @@ void vr_destroy(vr_ctx *c)
         hipEventDestroy(pr.second);
     }
     for (auto e : c->ev_pool) hipEventDestroy(e);
+    if (c->built_ev) hipEventDestroy(c->built_ev);
     if (c->bricks) hipFree(c->bricks);
     if (c->tf) hipFree(c->tf);
     if (c->tf_nz) hipFree(c->tf_nz);
@@ -682,6 +724,13 @@ int vr_get_size(const vr_ctx *c, uint32_t *w, uint32_t *h)
     if (!c || !w || !h) return fail(nullptr, VR_EINVAL, "NULL argument");
     *w = c->width;
     *h = c->height;
+    return VR_OK;
+}
+
+int vr_get_device(const vr_ctx *c, int *device)
+{
+    if (!c || !device) return fail(nullptr, VR_EINVAL, "NULL argument");
+    *device = c->device;
     return VR_OK;
 }
 
@@ -906,11 +955,8 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (p->skip_empty) {
-        rc = ensure_skip(c, P, s);
-        if (rc) return rc;
-    }
-    if (p->shading) ensure_grad(c, P, s);
+    rc = ensure_derived(c, p, P, s);
+    if (rc) return rc;
     if (use_pair(P, p)) {  // L lanes per ray on 16 x (16 / L) tiles (march_pair_kernel)
         // 4 lanes below kPairQuadMaxWaves (N = 8 C3 share: 0.151 -> 0.144 ms), else 2
         P.pair = P.tiles_x * P.tiles_y * (kThreadsPerTile / 64) < kPairQuadMaxWaves ? 4 : 2;
@@ -919,7 +965,7 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
         P.tiles_y = (P.local_rows + th - 1) / th;
         P.supers_total = P.supers_x * ((P.tiles_y + 3) / 4);
     }
-    vr_ctx::TileSched *ts = tile_sched(c, P);
+    vr_ctx::TileSched *ts = tile_sched(c, P, stream);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing) {
         e0 = pooled_event(c);
@@ -995,11 +1041,8 @@ int vr_count_work(vr_ctx *c, const vr_camera *cam, const vr_params *p, uint32_t 
     MarchParams P;
     int rc = build_params(c, cam, p, c->frame_dev, VR_OUT_RGBA8, row_block, rank, nranks, P);
     if (rc) return rc;
-    if (p->skip_empty) {
-        rc = ensure_skip(c, P, nullptr);
-        if (rc) return rc;
-    }
-    if (p->shading) ensure_grad(c, P, nullptr);
+    rc = ensure_derived(c, p, P, nullptr);
+    if (rc) return rc;
     HIP_TRY(c, hipMemset(c->counters, 0, 8 * sizeof(unsigned long long)), "hipMemset(counters)");
     HIP_TRY(c, launch_march(c->storage, p->shading != 0, true, P, nullptr), "march (count) launch");
     unsigned long long h[5];

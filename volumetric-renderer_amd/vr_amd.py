@@ -47,7 +47,7 @@ class vr_params(C.Structure):
                 ("ambient", C.c_float), ("diffuse", C.c_float), ("specular", C.c_float),
                 ("spec_power", C.c_int32), ("tile_order", C.c_int32),
                 ("skip_empty", C.c_int32), ("wave_shape", C.c_int32),
-                ("reserved", C.c_int32 * 1)]
+                ("frames_in_flight", C.c_int32)]
 
 
 class vr_stats(C.Structure):
@@ -69,7 +69,7 @@ class vr_dataset(C.Structure):
 # Every entry point include/vr/vr.h and include/vr/vr_host.h declare (checked by the CPU tests).
 ABI_SYMBOLS = [
     "vr_abi_version", "vr_params_default", "vr_create", "vr_destroy", "vr_last_error",
-    "vr_resize", "vr_get_size", "vr_set_volume", "vr_set_volume_device", "vr_generate_volume",
+    "vr_resize", "vr_get_size", "vr_get_device", "vr_set_volume", "vr_set_volume_device", "vr_generate_volume",
     "vr_volume_bytes", "vr_debug_read_volume", "vr_debug_volume_info",
     "vr_set_transfer_function", "vr_set_slicing", "vr_render", "vr_render_device",
     "vr_shard_rows", "vr_assemble_rows", "vr_count_work", "vr_timing_enable",
@@ -85,7 +85,13 @@ HOST_SYMBOLS = [
     "vr_csv_load", "vr_dataset_free", "vr_host_last_error",
 ]
 
-ABI_VERSION = 2  # include/vr/vr.h VR_ABI_VERSION
+DIST_SYMBOLS = [
+    "vr_dist_unique_id", "vr_dist_create", "vr_dist_render", "vr_dist_synchronize",
+    "vr_dist_last_error", "vr_dist_destroy",
+]
+DIST_ID_BYTES = 128  # include/vr/vr_dist.h VR_DIST_ID_BYTES
+
+ABI_VERSION = 3  # include/vr/vr.h VR_ABI_VERSION
 _LIB = None
 
 
@@ -107,6 +113,13 @@ def lib() -> C.CDLL:
         "vr_last_error": (C.c_char_p, [vp]),
         "vr_resize": (i32, [vp, u32, u32]),
         "vr_get_size": (i32, [vp, C.POINTER(u32), C.POINTER(u32)]),
+        "vr_get_device": (i32, [vp, C.POINTER(i32)]),
+        "vr_dist_unique_id": (i32, [vp]),
+        "vr_dist_create": (vp, [vp, vp, i32, i32, u32, i32]),
+        "vr_dist_render": (i32, [vp, C.POINTER(vr_camera), C.POINTER(vr_params), vp, vp]),
+        "vr_dist_synchronize": (i32, [vp]),
+        "vr_dist_last_error": (C.c_char_p, [vp]),
+        "vr_dist_destroy": (None, [vp]),
         "vr_set_volume": (i32, [vp, vp, i32, u32, u32, u32, f32, f32]),
         "vr_set_volume_device": (i32, [vp, vp, i32, u32, u32, u32, f32, f32, vp]),
         "vr_generate_volume": (i32, [vp, i32, i32, u32, u32, u32, u32, C.POINTER(f32), C.POINTER(f32)]),
@@ -331,7 +344,10 @@ class OffscreenPass:
             self._ctx = None
 
     def __del__(self):
-        self.close()
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown: module globals may already be gone
+            pass
 
     def _check(self, rc: int, what: str):
         if rc != 0:
@@ -445,6 +461,59 @@ class OffscreenPass:
 
     def kernel_name(self, params) -> str:
         return lib().vr_kernel_name(self._ctx, C.byref(params)).decode()
+
+
+def dist_unique_id() -> bytes:
+    """Rank 0: a fresh RCCL communicator id (vr_dist_unique_id) to send to every rank."""
+    buf = C.create_string_buffer(DIST_ID_BYTES)
+    rc = lib().vr_dist_unique_id(buf)
+    if rc:
+        raise RuntimeError(f"vr_dist_unique_id failed ({rc}): {lib().vr_dist_last_error(None).decode()}")
+    return buf.raw
+
+
+class DistFrames:
+    """Multi-GPU frames of one OffscreenPass over RCCL (include/vr/vr_dist.h): this rank's
+    row blocks -> ncclGather to rank 0 -> de-interleave there, all stream-ordered, with
+    `frames_in_flight` frames in flight.  Every rank constructs it together (it blocks until
+    all `nranks` have joined) with the same communicator id."""
+
+    def __init__(self, rp: "OffscreenPass", uid: bytes, nranks: int, rank: int,
+                 row_block: int = 8, frames_in_flight: int = 3):
+        if len(uid) != DIST_ID_BYTES:
+            raise ValueError("communicator id must be DIST_ID_BYTES bytes")
+        self.rank, self.nranks = rank, nranks
+        self._rp = rp  # keeps the context alive
+        self._d = lib().vr_dist_create(rp._ctx, C.create_string_buffer(uid, DIST_ID_BYTES),
+                                       nranks, rank, row_block, frames_in_flight)
+        if not self._d:
+            raise RuntimeError(f"vr_dist_create failed: {lib().vr_dist_last_error(None).decode()}")
+
+    def _check(self, rc: int, what: str):
+        if rc:
+            raise RuntimeError(f"{what} failed ({rc}): {lib().vr_dist_last_error(self._d).decode()}")
+
+    def render(self, camera, params, frame_ptr: int = 0, stream: int = 0):
+        """Enqueue one frame; rank 0's RGBA8 frame (H x W x 4 bytes at frame_ptr) is complete
+        once `stream` passes this point."""
+        cam = camera.to_vr_camera() if isinstance(camera, OrbitCamera) else camera
+        self._check(lib().vr_dist_render(self._d, C.byref(cam), C.byref(params),
+                                         C.c_void_p(frame_ptr or None), C.c_void_p(stream or None)),
+                    "vr_dist_render")
+
+    def synchronize(self):
+        self._check(lib().vr_dist_synchronize(self._d), "vr_dist_synchronize")
+
+    def close(self):
+        if getattr(self, "_d", None):
+            lib().vr_dist_destroy(self._d)
+            self._d = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def shard_rows(height: int, row_block: int, nranks: int) -> int:

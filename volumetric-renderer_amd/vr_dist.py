@@ -42,69 +42,93 @@ def gather_to_root(local, gathered_views, rank: int, dist, async_op: bool = Fals
     return dist.gather(local, gathered_views if rank == 0 else None, dst=0, async_op=async_op)
 
 
-class FramePipeline:
-    """Per-frame render -> gather -> assemble with the gather of frame k overlapped with the
-    render of frame k+1 (double-buffered shards and gather buffers).
+class Slot:
+    """One frame in flight: this rank's shard buffer, rank 0's rank-major gather buffer and
+    assembled frame, and the stream the frame's work is enqueued on (None on CPU)."""
 
-    `render(buf)` enqueues this rank's shard of the next frame into `buf`; `assemble(gbuf)`
-    (rank 0) enqueues the de-interleave of a gathered rank-major buffer.  With overlap, the
-    gather is issued async_op=True and only waited for (work.wait(): a stream wait for
-    NCCL/RCCL, a host wait for gloo) one frame later, right before that frame is assembled
-    and before its shard buffer is rendered into again.  overlap=False is the serial form.
+    def __init__(self, shard, gbuf=None, frame=None, stream=None):
+        self.shard, self.gbuf, self.frame, self.stream = shard, gbuf, frame, stream
+        self.work = None  # the gather of the frame last rendered in this slot
+
+
+class FramePipeline:
+    """Per-frame render -> gather -> assemble with F = len(slots) frames in flight.
+
+    Frame i uses slot i mod F: `render(slot)` enqueues this rank's shard of the frame into
+    slot.shard on slot.stream, the gather to rank 0 is issued from that stream
+    (async_op=True; RCCL orders it after the render), and `assemble(slot)` (rank 0)
+    de-interleaves slot.gbuf into slot.frame.  The gather is only waited for (work.wait():
+    a stream wait for NCCL/RCCL, a host wait for gloo) when the slot comes round again, F
+    frames later, right before its assembly and before its buffers are rendered into again.
+    So with F >= 2 frame k+1..k+F-1 render while frame k's gather is on the wire, and the
+    frames' kernels overlap on the device (the reference keeps MAX_FRAMES_IN_FLIGHT = 2,
+    vulkan_context.h:17).  F = 1 is the serial form: each gather is waited for and its
+    frame assembled before the next render.
     """
 
-    def __init__(self, shards, gather_bufs, rank, world, dist, render, assemble, overlap=True,
-                 host_staging=False):
-        self.shards = shards            # list of 1 or 2 local shard tensors
-        self.gather_bufs = gather_bufs  # rank 0: list of (world, rows, W) tensors, else None
+    def __init__(self, slots, rank, world, dist, render, assemble, host_staging=False):
+        self.slots = list(slots)
         self.rank, self.world, self.dist = rank, world, dist
         self.render, self.assemble = render, assemble
         # host_staging: device shards gathered through host copies (gloo rehearsal of the
-        # multi-GPU path on one device); always serial
+        # multi-GPU path on ranks sharing one device); always serial
         self.host_staging = host_staging
-        self.overlap = overlap and world > 1 and len(shards) > 1 and not host_staging
         self.k = 0
-        self.pending = None
+        self.order = []  # slots with a gather outstanding, oldest first
 
-    def _views(self, i):
+    @property
+    def last(self):
+        """The slot of the most recently issued frame."""
+        return self.slots[(self.k - 1) % len(self.slots)]
+
+    def _ctx(self, slot):
+        import contextlib
+        if slot.stream is None:
+            return contextlib.nullcontext()
+        import torch
+        return torch.cuda.stream(slot.stream)
+
+    def _views(self, slot):
         if self.rank != 0:
             return None
-        g = self.gather_bufs[i]
-        return [g[r] for r in range(self.world)]
+        return [slot.gbuf[r] for r in range(self.world)]
 
-    def _finish(self, work, i):
-        work.wait()
+    def _finish(self, slot):
+        # called with slot.stream current: the wait orders this stream after the gather
+        slot.work.wait()
+        slot.work = None
+        self.order.remove(slot)
         if self.rank == 0:
-            self.assemble(self.gather_bufs[i])
+            self.assemble(slot)
 
     def step(self):
-        i = self.k % len(self.shards)
+        slot = self.slots[self.k % len(self.slots)]
         self.k += 1
-        buf = self.shards[i]
-        self.render(buf)
-        if self.world == 1:
-            return
-        gi = i % len(self.gather_bufs) if self.rank == 0 else 0
-        if self.host_staging:
-            host = buf.cpu()
-            hviews = None
-            if self.rank == 0:
-                hg = self.gather_bufs[gi].cpu()
-                hviews = [hg[r] for r in range(self.world)]
-            gather_to_root(host, hviews, self.rank, self.dist)
-            if self.rank == 0:
-                self.gather_bufs[gi].copy_(hg)
-                self.assemble(self.gather_bufs[gi])
-            return
-        work = gather_to_root(buf, self._views(gi), self.rank, self.dist, async_op=True)
-        if not self.overlap:
-            self._finish(work, gi)
-            return
-        if self.pending is not None:
-            self._finish(*self.pending)
-        self.pending = (work, gi)
+        with self._ctx(slot):
+            if slot.work is not None:
+                self._finish(slot)
+            self.render(slot)
+            if self.world == 1:
+                return
+            if self.host_staging:
+                host = slot.shard.cpu()
+                hviews = None
+                if self.rank == 0:
+                    hg = slot.gbuf.cpu()
+                    hviews = [hg[r] for r in range(self.world)]
+                gather_to_root(host, hviews, self.rank, self.dist)
+                if self.rank == 0:
+                    slot.gbuf.copy_(hg)
+                    self.assemble(slot)
+                return
+            slot.work = gather_to_root(slot.shard, self._views(slot), self.rank, self.dist,
+                                       async_op=True)
+            self.order.append(slot)
+            if len(self.slots) == 1:
+                self._finish(slot)
 
     def drain(self):
-        if self.pending is not None:
-            self._finish(*self.pending)
-            self.pending = None
+        while self.order:
+            slot = self.order[0]
+            with self._ctx(slot):
+                self._finish(slot)
