@@ -83,6 +83,11 @@ def setup_pass(cfg, device):
 _DIST = {}
 
 
+def set_gather(kind):
+    global GATHER
+    GATHER = kind
+
+
 def dist_frames(rp, rank, world, row_block, inflight):
     """One RCCL communicator per frames-in-flight setting (vr_dist_create), id from rank 0
     broadcast over the torch.distributed process group."""
@@ -145,10 +150,16 @@ def run_variant(rp, cfg, steps, warmup, rank, world, inflight, row_block=8):
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     frame_stats = dict(zip(keys, [int(x) for x in tot.tolist()]))
 
+    pipe = None
     if world > 1 and BACKEND == "nccl" and GATHER == "native":
         # the whole frame in the library: render -> ncclGather -> assemble, stream-ordered
-        pipe = NativeFrames(dist_frames(rp, rank, world, row_block, inflight), cam, p, rank, H, W)
-    else:
+        try:
+            pipe = NativeFrames(dist_frames(rp, rank, world, row_block, inflight), cam, p, rank, H, W)
+        except RuntimeError as e:  # e.g. librccl.so.1 not loadable: same on every rank
+            print(f"bench: native RCCL frame path unavailable ({e}); using torch.distributed.gather",
+                  file=sys.stderr, flush=True)
+            set_gather("torch")
+    if pipe is None:
         pipe = vr_dist.FramePipeline(
             slots, rank, world, dist,
             render=lambda sl: rp.render_device(cam, p, sl.shard.data_ptr(), vr_amd.OUT_RGBA8,
@@ -382,6 +393,8 @@ def main():
                 "traffic": traffic,
                 "traffic_frac": (round(traffic / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                                  if traffic else None),
+                "traffic_frac_per_frame_period": (round(traffic / (secs / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
+                                                  if traffic else None),
                 "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"
                                   if traffic else None,
                 "kernel_ms": round(kms, 4),
