@@ -17,7 +17,7 @@ i=0
 while read -r GROUP; do
   [ -z "$GROUP" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $GROUP -d "$OUT/p$i" -o run --output-format csv \
+  timeout -s KILL ${PASS_TIMEOUT:-90} rocprofv3 --kernel-trace --pmc $GROUP -d "$OUT/p$i" -o run --output-format csv \
       -- python3 tools/prof_run.py $ARGS > "$OUT/p$i.log" 2>&1 < /dev/null
   rc=$?
   echo "pass $i [$GROUP] rc=$rc" >> "$OUT/passes.txt"

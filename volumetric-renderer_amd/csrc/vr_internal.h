@@ -25,6 +25,12 @@ namespace vr {
 #define VR_BRICK_SHIFT 3  // 8^3 bricks (experiment builds may use 4: 16^3)
 #endif
 constexpr int kBrickShift = VR_BRICK_SHIFT;
+// VR_F32_PLAIN=1 (experiment builds): f32 elements hold one voxel (no z-pair duplication);
+// a sample is then 4 x 8-B loads (elements x, x+1 of the rows (y|y+1, z|z+1)).
+#ifndef VR_F32_PLAIN
+#define VR_F32_PLAIN 0
+#endif
+constexpr size_t kF32VoxelsPerElement = VR_F32_PLAIN ? 1 : 2;
 constexpr int kBrick = 1 << kBrickShift;
 constexpr int kStore = kBrick + 1;
 constexpr int kBrickElems = kStore * kStore * kStore;  // 729
@@ -47,7 +53,7 @@ inline size_t storage_size(int st)
         default: return 4;
     }
 }
-inline size_t voxels_per_element(int st) { return st == ST_F32 ? 2 : 4; }
+inline size_t voxels_per_element(int st) { return st == ST_F32 ? kF32VoxelsPerElement : 4; }
 inline size_t element_size(int st) { return storage_size(st) * voxels_per_element(st); }
 
 // ---- Kernel parameters (one frame) -------------------------------------------------------

@@ -53,7 +53,7 @@ template <typename VT>
 constexpr bool kZPair = std::is_same<VT, float>::value;
 // bytes per element; 32-bit words per element (quad layouts)
 template <typename VT>
-constexpr int kElemBytes = kZPair<VT> ? 8 : 4 * (int)sizeof(VT);
+constexpr int kElemBytes = kZPair<VT> ? 4 * (int)kF32VoxelsPerElement : 4 * (int)sizeof(VT);
 template <typename VT>
 constexpr int kQuadWords = sizeof(VT) == 1 ? 1 : 2;
 
@@ -158,7 +158,15 @@ struct Cell8 {
     float v[8];  // index dx + 2 dy + 4 dz
     __device__ __forceinline__ void load(const char *__restrict__ base, size_t e)
     {
-        if constexpr (kZPair<VT>) {
+        if constexpr (kZPair<VT> && VR_F32_PLAIN) {  // rows (y, z), (y+1, z), (y, z+1), (y+1, z+1)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const f2a q = *reinterpret_cast<const f2a *>(
+                    base + (e + (size_t)((r & 1) * kStore + (r >> 1) * kStore * kStore)) * 4);
+                v[2 * r] = q.x;
+                v[2 * r + 1] = q.y;
+            }
+        } else if constexpr (kZPair<VT>) {
             const f4a r0 = zpair_load2(base, e);
             const f4a r1 = zpair_load2(base, e + kStore);
             v[0] = r0.x;
@@ -228,7 +236,39 @@ __device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e
     const long dzm = lz > 0 ? -S2 : (L * S2 - bz_stride);
     const float *v = c.v;
     float Dx[8], Dy[8], Dz[8];
-    if constexpr (kZPair<VT>) {
+    if constexpr (kZPair<VT> && VR_F32_PLAIN) {
+        const long dyp = ly < L ? 2 * S : (by_stride - (L - 1) * S);
+        const long dzp = lz < L ? 2 * S2 : (bz_stride - (L - 1) * S2);
+        auto ld1 = [&](long o) { return *reinterpret_cast<const float *>(base + (e + o) * 4); };
+        auto ld2 = [&](long o) { return *reinterpret_cast<const f2a *>(base + (e + o) * 4); };
+#pragma unroll
+        for (int dz_ = 0; dz_ < 2; ++dz_)
+#pragma unroll
+            for (int dy_ = 0; dy_ < 2; ++dy_) {
+                const int o = 2 * dy_ + 4 * dz_;
+                const long r = dy_ * S + dz_ * S2;
+                Dx[o] = v[o + 1] - ld1(dxm + r);
+                Dx[o + 1] = ld1(dxp + r) - v[o];
+            }
+#pragma unroll
+        for (int dz_ = 0; dz_ < 2; ++dz_) {
+            const f2a m = ld2(dym + dz_ * S2), q = ld2(dyp + dz_ * S2);
+            const int o = 4 * dz_;
+            Dy[o] = v[o + 2] - m.x;
+            Dy[o + 1] = v[o + 3] - m.y;
+            Dy[o + 2] = q.x - v[o];
+            Dy[o + 3] = q.y - v[o + 1];
+        }
+#pragma unroll
+        for (int dy_ = 0; dy_ < 2; ++dy_) {
+            const f2a m = ld2(dzm + dy_ * S), q = ld2(dzp + dy_ * S);
+            const int o = 2 * dy_;
+            Dz[o] = v[o + 4] - m.x;
+            Dz[o + 1] = v[o + 5] - m.y;
+            Dz[o + 4] = q.x - v[o];
+            Dz[o + 5] = q.y - v[o + 1];
+        }
+    } else if constexpr (kZPair<VT>) {
         const long dyp = ly < L ? 2 * S : (by_stride - (L - 1) * S);
         // z-pairs (.x = z, .y = z + 1) of the x - 1 and x + 2 columns, rows y and y + 1
         const f2a xm0 = zpair_load1(base, e + dxm), xm1 = zpair_load1(base, e + dxm + S);
@@ -1051,7 +1091,9 @@ __global__ __launch_bounds__(256) void brick_kernel(const SrcT *__restrict__ src
                 return (DstT)0;
             return (DstT)src[(size_t)xx + (size_t)nx * ((size_t)yy + (size_t)ny * (size_t)zz)];
         };
-        if constexpr (zpair) {
+        if constexpr (zpair && VR_F32_PLAIN) {
+            dst[g] = at(x, y, z);
+        } else if constexpr (zpair) {
             dst[2 * g + 0] = at(x, y, z);
             dst[2 * g + 1] = at(x, y, z + 1);
         } else {
@@ -1155,7 +1197,7 @@ __device__ __forceinline__ float padded_voxel(const float *__restrict__ bricks, 
     if (px < kPad || py < kPad || pz < kPad || px >= (int)nx + kPad || py >= (int)ny + kPad ||
         pz >= (int)nz + kPad)
         return 0.0f;
-    return bricks[2 * cell_offset(px, py, pz, nbx, nby)];
+    return bricks[kF32VoxelsPerElement * cell_offset(px, py, pz, nbx, nby)];
 }
 
 // One thread per stored element: D_e(p) = v(p + e) - v(p - e) (the oracle's dvox) for the
