@@ -1067,8 +1067,8 @@ __global__ __launch_bounds__(256) void order_tiles_kernel(const uint32_t *__rest
 
 // ---- volume ingest: linear (any NRRD element type) -> bricked paired elements -------------
 
-// One thread per stored element: padded element coordinates -> the 2 (z-pair) or 4 (yz-quad)
-// voxels it holds, 0 outside the logical volume (border).
+// One thread per stored element: padded element coordinates -> the voxels it holds (2 z-pair,
+// 4 yz-quad), 0 outside the logical volume (border).
 template <typename SrcT, typename DstT>
 __global__ __launch_bounds__(256) void brick_kernel(const SrcT *__restrict__ src,
                                                     DstT *__restrict__ dst, uint32_t nx,
@@ -1076,10 +1076,13 @@ __global__ __launch_bounds__(256) void brick_kernel(const SrcT *__restrict__ src
                                                     uint32_t nby, size_t total)
 {
     constexpr bool zpair = std::is_same<DstT, float>::value;
-    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
-         g += (size_t)gridDim.x * blockDim.x) {
-        const size_t bidx = g / kBrickElems;
-        const uint32_t l = (uint32_t)(g - bidx * kBrickElems);
+    // a workgroup per brick (grid-stride over bricks), its threads over the brick's elements:
+    // brick coordinates once per brick, element coordinates by constant divisors, and each
+    // brick's elements written contiguously
+    const size_t nbricks = total / kBrickElems;
+    for (size_t bidx = blockIdx.x; bidx < nbricks; bidx += gridDim.x)
+    for (uint32_t l = threadIdx.x; l < (uint32_t)kBrickElems; l += blockDim.x) {
+        const size_t g = bidx * kBrickElems + l;
         const uint32_t lx = l % kStore, lyz = l / kStore, lyy = lyz % kStore, lz = lyz / kStore;
         const uint32_t bx = (uint32_t)(bidx % nbx), byz = (uint32_t)(bidx / nbx);
         const uint32_t by = byz % nby, bz = byz / nby;
@@ -1091,16 +1094,21 @@ __global__ __launch_bounds__(256) void brick_kernel(const SrcT *__restrict__ src
                 return (DstT)0;
             return (DstT)src[(size_t)xx + (size_t)nx * ((size_t)yy + (size_t)ny * (size_t)zz)];
         };
+        // one store per element (a u8 quad is one dword, not four byte stores)
         if constexpr (zpair && VR_F32_PLAIN) {
             dst[g] = at(x, y, z);
         } else if constexpr (zpair) {
-            dst[2 * g + 0] = at(x, y, z);
-            dst[2 * g + 1] = at(x, y, z + 1);
+            reinterpret_cast<float2 *>(dst)[g] = make_float2(at(x, y, z), at(x, y, z + 1));
         } else {
-            dst[4 * g + 0] = at(x, y, z);
-            dst[4 * g + 1] = at(x, y, z + 1);
-            dst[4 * g + 2] = at(x, y + 1, z);
-            dst[4 * g + 3] = at(x, y + 1, z + 1);
+            struct alignas(4 * sizeof(DstT)) Quad {
+                DstT v[4];
+            };
+            Quad q;
+            q.v[0] = at(x, y, z);
+            q.v[1] = at(x, y, z + 1);
+            q.v[2] = at(x, y + 1, z);
+            q.v[3] = at(x, y + 1, z + 1);
+            reinterpret_cast<Quad *>(dst)[g] = q;
         }
     }
 }
@@ -1207,10 +1215,13 @@ __global__ __launch_bounds__(256) void grad_field_kernel(const float *__restrict
                                                          uint32_t ny, uint32_t nz, uint32_t nbx,
                                                          uint32_t nby, size_t total)
 {
-    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
-         g += (size_t)gridDim.x * blockDim.x) {
-        const size_t bidx = g / kBrickElems;
-        const uint32_t l = (uint32_t)(g - bidx * kBrickElems);
+    // a workgroup per brick (grid-stride over bricks), its threads over the brick's elements:
+    // brick coordinates once per brick, element coordinates by constant divisors, and each
+    // brick's elements written contiguously
+    const size_t nbricks = total / kBrickElems;
+    for (size_t bidx = blockIdx.x; bidx < nbricks; bidx += gridDim.x)
+    for (uint32_t l = threadIdx.x; l < (uint32_t)kBrickElems; l += blockDim.x) {
+        const size_t g = bidx * kBrickElems + l;
         const uint32_t lx = l % kStore, lyz = l / kStore, lyy = lyz % kStore, lz = lyz / kStore;
         const uint32_t bx = (uint32_t)(bidx % nbx), byz = (uint32_t)(bidx / nbx);
         const uint32_t by = byz % nby, bz = byz / nby;
@@ -1226,9 +1237,10 @@ __global__ __launch_bounds__(256) void grad_field_kernel(const float *__restrict
             out[2 + h] = V(0, 1, 0) - V(0, -1, 0);
             out[4 + h] = V(0, 0, 1) - V(0, 0, -1);
         }
-        float *o = grad + 6 * g;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) o[k] = out[k];
+        float2 *o = reinterpret_cast<float2 *>(grad) + 3 * g;  // 24-B element, 8-B aligned
+        o[0] = make_float2(out[0], out[1]);
+        o[1] = make_float2(out[2], out[3]);
+        o[2] = make_float2(out[4], out[5]);
     }
 }
 
@@ -1414,6 +1426,13 @@ hipError_t launch_march_vt(bool shade, bool count, const MarchParams &p, hipStre
                  : launch_march_t<VT, false, false, false>(p, s);
 }
 
+// workgroups for the per-brick kernels (brick_kernel, grad_field_kernel): one per brick
+inline unsigned grid_bricks(size_t total_elems)
+{
+    const size_t nb = total_elems / kBrickElems;
+    return (unsigned)(nb > 65536 ? 65536 : (nb == 0 ? 1 : nb));
+}
+
 inline unsigned grid_for(size_t total)
 {
     size_t g = (total + 255) / 256;
@@ -1428,11 +1447,11 @@ hipError_t brick_from(const void *src, void *dst, uint32_t nx, uint32_t ny, uint
     const size_t total = (size_t)nbx * nby * nbz * kBrickElems;  // elements
     const SrcT *sp = static_cast<const SrcT *>(src);
     switch (storage) {
-        case ST_U8: hipLaunchKernelGGL((brick_kernel<SrcT, uint8_t>), dim3(grid_for(total)), dim3(256), 0, s, sp, (uint8_t *)dst, nx, ny, nz, nbx, nby, total); break;
-        case ST_I8: hipLaunchKernelGGL((brick_kernel<SrcT, int8_t>), dim3(grid_for(total)), dim3(256), 0, s, sp, (int8_t *)dst, nx, ny, nz, nbx, nby, total); break;
-        case ST_U16: hipLaunchKernelGGL((brick_kernel<SrcT, uint16_t>), dim3(grid_for(total)), dim3(256), 0, s, sp, (uint16_t *)dst, nx, ny, nz, nbx, nby, total); break;
-        case ST_I16: hipLaunchKernelGGL((brick_kernel<SrcT, int16_t>), dim3(grid_for(total)), dim3(256), 0, s, sp, (int16_t *)dst, nx, ny, nz, nbx, nby, total); break;
-        default: hipLaunchKernelGGL((brick_kernel<SrcT, float>), dim3(grid_for(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
+        case ST_U8: hipLaunchKernelGGL((brick_kernel<SrcT, uint8_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (uint8_t *)dst, nx, ny, nz, nbx, nby, total); break;
+        case ST_I8: hipLaunchKernelGGL((brick_kernel<SrcT, int8_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (int8_t *)dst, nx, ny, nz, nbx, nby, total); break;
+        case ST_U16: hipLaunchKernelGGL((brick_kernel<SrcT, uint16_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (uint16_t *)dst, nx, ny, nz, nbx, nby, total); break;
+        case ST_I16: hipLaunchKernelGGL((brick_kernel<SrcT, int16_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (int16_t *)dst, nx, ny, nz, nbx, nby, total); break;
+        default: hipLaunchKernelGGL((brick_kernel<SrcT, float>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
     }
     return hipGetLastError();
 }
@@ -1553,7 +1572,7 @@ hipError_t launch_grad_field(const float *bricks, float *grad, uint32_t nx, uint
 {
     const uint32_t nbx = bricks_for(nx), nby = bricks_for(ny), nbz = bricks_for(nz);
     const size_t total = (size_t)nbx * nby * nbz * kBrickElems;
-    hipLaunchKernelGGL(grad_field_kernel, dim3(grid_for(total)), dim3(256), 0, s, bricks, grad,
+    hipLaunchKernelGGL(grad_field_kernel, dim3(grid_bricks(total)), dim3(256), 0, s, bricks, grad,
                        nx, ny, nz, nbx, nby, total);
     return hipGetLastError();
 }

@@ -407,38 +407,49 @@ size_t elem_size(int dtype)
     }
 }
 
+// std::min_element / std::max_element over static_cast<float> (nrrd_file_parser.cpp:39-40):
+// the first element, replaced by every later one that compares smaller (larger).  Integer
+// -> float conversion is monotone, so integers reduce in their own type (vectorised) and
+// convert once; floats compare as float in element order, so a NaN first element stays the
+// result and later NaNs never replace it, exactly as the reference.
 template <typename T>
-float as_float(const void *p, size_t i)
+void minmax_t(const void *data, size_t count, float &lo, float &hi)
 {
-    T v;
-    std::memcpy(&v, static_cast<const char *>(p) + i * sizeof(T), sizeof(T));
-    return static_cast<float>(v);
-}
-
-float elem_float(const void *data, int dtype, size_t i)
-{
-    switch (dtype) {
-        case VR_DTYPE_I8: return as_float<int8_t>(data, i);
-        case VR_DTYPE_U8: return as_float<uint8_t>(data, i);
-        case VR_DTYPE_I16: return as_float<int16_t>(data, i);
-        case VR_DTYPE_U16: return as_float<uint16_t>(data, i);
-        case VR_DTYPE_I32: return as_float<int32_t>(data, i);
-        case VR_DTYPE_U32: return as_float<uint32_t>(data, i);
-        case VR_DTYPE_I64: return as_float<int64_t>(data, i);
-        case VR_DTYPE_U64: return as_float<uint64_t>(data, i);
-        case VR_DTYPE_F32: return as_float<float>(data, i);
-        default: return as_float<double>(data, i);
+    const T *p = static_cast<const T *>(data);
+    if constexpr (std::is_integral_v<T>) {
+        T a = p[0], b = p[0];
+        for (size_t i = 1; i < count; ++i) {
+            a = p[i] < a ? p[i] : a;
+            b = b < p[i] ? p[i] : b;
+        }
+        lo = static_cast<float>(a);
+        hi = static_cast<float>(b);
+    } else {
+        float a = static_cast<float>(p[0]), b = a;
+        for (size_t i = 1; i < count; ++i) {
+            const float v = static_cast<float>(p[i]);
+            if (v < a) a = v;
+            if (b < v) b = v;
+        }
+        lo = a;
+        hi = b;
     }
 }
 
 void minmax(vr_dataset *d, size_t count)
 {
-    // std::min_element / std::max_element over static_cast<float> (nrrd_file_parser.cpp:39-40)
-    float lo = elem_float(d->data, d->dtype, 0), hi = lo;
-    for (size_t i = 1; i < count; ++i) {
-        const float v = elem_float(d->data, d->dtype, i);
-        if (v < lo) lo = v;
-        if (hi < v) hi = v;
+    float lo = 0.0f, hi = 0.0f;
+    switch (d->dtype) {
+        case VR_DTYPE_I8: minmax_t<int8_t>(d->data, count, lo, hi); break;
+        case VR_DTYPE_U8: minmax_t<uint8_t>(d->data, count, lo, hi); break;
+        case VR_DTYPE_I16: minmax_t<int16_t>(d->data, count, lo, hi); break;
+        case VR_DTYPE_U16: minmax_t<uint16_t>(d->data, count, lo, hi); break;
+        case VR_DTYPE_I32: minmax_t<int32_t>(d->data, count, lo, hi); break;
+        case VR_DTYPE_U32: minmax_t<uint32_t>(d->data, count, lo, hi); break;
+        case VR_DTYPE_I64: minmax_t<int64_t>(d->data, count, lo, hi); break;
+        case VR_DTYPE_U64: minmax_t<uint64_t>(d->data, count, lo, hi); break;
+        case VR_DTYPE_F32: minmax_t<float>(d->data, count, lo, hi); break;
+        default: minmax_t<double>(d->data, count, lo, hi); break;
     }
     d->vmin = lo;
     d->vmax = hi;
