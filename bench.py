@@ -344,6 +344,25 @@ def main():
             reference_equivalent_gsamples_per_s=round(
                 (f3["samples"] + f3["skipped_samples"]) * args.steps / s3 / 1e9, 3),
             samples_per_frame=f3["samples"], skipped_samples_per_frame=f3["skipped_samples"])
+    if not args.no_variants and world == 1:
+        # PCIe-inclusive: vr_render into (pageable) host memory, the drop-in record() path.
+        # The frame's RGBA8 bytes cross PCIe inside the timed region; row bands copy while
+        # the later bands render (vr_api.hip vr_render).  Never the headline value.
+        rp.transfer_function_changed(synth.TFS[cfg["tf"]]())
+        hcam = synth.camera(cfg["cam"]).to_vr_camera()
+        hp = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"])
+        hbuf = np.empty((cfg["H"], cfg["W"], 4), dtype=np.uint8)
+        for _ in range(min(args.warmup, 5)):
+            rp.render(hcam, hp, vr_amd.OUT_RGBA8, out=hbuf)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            rp.render(hcam, hp, vr_amd.OUT_RGBA8, out=hbuf)
+        sh = time.perf_counter() - t0
+        variants["host_output_pcie"] = dict(
+            fps=round(args.steps / sh, 2), ms_per_step=round(sh / args.steps * 1e3, 4),
+            gsamples_per_s=round(fstats["samples"] * args.steps / sh / 1e9, 3),
+            frame_bytes=int(hbuf.nbytes),
+            path="vr_render -> pageable host RGBA8 each frame (synchronous, as OffscreenPass::record + readback)")
 
     cpu = None
     small = int(np.prod(cfg["dims"])) <= 512 ** 3  # the oracle needs the volume as host floats

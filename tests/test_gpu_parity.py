@@ -498,3 +498,29 @@ def test_frames_in_flight_on_streams_are_identical(rp):
     bad = vr_amd.default_params(frames_in_flight=17)
     with pytest.raises(RuntimeError):
         rp.render(cam, bad)
+
+
+def test_host_render_row_bands_equal_device_frame(rp):
+    """vr_render (host output) renders frames of >= 256 rows as 4 row bands on two streams and
+    copies each band to the host while the later ones render.  Every frame equals the
+    single-launch device render byte for byte: RGBA8 and RGBA32F, shaded or not, skip-empty,
+    right after a volume/TF change (the first band builds the derived fields the others wait
+    for) and on repeated frames (per-band adaptive tile order)."""
+    import torch
+    cam = synth.camera("fill_oblique").to_vr_camera()
+    vol = synth.gaussians_numpy((41, 37, 45), seed=8).astype(np.float32)
+    for W, H in ((300, 257), (128, 512), (1920, 1080)):
+        rp.framebuffer_size_changed(W, H)
+        for shading, skip in ((0, 0), (1, 0), (1, 1)):
+            p = vr_amd.default_params(shading=shading, skip_empty=skip, ert_eps=1e-5)
+            rp.volume_dataset_changed(synth.dataset(vol))
+            rp.transfer_function_changed(synth.tf2())
+            for fmt, dt, ch in ((vr_amd.OUT_RGBA8, np.uint8, 1), (vr_amd.OUT_RGBA32F, np.float32, 4)):
+                frames = [rp.render(cam, p, fmt) for _ in range(3)]
+                dev = torch.empty((H, W * ch), dtype=torch.int32, device="cuda")
+                rp.render_device(cam, p, dev.data_ptr(), fmt, 16, 0, 1)
+                torch.cuda.synchronize()
+                ref = dev.cpu().numpy().view(dt).reshape(H, W, 4)
+                for i, f in enumerate(frames):
+                    assert f.shape == ref.shape
+                    assert np.array_equal(f.view(np.uint8), ref.view(np.uint8)), (W, H, shading, skip, fmt, i)

@@ -53,8 +53,11 @@ struct vr_ctx {
     // Keyed by the launch stream too: frames in flight on different streams each own their
     // duration/permutation buffers, so one stream's order kernel never rewrites a permutation
     // another stream's march kernel is reading.
+    // Keyed by the row shard as well: one stream may render several shares of a frame (the
+    // row bands of vr_render), each with its own tile durations.
     struct TileSched {
         uint32_t tiles_x = 0, tiles_y = 0, supers_x = 0, per_xcd = 0;
+        uint32_t row_block = 0, rank = 0, nranks = 0;
         int pair = 0;
         void *stream = nullptr;
         uint32_t *cost = nullptr, *perm = nullptr, *lists = nullptr;
@@ -70,6 +73,11 @@ struct vr_ctx {
     unsigned long long *counters = nullptr;
     void *frame_dev = nullptr;
     size_t frame_bytes = 0;
+    // vr_render (host output): row bands rendered on two streams while finished bands copy
+    // to the host on a third, so the PCIe copy hides behind the rest of the frame
+    hipStream_t band_stream[2] = {nullptr, nullptr};
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t band_ev[kHostBands] = {};
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
@@ -555,7 +563,8 @@ vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P, void *stream)
     if (P.tile_order != 4) return nullptr;
     for (auto &t : c->sched)
         if (t.tiles_x == P.tiles_x && t.tiles_y == P.tiles_y && t.pair == P.pair &&
-            t.stream == stream) {
+            t.stream == stream && t.row_block == P.row_block && t.rank == P.rank &&
+            t.nranks == P.nranks) {
             P.tile_cost = t.cost;
             if (t.have_perm) {
                 P.tile_perm = t.perm;
@@ -575,6 +584,9 @@ vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P, void *stream)
     t.supers_x = P.supers_x;
     t.pair = P.pair;
     t.stream = stream;
+    t.row_block = P.row_block;
+    t.rank = P.rank;
+    t.nranks = P.nranks;
     // per-XCD tile lists (tile_order 3's super-tile assignment), padded with ~0
     std::vector<std::vector<uint32_t>> xl(8);
     for (uint32_t ty = 0; ty < P.tiles_y; ++ty)
@@ -707,6 +719,11 @@ void vr_destroy(vr_ctx *c)
     }
     if (c->counters) hipFree(c->counters);
     if (c->frame_dev) hipFree(c->frame_dev);
+    for (auto e : c->band_ev)
+        if (e) hipEventDestroy(e);
+    for (auto st : c->band_stream)
+        if (st) hipStreamDestroy(st);
+    if (c->copy_stream) hipStreamDestroy(c->copy_stream);
     delete c;
 }
 
@@ -994,8 +1011,15 @@ int vr_render(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out, in
 {
     if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
     if (!out) return fail(c, VR_EINVAL, "output buffer is NULL");
+    if (!p) return fail(c, VR_EINVAL, "params is NULL");
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
-    const size_t bytes = (size_t)c->width * c->height * (out_format == VR_OUT_RGBA32F ? 16 : 4);
+    const size_t bpp = out_format == VR_OUT_RGBA32F ? 16 : 4;
+    const uint32_t W = c->width, H = c->height;
+    // kHostBands row bands of R rows (a multiple of the 16-row tile): band b is the row shard
+    // (row_block R, rank b, nranks kHostBands), rendered densely at rows [b R, b R + R)
+    const int nb = H >= kHostBandMinRows ? kHostBands : 1;
+    const uint32_t R = nb == 1 ? 16 : ((H + nb - 1) / nb + 15) / 16 * 16;
+    const size_t bytes = (size_t)W * (nb == 1 ? H : (size_t)R * nb) * bpp;
     if (c->frame_bytes < bytes) {
         if (c->frame_dev) hipFree(c->frame_dev);
         c->frame_dev = nullptr;
@@ -1003,9 +1027,45 @@ int vr_render(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out, in
         HIP_TRY(c, hipMalloc(&c->frame_dev, bytes), "hipMalloc(frame)");
         c->frame_bytes = bytes;
     }
-    int rc = vr_render_device(c, cam, p, c->frame_dev, out_format, 16, 0, 1, nullptr);
-    if (rc) return rc;
-    HIP_TRY(c, hipMemcpy(out, c->frame_dev, bytes, hipMemcpyDeviceToHost), "hipMemcpy(frame)");
+    if (nb == 1) {
+        int rc = vr_render_device(c, cam, p, c->frame_dev, out_format, 16, 0, 1, nullptr);
+        if (rc) return rc;
+        HIP_TRY(c, hipMemcpy(out, c->frame_dev, (size_t)W * H * bpp, hipMemcpyDeviceToHost),
+                "hipMemcpy(frame)");
+        return VR_OK;
+    }
+    if (!c->copy_stream) {
+        for (auto &s : c->band_stream)
+            HIP_TRY(c, hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate(band)");
+        HIP_TRY(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking),
+                "hipStreamCreate(copy)");
+        for (auto &e : c->band_ev)
+            HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate(band)");
+    }
+    // the bands overlap on two streams: the throughput kernels, not the latency-oriented lane
+    // groups (use_pair), as for frames in flight
+    vr_params pb = *p;
+    if (pb.frames_in_flight < 2) pb.frames_in_flight = 2;
+    for (int b = 0; b < nb; ++b) {
+        hipStream_t s = c->band_stream[b & 1];
+        int rc = vr_render_device(c, cam, &pb, static_cast<char *>(c->frame_dev) + (size_t)b * R * W * bpp,
+                                  out_format, R, (uint32_t)b, (uint32_t)nb, s);
+        if (rc) return rc;
+        HIP_TRY(c, hipEventRecord(c->band_ev[b], s), "hipEventRecord(band)");
+    }
+    // band b's copy starts as soon as it is rendered; a pageable destination makes each copy
+    // return once its bytes are in `out`, while the device renders the later bands
+    for (int b = 0; b < nb; ++b) {
+        const size_t row0 = (size_t)b * R;
+        if (row0 >= H) break;
+        const size_t rows = std::min<size_t>(R, H - row0);
+        HIP_TRY(c, hipStreamWaitEvent(c->copy_stream, c->band_ev[b], 0), "hipStreamWaitEvent(band)");
+        HIP_TRY(c, hipMemcpyAsync(static_cast<char *>(out) + row0 * W * bpp,
+                                  static_cast<char *>(c->frame_dev) + row0 * W * bpp,
+                                  rows * W * bpp, hipMemcpyDeviceToHost, c->copy_stream),
+                "hipMemcpyAsync(band)");
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->copy_stream), "hipStreamSynchronize(copy)");
     return VR_OK;
 }
 

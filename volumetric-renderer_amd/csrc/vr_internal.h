@@ -117,6 +117,9 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
 constexpr uint32_t kPipelineMaxWaves = 24576;  // between N = 2 (16 K) and N = 1 (33 K) at 1080p
 constexpr size_t kPipelineMinBytes = 4ull << 30;  // large volumes: always pipelined
 constexpr uint32_t kThreadsPerTile = 256;  // 16 x 16 pixels
+// vr_render (host output): row bands per frame, each copied to the host while later bands render
+constexpr int kHostBands = 4;
+constexpr uint32_t kHostBandMinRows = 256;  // shorter frames: one band
 // Adaptive tile order: from the per-tile durations of the last launch with the same tile
 // geometry, the next launch's workgroup -> tile permutation, longest first within each XCD's
 // super-tiles (as tile_order 3 assigns them).

@@ -414,15 +414,17 @@ class OffscreenPass:
 
     # -- record/render --
     def render(self, camera: OrbitCamera, params: Optional[vr_params] = None,
-               out_format: int = OUT_RGBA32F) -> np.ndarray:
-        """Synchronous full frame into host memory: (H, W, 4) float32 or uint8."""
+               out_format: int = OUT_RGBA32F, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """Synchronous full frame into host memory: (H, W, 4) float32 or uint8 (into `out`
+        when given, e.g. a buffer reused frame after frame)."""
         w, h = self.size
         p = params if params is not None else default_params()
         cam = camera.to_vr_camera() if isinstance(camera, OrbitCamera) else camera
-        if out_format == OUT_RGBA32F:
-            out = np.empty((h, w, 4), dtype=np.float32)
-        else:
-            out = np.empty((h, w, 4), dtype=np.uint8)
+        dt = np.float32 if out_format == OUT_RGBA32F else np.uint8
+        if out is None:
+            out = np.empty((h, w, 4), dtype=dt)
+        elif out.shape != (h, w, 4) or out.dtype != dt or not out.flags.c_contiguous:
+            raise ValueError(f"out must be a C-contiguous ({h}, {w}, 4) {np.dtype(dt).name} array")
         self._check(lib().vr_render(self._ctx, C.byref(cam), C.byref(p), out.ctypes.data, out_format),
                     "render")
         return out
