@@ -1,8 +1,9 @@
-"""Minimal profiling workload (no torch): one configuration, K frames through the C ABI.
+"""Minimal profiling workload: one configuration, K whole-frame launches through the C ABI.
 
 Used under rocprofv3 (--kernel-trace --stats, or one --pmc group per run) so that every
 counter pass replays a short process.  Prints the in-process HIP-event kernel time so the
-profile's per-dispatch durations can be matched.
+profile's per-dispatch durations can be matched.  Frames go to a device buffer in one launch
+each (vr_render_device): vr_render splits host-output frames into row bands.
   python tools/prof_run.py [--n 512] [--dtype float32] [--size 1920x1080] [--cam fill]
                            [--tf tf2] [--shading 1] [--ert 1e-5] [--frames 10] [--tile-order 0]
                            [--skip-empty 0]
@@ -43,10 +44,15 @@ def main():
     cam = synth.camera(a.cam).to_vr_camera()
     p = vr_amd.default_params(shading=a.shading, ert_eps=a.ert, tile_order=a.tile_order,
                               skip_empty=a.skip_empty, wave_shape=a.wave_shape)
-    rp.render(cam, p, vr_amd.OUT_RGBA8)
+    import torch
+    frame = torch.empty((H, W), dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    rp.render_device(cam, p, frame.data_ptr(), vr_amd.OUT_RGBA8, 16, 0, 1, s)
+    torch.cuda.synchronize()
     rp.timing_enable(True)
     for _ in range(a.frames):
-        rp.render(cam, p, vr_amd.OUT_RGBA8)
+        rp.render_device(cam, p, frame.data_ptr(), vr_amd.OUT_RGBA8, 16, 0, 1, s)
+    torch.cuda.synchronize()
     ms, n = rp.timing_read()
     st = rp.count_work(cam, p)
     print(json.dumps(dict(args=vars(a), kernel=rp.kernel_name(p), kernel_ms=ms / n, stats=st,
