@@ -159,6 +159,63 @@ def test_nrrd_roundtrip_writer(tmp_path):
             assert rc == 0 and np.array_equal(res["data"], a.astype(np.float32))
 
 
+def test_nrrd_large_raw_parallel_read_and_minmax(tmp_path):
+    """Raw payloads >= 64 MiB are read (pread) and reduced by chunks on up to 16 threads.  The
+    result must be the sequential one (nrrd_file_parser.cpp:39-40 min/max_element over floats):
+    a NaN first element stays, later NaNs never enter, equal values keep the first occurrence
+    (0.0 / -0.0), and a truncated payload still fails."""
+    n = 24 << 20  # 96 MiB of float32, 24 MiB of uint8 x 4
+    rng = np.random.default_rng(11)
+    u8 = rng.integers(3, 250, size=(96, 1024, 1024), dtype=np.uint8)
+    u8[95, 1023, 1023] = 255
+    u8[40, 7, 9] = 1
+    p = str(tmp_path / "u8.nhdr")
+    vr_amd.write_nrrd_raw(p, u8)
+    ds = vr_amd.load_nrrd(p)
+    assert np.array_equal(ds.data, u8) and (ds.vmin, ds.vmax) == (1.0, 255.0)
+
+    base = (rng.random(n, dtype=np.float32) + 1.0).reshape(96, 512, 512)
+    chunk = n // 16
+    cases = []
+    a = base.copy().ravel()
+    a[[chunk, 3 * chunk, n - 1]] = np.nan  # NaNs at chunk starts and the end
+    a[5 * chunk + 3] = 0.25
+    a[7 * chunk] = 7.5
+    cases.append((a, 0.25, 7.5, None))
+    a = base.copy().ravel()
+    a[0] = np.nan  # NaN first: both results NaN
+    cases.append((a, np.nan, np.nan, None))
+    a = base.copy().ravel()
+    a[5], a[9 * chunk + 1] = 0.0, -0.0  # first occurrence of the minimum wins
+    cases.append((a, 0.0, None, False))
+    a = base.copy().ravel()
+    a[2 * chunk + 17], a[9 * chunk] = -0.0, 0.0
+    cases.append((a, 0.0, None, True))
+    for i, (arr, lo, hi, signbit) in enumerate(cases):
+        p = str(tmp_path / f"f{i}.nhdr")
+        vr_amd.write_nrrd_raw(p, arr.reshape(96, 512, 512))
+        ds = vr_amd.load_nrrd(p)
+        assert np.array_equal(ds.data.view(np.uint32), arr.reshape(96, 512, 512).view(np.uint32))
+        if np.isnan(lo):
+            assert np.isnan(ds.vmin) and np.isnan(ds.vmax)
+            continue
+        assert ds.vmin == lo, i
+        if hi is not None:
+            assert ds.vmax == hi, i
+        if signbit is not None:
+            assert bool(np.signbit(np.float32(ds.vmin))) == signbit, i
+
+    # attached header + payload in one file, and a truncated payload
+    hdr = b"NRRD0004\ntype: uint8\ndimension: 3\nsizes: 1024 1024 96\nencoding: raw\n\n"
+    p = tmp_path / "att.nrrd"
+    p.write_bytes(hdr + u8.tobytes())
+    ds = vr_amd.load_nrrd(str(p))
+    assert np.array_equal(ds.data, u8) and (ds.vmin, ds.vmax) == (1.0, 255.0)
+    p.write_bytes(hdr + u8.tobytes()[:-1])
+    with pytest.raises(RuntimeError, match="Failed to read file"):
+        vr_amd.load_nrrd(str(p))
+
+
 def test_nrrd_missing_file():
     with pytest.raises(RuntimeError, match="Failed to read file"):
         vr_amd.load_nrrd("/nonexistent/file.nhdr")

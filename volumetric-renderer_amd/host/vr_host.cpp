@@ -16,7 +16,11 @@
 #include <sstream>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
+
+#include <fcntl.h>
+#include <unistd.h>
 
 namespace {
 
@@ -407,33 +411,100 @@ size_t elem_size(int dtype)
     }
 }
 
+// Large raw payloads are read and reduced by up to kIoThreads threads, each on its own
+// contiguous chunk (the page faults of the fresh buffer and the page-cache copy are the cost).
+constexpr size_t kParallelMinBytes = 64ull << 20;
+constexpr unsigned kIoThreads = 16;
+
+unsigned io_threads(size_t bytes)
+{
+    if (bytes < kParallelMinBytes) return 1;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    return (unsigned)std::min<size_t>({(size_t)kIoThreads, (size_t)hw, bytes / (16ull << 20)});
+}
+
+template <typename F>
+void parallel_chunks(size_t count, unsigned nt, F &&fn)  // fn(chunk, begin, end)
+{
+    if (nt <= 1) {
+        fn(0u, (size_t)0, count);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = (count + nt - 1) / nt;
+    for (unsigned t = 0; t < nt; ++t) {
+        const size_t b = std::min(count, (size_t)t * per), e = std::min(count, b + per);
+        th.emplace_back(fn, t, b, e);
+    }
+    for (auto &x : th) x.join();
+}
+
 // std::min_element / std::max_element over static_cast<float> (nrrd_file_parser.cpp:39-40):
 // the first element, replaced by every later one that compares smaller (larger).  Integer
 // -> float conversion is monotone, so integers reduce in their own type (vectorised) and
-// convert once; floats compare as float in element order, so a NaN first element stays the
-// result and later NaNs never replace it, exactly as the reference.
+// convert once.  Floats: each chunk reduces from +inf / -inf (a NaN never replaces), and the
+// chunk results fold into element 0 in chunk order with the same strict compare -- the
+// sequential result exactly: a NaN first element stays the result, later NaNs never enter,
+// and among equal values (0.0 / -0.0) the first occurrence wins.
 template <typename T>
 void minmax_t(const void *data, size_t count, float &lo, float &hi)
 {
     const T *p = static_cast<const T *>(data);
+    const unsigned nt = io_threads(count * sizeof(T));
     if constexpr (std::is_integral_v<T>) {
-        T a = p[0], b = p[0];
-        for (size_t i = 1; i < count; ++i) {
-            a = p[i] < a ? p[i] : a;
-            b = b < p[i] ? p[i] : b;
-        }
-        lo = static_cast<float>(a);
-        hi = static_cast<float>(b);
+        std::vector<T> a(nt, p[0]), b(nt, p[0]);
+        parallel_chunks(count, nt, [&](unsigned t, size_t s, size_t e) {
+            T x = p[0], y = p[0];
+            for (size_t i = s; i < e; ++i) {
+                x = p[i] < x ? p[i] : x;
+                y = y < p[i] ? p[i] : y;
+            }
+            a[t] = x;
+            b[t] = y;
+        });
+        lo = static_cast<float>(*std::min_element(a.begin(), a.end()));
+        hi = static_cast<float>(*std::max_element(b.begin(), b.end()));
     } else {
-        float a = static_cast<float>(p[0]), b = a;
-        for (size_t i = 1; i < count; ++i) {
-            const float v = static_cast<float>(p[i]);
-            if (v < a) a = v;
-            if (b < v) b = v;
+        std::vector<float> a(nt, INFINITY), b(nt, -INFINITY);
+        parallel_chunks(count, nt, [&](unsigned t, size_t s, size_t e) {
+            float x = INFINITY, y = -INFINITY;
+            for (size_t i = s; i < e; ++i) {
+                const float v = static_cast<float>(p[i]);
+                if (v < x) x = v;
+                if (y < v) y = v;
+            }
+            a[t] = x;
+            b[t] = y;
+        });
+        float x = static_cast<float>(p[0]), y = x;
+        for (unsigned t = 0; t < nt; ++t) {
+            if (a[t] < x) x = a[t];
+            if (y < b[t]) y = b[t];
         }
-        lo = a;
-        hi = b;
+        lo = x;
+        hi = y;
     }
+}
+
+// Raw payload of `bytes` at byte offset `off` of `path` into dst: pread by chunks in parallel.
+bool read_raw_parallel(const std::string &path, std::streamoff off, char *dst, size_t bytes)
+{
+    const int fd = ::open(path.c_str(), O_RDONLY);
+    if (fd < 0) return false;
+    const unsigned nt = io_threads(bytes);
+    std::vector<char> ok(nt, 0);
+    parallel_chunks(bytes, nt, [&](unsigned t, size_t s, size_t e) {
+        size_t done = s;
+        while (done < e) {
+            const ssize_t r = ::pread(fd, dst + done, std::min<size_t>(e - done, 1ull << 30),
+                                      (off_t)(off + (std::streamoff)done));
+            if (r <= 0) return;
+            done += (size_t)r;
+        }
+        ok[t] = 1;
+    });
+    ::close(fd);
+    return std::all_of(ok.begin(), ok.end(), [](char c) { return c != 0; });
 }
 
 void minmax(vr_dataset *d, size_t count)
@@ -570,12 +641,13 @@ extern "C" int vr_nrrd_load(const char *path, vr_dataset *out)
     if (es > 1 && (raw || hex) && endian.empty()) return herr(-1, "Failed to read file");
 
     std::ifstream detached;
+    std::string data_path;
     std::istream *in = &f;
     if (!datafile.empty()) {
         if (datafile.find(' ') != std::string::npos || datafile == "LIST")
             return herr(-3, "multi-file NRRD data is not supported");
-        std::string p = datafile[0] == '/' ? datafile : dir_of(path) + "/" + datafile;
-        detached.open(p, std::ios::binary);
+        data_path = datafile[0] == '/' ? datafile : dir_of(path) + "/" + datafile;
+        detached.open(data_path, std::ios::binary);
         if (!detached) return herr(-1, "Failed to read file");
         in = &detached;
     } else if (!header_done) {
@@ -595,8 +667,19 @@ extern "C" int vr_nrrd_load(const char *path, vr_dataset *out)
         } else if (byteskip > 0) {
             in->seekg(byteskip, std::ios::cur);
         }
-        in->read(static_cast<char *>(data), (std::streamsize)(count * es));
-        ok = (size_t)in->gcount() == count * es;
+        const size_t bytes = count * es;
+        const std::streamoff pos = in->tellg();
+        const std::string &src = datafile.empty() ? std::string(path) : data_path;
+        if (io_threads(bytes) > 1 && pos >= 0) {
+            // the payload must be all there, as a sequential read of `bytes` would find it
+            in->seekg(0, std::ios::end);
+            const std::streamoff end = in->tellg();
+            ok = end - pos >= (std::streamoff)bytes &&
+                 read_raw_parallel(src, pos, static_cast<char *>(data), bytes);
+        } else {
+            in->read(static_cast<char *>(data), (std::streamsize)bytes);
+            ok = (size_t)in->gcount() == bytes;
+        }
     } else if (hex) {
         unsigned char *d = static_cast<unsigned char *>(data);
         size_t n = 0;

@@ -291,7 +291,8 @@ def _take_dataset(ds: vr_dataset) -> Dataset:
     npdt = DTYPE_TO_NP[ds.dtype]
     n = dims[0] * dims[1] * dims[2]
     buf = (C.c_char * (n * npdt.itemsize)).from_address(ds.data)
-    arr = np.frombuffer(bytes(buf), dtype=npdt).reshape(dims[2], dims[1], dims[0]).copy()
+    # one copy out of the library's buffer, which is freed below
+    arr = np.frombuffer(buf, dtype=npdt).reshape(dims[2], dims[1], dims[0]).copy()
     out = Dataset(dims, float(ds.vmin), float(ds.vmax), arr)
     lib().vr_dataset_free(C.byref(ds))
     return out
