@@ -451,7 +451,7 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.nranks = nranks;
     P.local_rows = vr_shard_rows(c->height, row_block, nranks);
     P.tiles_x = (c->width + 15) / 16;
-    P.tiles_y = (P.local_rows + 15) / 16;
+    P.tiles_y = (P.local_rows + kMarchRows - 1) / kMarchRows;
     P.tile_order = p->tile_order >= 1 && p->tile_order <= 4 ? (uint32_t)p->tile_order : 4u;
     // wavefront footprint: 1 8x8, 2 16x4, 3 4x16; auto = 16x4 (x-contiguous brick rows:
     // fewer cache lines per wave-level load; measured -11% on the r=3 view, even on others)
@@ -1160,7 +1160,7 @@ const char *vr_kernel_name(const vr_ctx *c, const vr_params *p)
     // the variant the next vr_render_device launches (after a shaded frame built the field)
     const bool gf = p && p->shading && c->storage == ST_F32 && c->grad && c->grad_valid;
     // the full frame (row_block 16, one rank), as vr_render launches it
-    const uint32_t tiles = ((c->width + 15) / 16) * ((c->height + 15) / 16);
+    const uint32_t tiles = ((c->width + 15) / 16) * ((c->height + kMarchRows - 1) / kMarchRows);
     const bool pipe = use_pipeline(p && p->shading, tiles, c->brick_bytes) &&
                       !(p && p->skip_empty) && c->tf_n <= 256;
     return march_kernel_name(c->storage, p && p->shading != 0, false, p && p->skip_empty != 0, gf,

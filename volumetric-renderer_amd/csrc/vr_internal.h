@@ -116,7 +116,13 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
 // Wavefront count below which a launch uses the pipelined kernel (see build_params).
 constexpr uint32_t kPipelineMaxWaves = 24576;  // between N = 2 (16 K) and N = 1 (33 K) at 1080p
 constexpr size_t kPipelineMinBytes = 4ull << 30;  // large volumes: always pipelined
-constexpr uint32_t kThreadsPerTile = 256;  // 16 x 16 pixels
+// march_kernel tiles: 16 pixels wide, kMarchRows tall, one lane per pixel (experiment
+// builds may set VR_MARCH_ROWS=32: 512-thread workgroups whose 8 wavefronts share one CU's L1)
+#ifndef VR_MARCH_ROWS
+#define VR_MARCH_ROWS 16
+#endif
+constexpr uint32_t kMarchRows = VR_MARCH_ROWS;
+constexpr uint32_t kThreadsPerTile = 16 * kMarchRows;
 // vr_render (host output): row bands per frame, each copied to the host while later bands render
 constexpr int kHostBands = 4;
 constexpr uint32_t kHostBandMinRows = 256;  // shorter frames: one band

@@ -28,7 +28,7 @@ namespace vr {
 namespace {
 
 constexpr int kTile = 16;       // pixels per workgroup side
-constexpr int kThreads = 256;   // 4 waves, each an 8x8 pixel sub-tile
+constexpr int kThreads = 256;   // lane-pair kernel workgroup: 4 waves
 constexpr int kTfLds = 256;     // TF texels staged in LDS
 
 __device__ __forceinline__ float lerpf(float a, float b, float w) { return fmaf(w, b - a, a); }
@@ -614,7 +614,7 @@ __device__ __forceinline__ void shade_sample(const MarchParams &P, const char *_
 // rank's share of a multi-GPU frame), where every wave's serial chain of memory round trips,
 // not the chip's throughput, sets the time.  Reference-semantics results are identical.
 template <typename VT, bool SHADE, bool COUNT, bool SKIP, bool GF, bool PIPE>
-__global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP, GF, PIPE>)) void march_kernel(const MarchParams P)
+__global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, PIPE>)) void march_kernel(const MarchParams P)
 {
     __shared__ float4 s_tf[2 * kTfLds];  // {texel, difference to the next} pairs
     const int tid = threadIdx.x;
@@ -628,17 +628,17 @@ __global__ __launch_bounds__(kThreads, (kMarchMinWaves<COUNT, SKIP, GF, PIPE>)) 
 
     const bool tf_in_lds = P.tf_n <= kTfLds;
     if (tf_in_lds)
-        for (int i = tid; i < 2 * P.tf_n; i += kThreads) s_tf[i] = P.tf[i];
+        for (int i = tid; i < 2 * P.tf_n; i += (int)kThreadsPerTile) s_tf[i] = P.tf[i];
     __syncthreads();
     const long by_stride = (long)P.nbx * kBrickElems;  // elements between brick rows/slabs
     const long bz_stride = (long)P.nbx * P.nby * kBrickElems;
 
-    // wavefront -> (ww x wh) pixels, ww = 2^wave_w_shift, the 4 of them tiling the 16x16 tile
+    // wavefront -> (ww x wh) pixels, ww = 2^wave_w_shift, together tiling the 16 x kMarchRows tile
     const uint32_t wave = tid >> 6, lane = tid & 63;
     const uint32_t ws = P.wave_w_shift, ww = 1u << ws, wh = 64u >> ws;
     const uint32_t wpr = kTile >> ws;  // wavefronts per tile row
     const uint32_t px = tile_x * kTile + (wave % wpr) * ww + (lane & (ww - 1));
-    const uint32_t ly = tile_y * kTile + (wave / wpr) * wh + (lane >> ws);
+    const uint32_t ly = tile_y * kMarchRows + (wave / wpr) * wh + (lane >> ws);
     bool active = px < P.W && ly < P.local_rows;
     const uint32_t blk = ly / P.row_block;
     const uint32_t gy = (blk * P.nranks + P.rank) * P.row_block + (ly - blk * P.row_block);
@@ -1367,7 +1367,7 @@ hipError_t launch_march_t(const MarchParams &p, hipStream_t stream)
                              : p.tile_order >= 3 ? ((p.supers_total + 7) / 8) * 8 * 16
                                                  : p.tiles_x * p.tiles_y;
     if (p.tiles_x * p.tiles_y == 0) return hipSuccess;
-    hipLaunchKernelGGL((march_kernel<VT, SHADE, COUNT, SKIP, GF, PIPE>), dim3(nblocks), dim3(kThreads), 0,
+    hipLaunchKernelGGL((march_kernel<VT, SHADE, COUNT, SKIP, GF, PIPE>), dim3(nblocks), dim3(kThreadsPerTile), 0,
                        stream, p);
     return hipGetLastError();
 }
