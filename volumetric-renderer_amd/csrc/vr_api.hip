@@ -456,6 +456,8 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     // wavefront footprint: 1 8x8, 2 16x4, 3 4x16; auto = 16x4 (x-contiguous brick rows:
     // fewer cache lines per wave-level load; measured -11% on the r=3 view, even on others)
     P.wave_w_shift = p->wave_shape == 1 ? 3u : (p->wave_shape == 3 ? 2u : 4u);
+    // a wavefront is at most kMarchRows tall (experiment builds with shorter tiles)
+    while ((64u >> P.wave_w_shift) > kMarchRows) ++P.wave_w_shift;
     P.supers_x = (P.tiles_x + 3) / 4;
     P.supers_total = P.supers_x * ((P.tiles_y + 3) / 4);
     P.out_format = out_format;
