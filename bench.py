@@ -88,15 +88,40 @@ def set_gather(kind):
     GATHER = kind
 
 
+def _all_ok(ok: bool) -> bool:
+    """True on every rank iff `ok` holds on every rank (one MIN all-reduce)."""
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device="cuda")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return bool(flag.item())
+
+
 def dist_frames(rp, rank, world, row_block, inflight):
     """One RCCL communicator per frames-in-flight setting (vr_dist_create), id from rank 0
-    broadcast over the torch.distributed process group."""
+    broadcast over the torch.distributed process group.  Every rank checks that RCCL loads
+    and that its communicator came up, and the ranks agree on both, so a failure on any rank
+    sends all of them to the torch.distributed path together (never a rank left waiting in a
+    collective the others skipped)."""
     key = (row_block, inflight)
     if key not in _DIST:
-        uid = vr_amd.dist_unique_id() if rank == 0 else bytes(vr_amd.DIST_ID_BYTES)
+        err = None
+        try:
+            uid = vr_amd.dist_unique_id()  # every rank: proves RCCL loads here
+        except RuntimeError as e:
+            uid, err = bytes(vr_amd.DIST_ID_BYTES), e
+        if not _all_ok(err is None):
+            raise RuntimeError(f"RCCL unavailable on some rank ({err or 'another rank'})")
         t = torch.tensor(list(uid), dtype=torch.uint8, device="cuda")
         dist.broadcast(t, 0)
-        _DIST[key] = vr_amd.DistFrames(rp, bytes(t.cpu().tolist()), world, rank, row_block, inflight)
+        df = None
+        try:
+            df = vr_amd.DistFrames(rp, bytes(t.cpu().tolist()), world, rank, row_block, inflight)
+        except RuntimeError as e:
+            err = e
+        if not _all_ok(df is not None):
+            if df is not None:
+                df.close()
+            raise RuntimeError(f"vr_dist_create failed on some rank ({err or 'another rank'})")
+        _DIST[key] = df
     return _DIST[key]
 
 
@@ -155,7 +180,7 @@ def run_variant(rp, cfg, steps, warmup, rank, world, inflight, row_block=8):
         # the whole frame in the library: render -> ncclGather -> assemble, stream-ordered
         try:
             pipe = NativeFrames(dist_frames(rp, rank, world, row_block, inflight), cam, p, rank, H, W)
-        except RuntimeError as e:  # e.g. librccl.so.1 not loadable: same on every rank
+        except RuntimeError as e:  # raised on every rank together (dist_frames)
             print(f"bench: native RCCL frame path unavailable ({e}); using torch.distributed.gather",
                   file=sys.stderr, flush=True)
             set_gather("torch")
