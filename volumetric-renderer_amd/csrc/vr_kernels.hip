@@ -572,6 +572,9 @@ __device__ __forceinline__ bool block_tile(const MarchParams &P, uint32_t &tile_
     return true;
 }
 
+#ifndef VR_EXP_NO_GRAD_LOADS
+#define VR_EXP_NO_GRAD_LOADS 0  // experiment builds: time without the difference-field loads
+#endif
 // Gradient Phong extension for one sample with alpha > 0 (s: TF colour in/out): gradient from
 // the difference field (GF) or the stencil, scaled to normalised coordinates, headlight
 // ndl = |n . dir|, rgb' = rgb (ka + kd ndl) + ks ndl^p.  The oracle's march_pixel, same order.
@@ -583,7 +586,11 @@ __device__ __forceinline__ void shade_sample(const MarchParams &P, const char *_
                                              float4 &s)
 {
     float gx, gy_, gz;
-    if constexpr (GF) {  // f32: precomputed difference field
+    if constexpr (GF && VR_EXP_NO_GRAD_LOADS) {  // timing experiment only: wrong gradient
+        gx = c.v[1] - c.v[0];
+        gy_ = c.v[2] - c.v[0];
+        gz = c.v[4] - c.v[0];
+    } else if constexpr (GF) {  // f32: precomputed difference field
         grad_field<PACKED>(reinterpret_cast<const char *>(P.grad), ce, ax, ay, az, gx, gy_, gz);
     } else {
         gradient<VT, PACKED>(vol, ce, c, pi & (kBrick - 1), pj & (kBrick - 1), pk & (kBrick - 1),
