@@ -103,6 +103,15 @@ def lib() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C volumetric-renderer_amd` "
                            "(or __graft_entry__.build()); there is no CPU fallback")
+    # PyTorch ships its own libamdhip64.so.7 / libhsa-runtime64.so.1 under the same sonames as
+    # /opt/rocm's.  Whichever loads first serves the whole process, and torch's CUDA init
+    # failed ("No HIP GPUs are available") once this library had brought in /opt/rocm's
+    # runtime and initialised it.  Load torch first when it is installed, so the process
+    # runs one runtime that both use (the one the GPU tests and bench.py run on).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, u32, f32, i32 = C.c_void_p, C.c_uint32, C.c_float, C.c_int
     sig = {
