@@ -1,0 +1,37 @@
+"""GPU: bench.py keeps the driver's contract -- one JSON line on stdout with BASELINE.json's
+metric, the whole-job value, the roofline object for the timed kernel and the config's
+workload name (a short run: 4 steps, no CPU baseline, no variants)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_prints_one_contract_line(gpu):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "2",
+                        "--no-cpu-baseline", "--no-variants"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+    assert d["metric"] == base["metric"]
+    assert d["unit"] == "Gsamples/s" and d["higher_is_better"] is True
+    assert d["n_gpus"] == 1 and d["steps"] == 4 and d["warmup"] == 2
+    assert d["value"] > 0 and d["ms_per_step"] > 0 and d["fps"] > 0
+    assert d["dtype"] == "f32" and d["vs_baseline"] is None
+    assert d["config"]["workload"].startswith("C3:")
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    assert rf["achieved"] > 0 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    assert "march_kernel" in rf["kernel"] and rf["kernel_ms"] > 0
+    # the value is executed samples of the whole frame per second
+    spf = d["config"]["samples_per_frame"]
+    assert abs(d["value"] - spf * d["steps"] / (d["ms_per_step"] * 1e-3 * d["steps"]) / 1e9) < 0.01 * d["value"]
