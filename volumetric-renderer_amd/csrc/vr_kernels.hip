@@ -1033,41 +1033,59 @@ __global__ __launch_bounds__(kThreads) void march_pair_kernel(const MarchParams 
 // first, written to perm[x + 8 j] (j = rank), the XCD's remaining slots ~0.  Workgroups are
 // dispatched in index order round-robin over the XCDs, so each XCD starts its longest tiles
 // first and the frame no longer ends on a few long rays.
+// Each XCD's tiles, longest first by the last launch's durations: a stable counting sort
+// over one bucket per octave of duration (bucket 31 = longest).  Thread t owns list entries
+// [t chunk, (t + 1) chunk); counts per (bucket, thread), offsets bucket-major (longest
+// first) and thread-minor, so the tiles of one bucket keep their list order (the XCD's
+// super-tiles in raster order) and tiles running together on an XCD stay neighbours.
+// Against 4 buckets per octave in arbitrary order: C3 +1.8%, shaded views 1-4% faster
+// (profiles/r01/tile_order/stable_octave_ab.txt).
 __global__ __launch_bounds__(256) void order_tiles_kernel(const uint32_t *__restrict__ cost,
                                                           const uint32_t *__restrict__ lists,
                                                           uint32_t *__restrict__ perm,
                                                           uint32_t per_xcd)
 {
-    __shared__ uint32_t count[64], offset[64], n_tiles;
+    constexpr int NB = 32;
+    __shared__ uint32_t cnt[NB][257];  // [b][t]: offset within bucket b; [b][256]: bucket base
+    __shared__ uint32_t n_tiles;
     const uint32_t x = blockIdx.x, tid = threadIdx.x;
     const uint32_t *list = lists + (size_t)x * per_xcd;
-    if (tid < 64) count[tid] = 0;
-    if (tid == 0) n_tiles = 0;
+    auto bucket = [](uint32_t c) -> uint32_t { return c < 2 ? 0u : 31u - __clz(c); };
+    const uint32_t chunk = (per_xcd + 255) / 256;
+    const uint32_t j0 = min(per_xcd, tid * chunk), j1 = min(per_xcd, j0 + chunk);
+    for (int b = 0; b < NB; ++b) cnt[b][tid] = 0;
     __syncthreads();
-    auto bucket = [](uint32_t c) -> uint32_t {  // 4 buckets per octave, 63 = longest
-        if (c < 4) return 0;
-        const uint32_t m = 31 - __clz(c);
-        return min(4 * m + ((c >> (m - 2)) & 3u), 63u);
-    };
-    for (uint32_t j = tid; j < per_xcd; j += blockDim.x) {
+    for (uint32_t j = j0; j < j1; ++j) {
+        const uint32_t t = list[j];
+        if (t != 0xFFFFFFFFu) ++cnt[bucket(cost[t])][tid];
+    }
+    __syncthreads();
+    if (tid < NB) {  // exclusive prefix over the threads of bucket tid; its total in [256]
+        uint32_t acc = 0;
+        for (int k = 0; k < 256; ++k) {
+            const uint32_t v = cnt[tid][k];
+            cnt[tid][k] = acc;
+            acc += v;
+        }
+        cnt[tid][256] = acc;
+    }
+    __syncthreads();
+    if (tid == 0) {  // bucket bases, longest first
+        uint32_t acc = 0;
+        for (int b = NB - 1; b >= 0; --b) {
+            const uint32_t v = cnt[b][256];
+            cnt[b][256] = acc;
+            acc += v;
+        }
+        n_tiles = acc;
+    }
+    __syncthreads();
+    for (uint32_t j = j0; j < j1; ++j) {
         const uint32_t t = list[j];
         if (t != 0xFFFFFFFFu) {
-            atomicAdd(&count[bucket(cost[t])], 1u);
-            atomicAdd(&n_tiles, 1u);
+            const uint32_t b = bucket(cost[t]);
+            perm[x + 8 * (cnt[b][256] + cnt[b][tid]++)] = t;
         }
-    }
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t acc = 0;
-        for (int b = 63; b >= 0; --b) {
-            offset[b] = acc;
-            acc += count[b];
-        }
-    }
-    __syncthreads();
-    for (uint32_t j = tid; j < per_xcd; j += blockDim.x) {
-        const uint32_t t = list[j];
-        if (t != 0xFFFFFFFFu) perm[x + 8 * atomicAdd(&offset[bucket(cost[t])], 1u)] = t;
     }
     for (uint32_t j = n_tiles + tid; j < per_xcd; j += blockDim.x) perm[x + 8 * j] = 0xFFFFFFFFu;
 }
