@@ -458,8 +458,8 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.wave_w_shift = p->wave_shape == 1 ? 3u : (p->wave_shape == 3 ? 2u : 4u);
     // a wavefront is at most kMarchRows tall (experiment builds with shorter tiles)
     while ((64u >> P.wave_w_shift) > kMarchRows) ++P.wave_w_shift;
-    P.supers_x = (P.tiles_x + 3) / 4;
-    P.supers_total = P.supers_x * ((P.tiles_y + 3) / 4);
+    P.supers_x = (P.tiles_x + kSuper - 1) / kSuper;
+    P.supers_total = P.supers_x * ((P.tiles_y + kSuper - 1) / kSuper);
     P.out_format = out_format;
     P.slab_default = c->smin[0] == 0.0f && c->smin[1] == 0.0f && c->smin[2] == 0.0f &&
                      c->smax[0] == 1.0f && c->smax[1] == 1.0f && c->smax[2] == 1.0f;
@@ -591,9 +591,21 @@ vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P, void *stream)
     t.nranks = P.nranks;
     // per-XCD tile lists (tile_order 3's super-tile assignment), padded with ~0
     std::vector<std::vector<uint32_t>> xl(8);
-    for (uint32_t ty = 0; ty < P.tiles_y; ++ty)
-        for (uint32_t tx = 0; tx < P.tiles_x; ++tx)
-            xl[((ty >> 2) * P.supers_x + (tx >> 2)) & 7u].push_back(ty * P.tiles_x + tx);
+    if (VR_LIST_ORDER == 1) {  // super-tile major
+        const uint32_t sy_n = (P.tiles_y + kSuper - 1) / kSuper;
+        for (uint32_t sy = 0; sy < sy_n; ++sy)
+            for (uint32_t sx = 0; sx < P.supers_x; ++sx)
+                for (uint32_t w = 0; w < kSuper * kSuper; ++w) {
+                    const uint32_t tx = sx * kSuper + w % kSuper, ty = sy * kSuper + w / kSuper;
+                    if (tx < P.tiles_x && ty < P.tiles_y)
+                        xl[(sy * P.supers_x + sx) & 7u].push_back(ty * P.tiles_x + tx);
+                }
+    } else {  // frame raster
+        for (uint32_t ty = 0; ty < P.tiles_y; ++ty)
+            for (uint32_t tx = 0; tx < P.tiles_x; ++tx)
+                xl[((ty >> kSuperShift) * P.supers_x + (tx >> kSuperShift)) & 7u].push_back(
+                    ty * P.tiles_x + tx);
+    }
     for (int x = 0; x < 8; ++x) t.per_xcd = xl[x].size() > t.per_xcd ? (uint32_t)xl[x].size() : t.per_xcd;
     std::vector<uint32_t> lists(8 * (size_t)t.per_xcd, 0xFFFFFFFFu);
     for (int x = 0; x < 8; ++x)
@@ -984,7 +996,7 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
         if (const char *e = std::getenv("VR_PAIR_LANES")) P.pair = e[0] == '4' ? 4 : 2;
         const uint32_t th = 16 / P.pair;
         P.tiles_y = (P.local_rows + th - 1) / th;
-        P.supers_total = P.supers_x * ((P.tiles_y + 3) / 4);
+        P.supers_total = P.supers_x * ((P.tiles_y + kSuper - 1) / kSuper);
     }
     vr_ctx::TileSched *ts = tile_sched(c, P, stream);
     hipEvent_t e0 = nullptr, e1 = nullptr;

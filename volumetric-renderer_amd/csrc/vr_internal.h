@@ -122,6 +122,17 @@ constexpr size_t kPipelineMinBytes = 4ull << 30;  // large volumes: always pipel
 #define VR_MARCH_ROWS 16
 #endif
 constexpr uint32_t kMarchRows = VR_MARCH_ROWS;
+// super-tiles (tile orders 3 and 4): 2^kSuperShift tiles per side, dealt round-robin over the
+// 8 XCDs; experiment builds may change the size (VR_SUPER_SHIFT) and the order an XCD's tile
+// list is kept in for the adaptive sort (VR_LIST_ORDER 0: frame raster, 1: super-tile major)
+#ifndef VR_SUPER_SHIFT
+#define VR_SUPER_SHIFT 2
+#endif
+#ifndef VR_LIST_ORDER
+#define VR_LIST_ORDER 0
+#endif
+constexpr uint32_t kSuperShift = VR_SUPER_SHIFT;
+constexpr uint32_t kSuper = 1u << kSuperShift;
 constexpr uint32_t kThreadsPerTile = 16 * kMarchRows;
 // vr_render (host output): row bands per frame, each copied to the host while later bands render
 constexpr int kHostBands = 4;

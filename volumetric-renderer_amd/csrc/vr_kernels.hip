@@ -554,10 +554,10 @@ __device__ __forceinline__ bool block_tile(const MarchParams &P, uint32_t &tile_
         return t != 0xFFFFFFFFu;
     }
     if (P.tile_order >= 3) {  // 3, and 4 before its first permutation
-        const uint32_t k = b >> 3, w = k & 15;
-        const uint32_t s = (b & 7u) + 8u * (k >> 4);
-        tile_x = (s % P.supers_x) * 4 + (w & 3);
-        tile_y = (s / P.supers_x) * 4 + (w >> 2);
+        const uint32_t k = b >> 3, w = k & (kSuper * kSuper - 1);
+        const uint32_t s = (b & 7u) + 8u * (k >> (2 * kSuperShift));
+        tile_x = (s % P.supers_x) * kSuper + (w & (kSuper - 1));
+        tile_y = (s / P.supers_x) * kSuper + (w >> kSuperShift);
         return s < P.supers_total && tile_x < P.tiles_x && tile_y < P.tiles_y;
     }
     if (P.tile_order == 2) {
@@ -1389,7 +1389,7 @@ template <typename VT, bool SHADE, bool COUNT, bool SKIP, bool GF = false, bool 
 hipError_t launch_march_t(const MarchParams &p, hipStream_t stream)
 {
     const uint32_t nblocks = p.tile_perm ? p.nperm
-                             : p.tile_order >= 3 ? ((p.supers_total + 7) / 8) * 8 * 16
+                             : p.tile_order >= 3 ? ((p.supers_total + 7) / 8) * 8 * kSuper * kSuper
                                                  : p.tiles_x * p.tiles_y;
     if (p.tiles_x * p.tiles_y == 0) return hipSuccess;
     hipLaunchKernelGGL((march_kernel<VT, SHADE, COUNT, SKIP, GF, PIPE>), dim3(nblocks), dim3(kThreadsPerTile), 0,
@@ -1401,7 +1401,7 @@ template <typename VT, bool SHADE, bool GF>
 hipError_t launch_pair_t(const MarchParams &p, hipStream_t stream)
 {
     const uint32_t nblocks = p.tile_perm ? p.nperm
-                             : p.tile_order >= 3 ? ((p.supers_total + 7) / 8) * 8 * 16
+                             : p.tile_order >= 3 ? ((p.supers_total + 7) / 8) * 8 * kSuper * kSuper
                                                  : p.tiles_x * p.tiles_y;
     if (p.tiles_x * p.tiles_y == 0) return hipSuccess;
     if (p.pair == 4)
