@@ -1040,6 +1040,9 @@ __global__ __launch_bounds__(kThreads) void march_pair_kernel(const MarchParams 
 // super-tiles in raster order) and tiles running together on an XCD stay neighbours.
 // Against 4 buckets per octave in arbitrary order: C3 +1.8%, shaded views 1-4% faster
 // (profiles/r01/tile_order/stable_octave_ab.txt).
+#ifndef VR_ORDER_OCTAVES
+#define VR_ORDER_OCTAVES 1
+#endif
 __global__ __launch_bounds__(256) void order_tiles_kernel(const uint32_t *__restrict__ cost,
                                                           const uint32_t *__restrict__ lists,
                                                           uint32_t *__restrict__ perm,
@@ -1050,7 +1053,8 @@ __global__ __launch_bounds__(256) void order_tiles_kernel(const uint32_t *__rest
     __shared__ uint32_t n_tiles;
     const uint32_t x = blockIdx.x, tid = threadIdx.x;
     const uint32_t *list = lists + (size_t)x * per_xcd;
-    auto bucket = [](uint32_t c) -> uint32_t { return c < 2 ? 0u : 31u - __clz(c); };
+    // experiment builds: VR_ORDER_OCTAVES octaves per bucket
+    auto bucket = [](uint32_t c) -> uint32_t { return c < 2 ? 0u : (31u - __clz(c)) / VR_ORDER_OCTAVES; };
     const uint32_t chunk = (per_xcd + 255) / 256;
     const uint32_t j0 = min(per_xcd, tid * chunk), j1 = min(per_xcd, j0 + chunk);
     for (int b = 0; b < NB; ++b) cnt[b][tid] = 0;
