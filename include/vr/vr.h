@@ -188,7 +188,10 @@ int vr_set_slicing(vr_ctx *ctx, const float min_slice[3], const float max_slice[
 /* ---- render ---- */
 
 /* Render one full frame synchronously into host memory `out` (W*H*4 bytes for RGBA8,
- * W*H*16 for RGBA32F), row 0 = top (Vulkan framebuffer order). */
+ * W*H*16 for RGBA32F), row 0 = top (Vulkan framebuffer order).  Replaces
+ * OffscreenPass::record + update_uniform_buffer (offscreen_pass.cpp:163-230, 1152-1171) plus
+ * the readback a host-side presenter needs.  Frames of >= 256 rows render as 4 row bands
+ * whose device->host copies overlap the later bands; returns once `out` holds the frame. */
 int vr_render(vr_ctx *ctx, const vr_camera *cam, const vr_params *p, void *out,
               int out_format);
 
