@@ -1,7 +1,8 @@
 // vr_kernels.hip — gfx950 (CDNA4) kernels of the volume ray-marcher.
 //
-// The hot path is march_kernel: one lane per pixel, a 64-lane wavefront marches an 8x8
-// pixel tile (ray coherence), a 256-thread workgroup a 16x16 tile.  It restates the
+// The hot path is march_kernel: one lane per pixel, a 64-lane wavefront marches a 16x4
+// pixel strip by default (vr_params.wave_shape), a 256-thread workgroup a 16x16 tile.  It
+// restates the
 // reference fragment shader res/shaders/volume.frag:21-52 plus the Vulkan fixed-function
 // state it runs under (src/rendering/offscreen_pass.cpp: cube ray entry :55-90 + cull
 // :680-681 + depth clip :701-712, border trilinear sampler :1014-1039, sRGB TF sampler
@@ -9,11 +10,17 @@
 //
 // Design points (DESIGN.md has the roofline discussion):
 //  * memory-bound gather, no MFMA: each density sample is a 2x2x2 trilinear footprint;
-//  * bricked native-dtype volume (vr_internal.h): one brick base address + 7 immediate
-//    offsets per sample, zero apron = CLAMP_TO_BORDER without bounds tests;
-//  * TF decoded to linear float4 once per frame on the host and staged in LDS;
-//  * XCD-aware tile order (march_kernel head): tiles grouped in 64x64-pixel super-tiles, each
-//    super-tile's workgroups on one XCD (L2 locality), super-tiles dealt over all XCDs (balance);
+//  * bricked native-dtype volume with paired elements (vr_internal.h): f32 z-pairs (a sample
+//    is 2 x 16-B loads), 8/16-bit yz-quads (one load); zero apron = CLAMP_TO_BORDER without
+//    bounds tests; shaded f32 frames read a precomputed central-difference field;
+//  * TF decoded to linear float4 (with forward differences) once per upload on the host and
+//    staged in LDS;
+//  * XCD-aware tile order (block_tile / order_tiles_kernel): tiles grouped in 64x64-pixel
+//    super-tiles dealt over the 8 XCDs (balance); each XCD dispatches its tiles longest first
+//    by the last launches' durations, stable within a duration octave (co-running tiles stay
+//    neighbours in its L2);
+//  * pipelined variant (two samples of a ray in flight) for shaded frames, small launches and
+//    volumes >= 4 GiB; lane-group variant for small shaded launches with serial frames;
 //  * fp contraction is OFF (pragma below + -ffp-contract=off): every fused multiply-add is
 //    an explicit fmaf(), matching the CPU oracle's operation order bit for bit.
 #include "vr_internal.h"
