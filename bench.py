@@ -49,6 +49,11 @@ CONFIGS = {
     "c3_ref": dict(dims=(512, 512, 512), dtype=np.float32, W=1920, H=1080, cam="fill", tf="tf2",
                    shading=0, ert=0.0, seed=2024,
                    workload="C3 reference semantics: no shading, no ERT (volume.frag as written)"),
+    # benchmarks use r=1.6 (frame-filling) plus the reference's default camera
+    # (camera.cpp:7-13: r=3, 17% of the 1080p frame covered)
+    "c3_default": dict(dims=(512, 512, 512), dtype=np.float32, W=1920, H=1080, cam="default",
+                       tf="tf2", shading=1, ert=1e-5, seed=2024,
+                       workload="C3 at the reference's default camera (r=3), gradient Phong + ERT"),
     "c2": dict(dims=(256, 256, 256), dtype=np.uint8, W=1024, H=1024, cam="fill", tf="tf2",
                shading=0, ert=0.0, seed=1234, source="ct_head",
                workload="C2: 256^3 u8 synthetic CT head, 1024x1024, trilinear + 1D TF"),
@@ -144,8 +149,9 @@ class NativeFrames:
 
 
 def run_variant(rp, cfg, steps, warmup, rank, world, inflight, row_block=8):
-    """Time `steps` frames; returns (max-over-ranks seconds, avg kernel ms, frame stats,
-    this rank's stats, this rank's shard pixels, frame check).  For N > 1 a frame is: render
+    """Time `steps` frames; returns a dict: secs (max over ranks), kms (this rank's average
+    kernel ms), frame (frame work counters), mine (this rank's), shard_px, check (N > 1:
+    assembled frame == single-rank frame) and per_rank timings.  For N > 1 a frame is: render
     this rank's row blocks -> RCCL gather to rank 0 -> de-interleave on rank 0.  `inflight`
     frames are in flight (vr_dist.FramePipeline): frame i's work goes to stream i mod
     inflight, so consecutive frames overlap on the device and a frame's gather overlaps the
@@ -202,6 +208,10 @@ def run_variant(rp, cfg, steps, warmup, rank, world, inflight, row_block=8):
         dist.barrier()
     rp.timing_reset()
     rp.timing_enable(True)
+    native = isinstance(pipe, NativeFrames)
+    if native:
+        pipe.frames.timing_read()  # clears the warm-up record
+        pipe.frames.timing_enable(True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -215,9 +225,27 @@ def run_variant(rp, cfg, steps, warmup, rank, world, inflight, row_block=8):
     t1 = time.perf_counter()
     rp.timing_enable(False)
     kms, nl = rp.timing_read()
+    rend_ms = gath_ms = float("nan")
+    if native:
+        pipe.frames.timing_enable(False)
+        r, g, n = pipe.frames.timing_read()
+        rend_ms, gath_ms = r / max(n, 1), g / max(n, 1)
     el = torch.tensor([t1 - t0], dtype=torch.float64, device=sdev)
+    # per-rank diagnostics (straggler localisation): this rank's own loop time, its render
+    # kernel's average duration and, on the native RCCL path, the render and ncclGather
+    # spans timed by HIP events on their streams
+    mine = torch.tensor([rank, t1 - t0, kms / max(nl, 1), rend_ms, gath_ms], dtype=torch.float64,
+                        device=sdev)
+    per_rank = [mine]
     if world > 1:
+        per_rank = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(per_rank, mine)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    per_rank = [dict(rank=int(v[0]), loop_ms_per_frame=round(float(v[1]) / steps * 1e3, 4),
+                     kernel_ms=round(float(v[2]), 4),
+                     render_span_ms=None if np.isnan(float(v[3])) else round(float(v[3]), 4),
+                     gather_span_ms=None if np.isnan(float(v[4])) else round(float(v[4]), 4))
+                for v in (t.cpu() for t in per_rank)]
     check = None
     if world > 1 and rank == 0:
         # the assembled frame must equal this device's single-rank render of the whole frame
@@ -226,13 +254,33 @@ def run_variant(rp, cfg, steps, warmup, rank, world, inflight, row_block=8):
                          torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         check = bool(torch.equal(full[:H], pipe.last.frame))
-    return float(el.item()), kms / max(nl, 1), frame_stats, my_stats, sr * W, check
+    return dict(secs=float(el.item()), kms=kms / max(nl, 1), frame=frame_stats, mine=my_stats,
+                shard_px=sr * W, check=check, per_rank=per_rank)
 
 
-def cpu_baseline(rp, cfg, budget_s=12.0):
-    """The CPU oracle (oracle/oracle.c, OpenMP) on a bounded row sample of the same frame."""
+def host_cores():
+    """(threads to use, description): every CPU this process may run on (nproc = the affinity
+    mask), and the cgroup CPU quota beside it when one is set."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    desc = f"nproc={n}, os.cpu_count()={os.cpu_count()}, cgroup cpu quota=" + (
+        f"{quota:g} CPUs" if quota else "none")
+    return n, desc
+
+
+def cpu_baseline(rp, cfg, budget_s=12.0, nthreads=None):
+    """The CPU oracle (oracle/oracle.c, OpenMP over rows) on a bounded row sample of the same
+    frame, on all host cores (nproc)."""
     import pyoracle
-    nthreads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    cores_desc = ""
+    if nthreads is None:
+        nthreads, cores_desc = host_cores()
     vol = rp.read_volume()
     _, (vmin, vmax), _ = rp.volume_info()
     cam = synth.camera(cfg["cam"]).to_vr_camera()
@@ -258,23 +306,39 @@ def cpu_baseline(rp, cfg, budget_s=12.0):
         samples += st["samples"]
         reps += 1
     return dict(value=round(samples / t / 1e9, 4), unit="Gsamples/s", cores=nthreads, kind="port",
+                ms_per_frame=round(t / reps / len(rows) * H * 1e3, 2),
                 sample=f"{len(rows)} of {H} frame rows (every {stride}th row) x {reps} repeats, same "
                        f"volume/camera/TF/params; {samples} samples in {t:.2f} s (oracle/oracle.c, "
-                       f"OpenMP x{nthreads})")
+                       f"OpenMP x{nthreads}; {cores_desc})")
 
 
-def load_traffic(cfg_name, world):
+def cpu_baseline_other(name, device, budget_s, nthreads):
+    """the CPU baseline of C1 and C2 as well (their own volumes and frames)."""
+    cfg = CONFIGS[name]
+    rp = setup_pass(cfg, device)
+    try:
+        r = cpu_baseline(rp, cfg, budget_s, nthreads)
+    finally:
+        rp.close()
+    r["workload"] = cfg["workload"]
+    return r
+
+
+def load_traffic(cfg_name, world, kernel):
+    """Measured HBM bytes per frame (rocprofv3 PMC, profiles/pmc_traffic.json written by
+    tools/traffic_json.py from tools/measure_round.sh) for this config, if measured on the
+    kernel this run launches."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     try:
         d = json.load(open(path))
         e = d.get(cfg_name)
-        if e and int(e.get("n_gpus", 1)) == world:
-            return float(e["hbm_bytes_per_launch"])
+        if e and int(e.get("n_gpus", 1)) == world and e.get("kernel", kernel) == kernel:
+            return float(e["hbm_bytes_per_launch"]), e.get("source")
     except Exception:
-        return None
-    return None
+        return None, None
+    return None, None
 
 
 def main():
@@ -317,12 +381,14 @@ def main():
     inflight = 1 if args.serial_gather else max(1, min(16, args.frames_in_flight))
     if BACKEND != "nccl":
         inflight = 1
-    secs, kms, fstats, r0stats, shard_px, frame_check = run_variant(rp, cfg, args.steps, args.warmup, rank, world,
-                                                                    inflight)
+    R = run_variant(rp, cfg, args.steps, args.warmup, rank, world, inflight)
+    secs, kms, fstats, r0stats, shard_px = R["secs"], R["kms"], R["frame"], R["mine"], R["shard_px"]
+    frame_s = secs / args.steps
     value = fstats["samples"] * args.steps / secs / 1e9
     fps = args.steps / secs
-    achieved = algorithmic_bytes(r0stats, vbytes, shard_px) / (kms * 1e-3) / 1e9
-    traffic = load_traffic(args.config, world)
+    kernel = rp.kernel_name(vr_amd.default_params(shading=cfg["shading"]))
+    traffic, traffic_src = load_traffic(args.config, world, kernel)
+    gather_bytes = algorithmic_bytes(fstats, vbytes, cfg["W"] * cfg["H"])
 
     # also the reference-equivalent sample count (volume.frag as written: no
     # ERT, every in-slab step sampled) of the same frame, per second of this configuration
@@ -335,45 +401,55 @@ def main():
     ref_samples = int(ref_samples.item())
 
     variants = {}
+    serial_kms = None
     if not args.no_variants and inflight > 1:
         # the serial form too (one frame at a time; for N > 1 each frame's
         # gather waited for before the next render).  Its kernels run alone on the device,
-        # so their HIP-event durations are the kernel's own (reported beside the roofline).
+        # so their HIP-event durations are the kernel's own.
         ns = max(5, args.steps // 2)
-        s4, k4, _, r4, _, c4 = run_variant(rp, cfg, ns, min(args.warmup, 5), rank, world, 1)
+        V = run_variant(rp, cfg, ns, min(args.warmup, 5), rank, world, 1)
+        serial_kms = V["kms"]
         variants["serial_frames"] = dict(
-            value=round(fstats["samples"] * ns / s4 / 1e9, 3), unit="Gsamples/s",
-            ms_per_step=round(s4 / ns * 1e3, 4), fps=round(ns / s4, 2), kernel_ms=round(k4, 4),
-            roofline_frac=round(algorithmic_bytes(r4, vbytes, shard_px) / (k4 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            frame_check=c4)
+            value=round(fstats["samples"] * ns / V["secs"] / 1e9, 3), unit="Gsamples/s",
+            ms_per_step=round(V["secs"] / ns * 1e3, 4), fps=round(ns / V["secs"], 2),
+            kernel_ms=round(V["kms"], 4), frame_check=V["check"])
     if not args.no_variants and args.config == "c3":
+        # the reference's default camera (benchmarks at r=1.6 plus the default)
+        dcfg = CONFIGS["c3_default"]
+        V = run_variant(rp, dcfg, args.steps, min(args.warmup, 5), rank, world, inflight)
+        dtr, _ = load_traffic("c3_default", world, kernel)
+        variants["default_camera"] = dict(
+            workload=dcfg["workload"], camera=synth.CAMERAS[dcfg["cam"]],
+            value=round(V["frame"]["samples"] * args.steps / V["secs"] / 1e9, 3), unit="Gsamples/s",
+            ms_per_step=round(V["secs"] / args.steps * 1e3, 4), fps=round(args.steps / V["secs"], 2),
+            samples_per_frame=V["frame"]["samples"], rays_per_frame=V["frame"]["rays"],
+            hbm_bytes_per_frame=dtr,
+            hbm_frac=round(dtr / (V["secs"] / args.steps) / 1e9 / HBM_PEAK_GBS, 4) if dtr else None)
         vcfg = CONFIGS["c3_ref"]
-        rp.transfer_function_changed(synth.TFS[vcfg["tf"]]())
-        s2, k2, f2, r2, _, _ = run_variant(rp, vcfg, args.steps, min(args.warmup, 5), rank, world,
-                                           inflight)
+        V = run_variant(rp, vcfg, args.steps, min(args.warmup, 5), rank, world, inflight)
+        rtr, _ = load_traffic("c3_ref", world, rp.kernel_name(vr_amd.default_params(shading=0)))
         variants["reference_semantics_no_shading_no_ert"] = dict(
-            value=round(f2["samples"] * args.steps / s2 / 1e9, 3), unit="Gsamples/s",
-            fps=round(args.steps / s2, 2), samples_per_frame=f2["samples"],
-            kernel_ms=round(k2, 4),
-            roofline_frac=round(algorithmic_bytes(r2, vbytes, shard_px) / (k2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+            value=round(V["frame"]["samples"] * args.steps / V["secs"] / 1e9, 3), unit="Gsamples/s",
+            ms_per_step=round(V["secs"] / args.steps * 1e3, 4),
+            fps=round(args.steps / V["secs"], 2), samples_per_frame=V["frame"]["samples"],
+            kernel_ms=round(V["kms"], 4), hbm_bytes_per_frame=rtr,
+            hbm_frac=round(rtr / (V["secs"] / args.steps) / 1e9 / HBM_PEAK_GBS, 4) if rtr else None)
         # opt-in empty-space skipping (bit-identical frames): executed samples drop, so it is
         # reported as fps and as reference-equivalent samples/s, never as the headline value
         scfg = dict(CONFIGS["c3"], skip_empty=1)
-        rp.transfer_function_changed(synth.TFS[scfg["tf"]]())
-        s3, k3, f3, r3, _, _ = run_variant(rp, scfg, args.steps, min(args.warmup, 5), rank, world,
-                                           inflight)
+        V = run_variant(rp, scfg, args.steps, min(args.warmup, 5), rank, world, inflight)
+        f3 = V["frame"]
         variants["c3_skip_empty"] = dict(
-            fps=round(args.steps / s3, 2), ms_per_step=round(s3 / args.steps * 1e3, 4),
-            kernel_ms=round(k3, 4),
-            executed_gsamples_per_s=round(f3["samples"] * args.steps / s3 / 1e9, 3),
+            fps=round(args.steps / V["secs"], 2), ms_per_step=round(V["secs"] / args.steps * 1e3, 4),
+            kernel_ms=round(V["kms"], 4),
+            executed_gsamples_per_s=round(f3["samples"] * args.steps / V["secs"] / 1e9, 3),
             reference_equivalent_gsamples_per_s=round(
-                (f3["samples"] + f3["skipped_samples"]) * args.steps / s3 / 1e9, 3),
+                (f3["samples"] + f3["skipped_samples"]) * args.steps / V["secs"] / 1e9, 3),
             samples_per_frame=f3["samples"], skipped_samples_per_frame=f3["skipped_samples"])
     if not args.no_variants and world == 1:
         # PCIe-inclusive: vr_render into (pageable) host memory, the drop-in record() path.
         # The frame's RGBA8 bytes cross PCIe inside the timed region; row bands copy while
         # the later bands render (vr_api.hip vr_render).  Never the headline value.
-        rp.transfer_function_changed(synth.TFS[cfg["tf"]]())
         hcam = synth.camera(cfg["cam"]).to_vr_camera()
         hp = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"])
         hbuf = np.empty((cfg["H"], cfg["W"], 4), dtype=np.uint8)
@@ -393,8 +469,18 @@ def main():
     small = int(np.prod(cfg["dims"])) <= 512 ** 3  # the oracle needs the volume as host floats
     if rank == 0 and world == 1 and not args.no_cpu_baseline and small:
         cpu = cpu_baseline(rp, cfg, args.cpu_budget)
+        # C1-C3 on the host cores, C1/C2 on smaller budgets
+        cpu["other_configs"] = {n: cpu_baseline_other(n, device, min(4.0, args.cpu_budget), cpu["cores"])
+                                for n in ("c1", "c2")}
 
     if rank == 0:
+        # Roofline: the kernel is bound by HBM by the SURVEY's classification (a gather, no
+        # MFMA).  `achieved` is the MEASURED DRAM traffic of one frame (rocprofv3 PMC
+        # FETCH_SIZE x2 + WRITE_SIZE, same build/config/camera, profiles/pmc_traffic.json) over
+        # this run's frame period, so frac = traffic / ms_per_step / 8 TB/s.  The SURVEY 8d
+        # gather model (8 x sizeof(voxel) per sample + 48 x sizeof(voxel) per shaded sample +
+        # 4 B/pixel) counts L1/L2 hits as well and is reported apart as gather_bytes_frac,
+        # which can exceed 1.
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -402,7 +488,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(secs / args.steps * 1e3, 4),
+            "ms_per_step": round(frame_s * 1e3, 4),
             "fps": round(fps, 2),
             "reference_equivalent_gsamples_per_s": round(ref_samples * args.steps / secs / 1e9, 3),
             "higher_is_better": True,
@@ -429,27 +515,27 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": rp.kernel_name(vr_amd.default_params(shading=cfg["shading"])),
-                "achieved": round(achieved, 1),
+                "kernel": kernel,
+                "achieved": round(traffic / frame_s / 1e9, 1) if traffic else None,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "frac": round(traffic / frame_s / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
                 "traffic": traffic,
-                "traffic_frac": (round(traffic / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                                 if traffic else None),
-                "traffic_frac_per_frame_period": (round(traffic / (secs / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
-                                                  if traffic else None),
-                "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"
-                                  if traffic else None,
+                "traffic_source": (f"profiles/pmc_traffic.json ({traffic_src}): rocprofv3 --pmc "
+                                   "FETCH_SIZE x2 + WRITE_SIZE per frame launch") if traffic else None,
+                "basis": "measured HBM bytes per frame / this run's ms_per_step / 8000 GB/s",
                 "kernel_ms": round(kms, 4),
-                # with frames in flight a kernel shares the device with its neighbours, so its
-                # duration exceeds the frame period; this is the same bytes per frame period
-                "achieved_per_frame_period": round(
-                    algorithmic_bytes(r0stats, vbytes, shard_px) / (secs / args.steps) / 1e9, 1),
-                "bytes_model": "8*sizeof(voxel)/sample + 48*sizeof(voxel)/shaded sample + 4 B/pixel (SURVEY.md 8d)",
+                "serial_kernel_ms": round(serial_kms, 4) if serial_kms else None,
+                "gather_bytes_per_frame": int(gather_bytes),
+                "gather_bytes_frac": (round(gather_bytes / (serial_kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                      if serial_kms else None),
+                "gather_bytes_model": "SURVEY.md 8d: 8*sizeof(voxel)/sample + 48*sizeof(voxel)/shaded "
+                                      "sample + 4 B/pixel, over the kernel-alone (serial) duration; "
+                                      "counts L1/L2 hits, so it can exceed 1 (not HBM traffic)",
             },
             "cpu_baseline": cpu,
-            "frame_check": frame_check,  # N > 1: assembled frame == single-GPU frame, bit for bit
+            "frame_check": R["check"],  # N > 1: assembled frame == single-GPU frame, bit for bit
+            "per_rank": R["per_rank"],
             "variants": variants,
         }
         print(json.dumps(out), flush=True)

@@ -176,6 +176,10 @@ uint64_t vr_volume_bytes(const vr_ctx *ctx);
 /* Debug/test helpers: read the resident volume back as dense float (x fastest, nx*ny*nz
  * floats); query dims, min/max and the storage type (0 u8, 1 i8, 2 u16, 3 i16, 4 f32). */
 int vr_debug_read_volume(vr_ctx *ctx, float *out_host);
+/* The same voxels in the storage type (u8/i8 -> 1 B, u16/i16 -> 2 B, everything else the f32
+ * conversion NrrdFileParser::convert makes), x fastest: 1/4 of the host memory for 8-bit
+ * volumes (C5 2048^3: 8 GiB). */
+int vr_debug_read_volume_native(vr_ctx *ctx, void *out_host);
 int vr_debug_volume_info(const vr_ctx *ctx, uint32_t dims[3], float minmax[2], int *storage);
 
 /* transfer_function_changed: n texels, RGBA8 sRGB, R in the low byte (ImGui packing,

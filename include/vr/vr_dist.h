@@ -61,6 +61,13 @@ int vr_dist_synchronize(vr_dist *d);
 
 const char *vr_dist_last_error(const vr_dist *d);
 
+/* Per-rank diagnostics (a straggler shows as a long render on its own rank and long gathers on
+ * the others): with timing enabled, every later frame brackets its render and its ncclGather
+ * with timing events on their streams.  vr_dist_timing_read waits for the outstanding frames,
+ * returns the summed milliseconds and the number of frames timed, and clears the record. */
+int vr_dist_timing_enable(vr_dist *d, int enable);
+int vr_dist_timing_read(vr_dist *d, double *render_ms, double *gather_ms, uint64_t *frames);
+
 /* Waits for outstanding frames, then frees the slots and the communicator. */
 void vr_dist_destroy(vr_dist *d);
 

@@ -218,15 +218,24 @@ static inline float lerpf(float a, float b, float w) { return fmaf(w, b - a, a);
 
 /* R32_SFLOAT 3D image, CLAMP_TO_BORDER with TRANSPARENT_BLACK (offscreen_pass.cpp:968,
  * 1016-1031): texels outside [0,N) read 0. */
-static inline float voxel(const float *v, int nx, int ny, int nz, int x, int y, int z)
+/* The Dataset's voxels: dense float (the reference's vector<float>), or u8 for the multi-GiB
+ * u8 configurations (C5: 8 GiB instead of a 32 GiB float copy; float(u8) is exact, so the
+ * samples are the same). */
+typedef struct vsrc {
+    const float *f;
+    const uint8_t *u8;
+} vsrc;
+
+static inline float voxel(const vsrc *v, int nx, int ny, int nz, int x, int y, int z)
 {
     if (x < 0 || y < 0 || z < 0 || x >= nx || y >= ny || z >= nz) return 0.0f;
-    return v[(size_t)x + (size_t)nx * ((size_t)y + (size_t)ny * (size_t)z)];
+    const size_t i = (size_t)x + (size_t)nx * ((size_t)y + (size_t)ny * (size_t)z);
+    return v->u8 ? (float)v->u8[i] : v->f[i];
 }
 
 /* Trilinear filter of the 2x2x2 cell whose low corner is (i,j,k), weights (ax,ay,az):
  * lerp along x, then y, then z. */
-static inline float tri_cell(const float *v, int nx, int ny, int nz, int i, int j, int k,
+static inline float tri_cell(const vsrc *v, int nx, int ny, int nz, int i, int j, int k,
                              float ax, float ay, float az)
 {
     float c00 = lerpf(voxel(v, nx, ny, nz, i, j, k), voxel(v, nx, ny, nz, i + 1, j, k), ax);
@@ -244,12 +253,12 @@ static inline float tri_cell(const float *v, int nx, int ny, int nz, int i, int 
  * tri(v(. + e)) - tri(v(. - e)) with the subtraction done per voxel: one rounding per
  * difference, then the filter.  (The device reads D from precomputed arrays for f32 volumes
  * and forms it from the 4-wide stencil otherwise; same operations either way.) */
-static inline float dvox(const float *v, int nx, int ny, int nz, int x, int y, int z, int axis)
+static inline float dvox(const vsrc *v, int nx, int ny, int nz, int x, int y, int z, int axis)
 {
     const int ex = axis == 0, ey = axis == 1, ez = axis == 2;
     return voxel(v, nx, ny, nz, x + ex, y + ey, z + ez) - voxel(v, nx, ny, nz, x - ex, y - ey, z - ez);
 }
-static inline float grad_cell(const float *v, int nx, int ny, int nz, int i, int j, int k,
+static inline float grad_cell(const vsrc *v, int nx, int ny, int nz, int i, int j, int k,
                               float ax, float ay, float az, int axis)
 {
     float c00 = lerpf(dvox(v, nx, ny, nz, i, j, k, axis), dvox(v, nx, ny, nz, i + 1, j, k, axis), ax);
@@ -284,7 +293,8 @@ float or_trilinear(const float *vol, int nx, int ny, int nz, float px, float py,
     texel_coord(px, nx, &i, &ax);
     texel_coord(py, ny, &j, &ay);
     texel_coord(pz, nz, &k, &az);
-    return tri_cell(vol, nx, ny, nz, i, j, k, ax, ay, az);
+    const vsrc src = {vol, NULL};
+    return tri_cell(&src, nx, ny, nz, i, j, k, ax, ay, az);
 }
 
 /* R8G8B8A8_SRGB texels (offscreen_pass.cpp:1076): RGB UNORM-decoded then sRGB->linear
@@ -356,6 +366,7 @@ static void march_pixel(const or_scene *s, const ray_frame *f, const float *lut,
     }
     st->rays++;
     const int nx = s->nx, ny = s->ny, nz = s->nz;
+    const vsrc src = {s->vol, s->vol_u8};
     const float step = s->step;
     const int nsteps = (int)(s->ray_dist / step); /* volume.frag:31 int(ray_dist/step_size) */
     const float range = s->vmax - s->vmin;
@@ -373,16 +384,16 @@ static void march_pixel(const or_scene *s, const ray_frame *f, const float *lut,
             texel_coord(p0, nx, &i, &ax);
             texel_coord(p1, ny, &j, &ay);
             texel_coord(p2, nz, &k, &az);
-            const float d = tri_cell(s->vol, nx, ny, nz, i, j, k, ax, ay, az); /* :41 */
+            const float d = tri_cell(&src, nx, ny, nz, i, j, k, ax, ay, az); /* :41 */
             const float t = (d - s->vmin) / range;                              /* :42 */
             float sc[4];
             tf_lookup(lut, s->tf_n, t, sc); /* :43 */
             st->samples++;
             if (s->shading && sc[3] > 0.0f) {
                 /* extension: central differences one texel apart, same weights (grad_cell) */
-                const float gx = grad_cell(s->vol, nx, ny, nz, i, j, k, ax, ay, az, 0);
-                const float gy = grad_cell(s->vol, nx, ny, nz, i, j, k, ax, ay, az, 1);
-                const float gz = grad_cell(s->vol, nx, ny, nz, i, j, k, ax, ay, az, 2);
+                const float gx = grad_cell(&src, nx, ny, nz, i, j, k, ax, ay, az, 0);
+                const float gy = grad_cell(&src, nx, ny, nz, i, j, k, ax, ay, az, 1);
+                const float gz = grad_cell(&src, nx, ny, nz, i, j, k, ax, ay, az, 2);
                 st->shaded_samples++;
                 const float wx = gx * (float)nx, wy = gy * (float)ny, wz = gz * (float)nz;
                 const float g2 = wx * wx + wy * wy + wz * wz;
@@ -421,7 +432,7 @@ static void march_pixel(const or_scene *s, const ray_frame *f, const float *lut,
 int or_render_rows(const or_scene *s, float *out, int row0, int row1, int nthreads,
                    or_stats *stats)
 {
-    if (!s || !out || !s->vol || !s->tf || s->tf_n <= 0 || s->width <= 0 || s->height <= 0)
+    if (!s || !out || !(s->vol || s->vol_u8) || !s->tf || s->tf_n <= 0 || s->width <= 0 || s->height <= 0)
         return -22;
     if (row0 < 0) row0 = 0;
     if (row1 > s->height) row1 = s->height;
@@ -458,7 +469,7 @@ int or_render_rows(const or_scene *s, float *out, int row0, int row1, int nthrea
 int or_render_row_list(const or_scene *s, float *out, const int32_t *rows, int nrows,
                        int nthreads, or_stats *stats)
 {
-    if (!s || !out || !rows || !s->vol || !s->tf || s->tf_n <= 0 || s->width <= 0 || s->height <= 0)
+    if (!s || !out || !rows || !(s->vol || s->vol_u8) || !s->tf || s->tf_n <= 0 || s->width <= 0 || s->height <= 0)
         return -22;
     ray_frame f;
     make_ray_frame(s, &f);

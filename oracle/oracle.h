@@ -53,6 +53,8 @@ typedef struct or_scene {
     float clear[4];
     float ka, kd, ks;
     int32_t spec_power;
+    /* u8 voxels instead of vol (same layout; float(v) exact), for multi-GiB u8 volumes */
+    const uint8_t *vol_u8;
 } or_scene;
 
 typedef struct or_stats {

@@ -94,3 +94,48 @@ def test_c4_1024_u8_2048_sharding_determinism_ert(gpu):
     # colour error <= T_stop * (C + 0.11 + 1) <= 2.2 eps (blend: out = C A + 0.11 (1 - A))
     assert np.abs(a.astype(np.float64) - e).max() <= 2.2e-3
     rp.close()
+
+
+def test_c5_2048_u8_4096_shards_determinism_ert_and_rows(gpu):
+    """C5: 2048^3 u8 (generated on the device, seed 11) at 4096x4096, the multi-GPU config:
+    8-way row-block shards reassemble the single-GPU frame bit for bit, repeated renders are
+    identical, ERT stays within its bound, and rows spread over the frame match the CPU oracle
+    marching the SAME 8 GiB of voxels (read back in their u8 storage type: float(u8) is exact,
+    so the oracle samples what the reference's float Dataset would hold)."""
+    import torch
+    W, H, N = 4096, 4096, 2048
+    rp = vr_amd.OffscreenPass(W, H)
+    lo, hi = rp.generate_volume((N, N, N), np.uint8, seed=11)
+    tf = synth.tf2()
+    rp.transfer_function_changed(tf)
+    cam = synth.camera("fill").to_vr_camera()
+    p = vr_amd.default_params()
+    full = torch.empty((H, W), dtype=torch.int32, device="cuda")
+    rp.render_device(cam, p, full.data_ptr(), vr_amd.OUT_RGBA8, 8, 0, 1)
+    again = torch.empty_like(full)
+    rp.render_device(cam, p, again.data_ptr(), vr_amd.OUT_RGBA8, 8, 0, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(full, again)
+    n = 8
+    sr = vr_amd.shard_rows(H, 8, n)
+    g = torch.empty((n, sr, W), dtype=torch.int32, device="cuda")
+    for r in range(n):
+        rp.render_device(cam, p, g[r].data_ptr(), vr_amd.OUT_RGBA8, 8, r, n)
+    out = torch.empty_like(full)
+    rp.assemble_rows(g.data_ptr(), out.data_ptr(), vr_amd.OUT_RGBA8, 8, n)
+    torch.cuda.synchronize()
+    assert torch.equal(out, full)
+    del g, out, again
+    # oracle rows: the resident voxels, u8
+    vol = rp.read_volume(native=True)
+    assert vol.dtype == np.uint8 and vol.shape == (N, N, N)
+    assert float(vol.min()) == lo and float(vol.max()) == hi
+    a = None
+    for q in (p, vr_amd.default_params(shading=1, ert_eps=1e-5)):
+        img = rows_parity(rp, vol, lo, hi, tf, cam, W, H, q, nrows=8)
+        if a is None:
+            a = img
+    # ERT at eps: colour error <= T_stop * (C + 0.11 + 1) <= 2.2 eps
+    e = rp.render(cam, vr_amd.default_params(ert_eps=1e-3))
+    assert np.abs(a.astype(np.float64) - e).max() <= 2.2e-3
+    rp.close()

@@ -134,3 +134,18 @@ def test_row_range_rendering_matches_full():
     assert np.array_equal(full[5:9], part[5:9])
     assert np.isnan(part[:5]).all() and np.isnan(part[9:]).all()
     assert st2["samples"] < st["samples"]
+
+
+def test_u8_voxel_source_equals_float_copy():
+    """The oracle's u8 voxel source (used for multi-GiB u8 volumes, e.g. C5) renders exactly
+    what the reference's float Dataset of the same voxels renders (float(u8) is exact)."""
+    import vr_amd
+    rng = np.random.default_rng(4)
+    vol = rng.integers(0, 256, size=(13, 11, 9), dtype=np.uint8)
+    cam = vr_amd.make_camera(radius=2.0, rotate=(100.0, 60.0)).to_vr_camera()
+    for shading in (0, 1):
+        p = vr_amd.default_params(shading=shading)
+        a, sa = pyoracle.Scene.from_params(vol, 0.0, 255.0, synth.tf_color(), cam, 40, 30, p).render()
+        b, sb = pyoracle.Scene.from_params(vol.astype(np.float32), 0.0, 255.0, synth.tf_color(),
+                                           cam, 40, 30, p).render()
+        assert np.array_equal(a, b) and sa == sb

@@ -1,44 +1,58 @@
 """Turn tools/measure_round.sh PMC passes into profiles/pmc_traffic.json (read by bench.py).
 
-HBM bytes per launch of the timed march kernel = 2 x FETCH_SIZE x 1024 (gfx950: FETCH_SIZE
-reads 1/2 of the bytes of 128-B requests, MI355X_MICROARCH.md §HBM) + WRITE_SIZE x 1024.
+HBM bytes per frame launch of the timed march kernel = 2 x FETCH_SIZE x 1024 (gfx950:
+FETCH_SIZE reads 1/2 of the bytes of 128-B requests, MI355X_MICROARCH.md §HBM) + WRITE_SIZE x
+1024, averaged over the dispatches of the configuration's frame kernel (the counting kernel
+that bench.py launches once for its work counters is excluded).  The passes run bench.py
+itself (--config X --no-variants), so the launches are the benchmark's own.
 Usage: python tools/traffic_json.py gpurun_out/<tag> [out.json]
 """
+import collections
 import csv
 import glob
 import json
 import os
 import sys
 
+CONFIGS = ("c3", "c3_ref", "c3_default", "c2", "c4")
 
-def mean_counter(d, name):
-    vals = []
-    for f in glob.glob(os.path.join(d, "run_counter_collection.csv")) + glob.glob(os.path.join(d, "*", "run_counter_collection.csv")):
+
+def frame_kernel(name):
+    """True for a march launch that renders a frame (not the COUNT instantiation)."""
+    for k in ("march_kernel<", "march_pair_kernel<", "march_lds_kernel<"):
+        if k in name:
+            targs = [t.strip() for t in name.split(k, 1)[1].split(">", 1)[0].split(",")]
+            return not (k == "march_kernel<" and targs[2] == "true")  # <VT, SHADE, COUNT, ...>
+    return False
+
+
+def counter(d, name):
+    vals, kernels = [], collections.Counter()
+    for f in glob.glob(os.path.join(d, "run_counter_collection.csv")) + glob.glob(
+            os.path.join(d, "*", "run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"]
-            if "march_kernel<" in k:
-                targs = [t.strip() for t in k.split("march_kernel<", 1)[1].split(">", 1)[0].split(",")]
-                if targs[2] == "true":  # <VT, SHADE, COUNT, SKIP>: the counting kernel is not timed
-                    continue
-                if r["Counter_Name"] == name:
-                    vals.append(float(r["Counter_Value"]))
-    return sum(vals) / len(vals) if vals else None
+            if frame_kernel(r["Kernel_Name"]) and r["Counter_Name"] == name:
+                vals.append(float(r["Counter_Value"]))
+                kernels[r["Kernel_Name"]] += 1
+    if not vals:
+        return None, None, 0
+    return sum(vals) / len(vals), kernels.most_common(1)[0][0], len(vals)
 
 
 def main():
     src = sys.argv[1]
     out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
-    res = {}
-    for cfg in ("c3", "c3_ref"):
-        f = mean_counter(os.path.join(src, f"pmc_{cfg}_FETCH_SIZE"), "FETCH_SIZE")
-        w = mean_counter(os.path.join(src, f"pmc_{cfg}_WRITE_SIZE"), "WRITE_SIZE")
+    res = json.load(open(out)) if os.path.exists(out) else {}
+    for cfg in CONFIGS:
+        f, kern, n = counter(os.path.join(src, f"pmc_{cfg}_FETCH_SIZE"), "FETCH_SIZE")
+        w, _, _ = counter(os.path.join(src, f"pmc_{cfg}_WRITE_SIZE"), "WRITE_SIZE")
         if f is None:
             continue
-        res[cfg] = dict(n_gpus=1, fetch_size_kb=f, write_size_kb=w,
+        res[cfg] = dict(n_gpus=1, kernel=kern, dispatches=n, fetch_size_kb=f, write_size_kb=w,
                         hbm_bytes_per_launch=2 * f * 1024 + (w or 0) * 1024,
                         method="rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate runs of "
-                               "tools/prof_run.py (10 frames), mean over dispatches of the timed "
-                               "march kernel; FETCH_SIZE x2 gfx950 correction",
+                               f"bench.py --config {cfg} --no-variants, mean over the frame "
+                               "kernel's dispatches; FETCH_SIZE x2 gfx950 correction",
                         source=src)
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))

@@ -903,34 +903,43 @@ int vr_generate_volume(vr_ctx *c, int kind, int dtype, uint32_t nx, uint32_t ny,
 
 uint64_t vr_volume_bytes(const vr_ctx *c) { return c ? (uint64_t)c->brick_bytes : 0; }
 
-int vr_debug_read_volume(vr_ctx *c, float *out)
+int vr_debug_read_volume_native(vr_ctx *c, void *out)
 {
     if (!c || !out) return fail(c, VR_EINVAL, "NULL argument");
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
-    std::vector<unsigned char> host(c->brick_bytes);
-    HIP_TRY(c, hipMemcpy(host.data(), c->bricks, c->brick_bytes, hipMemcpyDeviceToHost),
-            "hipMemcpy(bricks)");
-    const uint32_t nbx = bricks_for(c->nx), nby = bricks_for(c->ny);
-    const size_t es = element_size(c->storage);  // component 0 of element (x,y,z) is v(x,y,z)
-    for (uint32_t z = 0; z < c->nz; ++z)
-        for (uint32_t y = 0; y < c->ny; ++y)
-            for (uint32_t x = 0; x < c->nx; ++x) {
-                const uint32_t pi = x + kPad, pj = y + kPad, pk = z + kPad;
-                const size_t b = ((size_t)(pk >> kBrickShift) * nby + (pj >> kBrickShift)) * nbx +
-                                 (pi >> kBrickShift);
-                const size_t l = ((size_t)(pk & (kBrick - 1)) * kStore + (pj & (kBrick - 1))) * kStore +
-                                 (pi & (kBrick - 1));
-                const unsigned char *src = host.data() + (b * kBrickElems + l) * es;
-                float v;
-                switch (c->storage) {
-                    case ST_U8: v = (float)*(const uint8_t *)src; break;
-                    case ST_I8: v = (float)*(const int8_t *)src; break;
-                    case ST_U16: { uint16_t t; std::memcpy(&t, src, 2); v = (float)t; } break;
-                    case ST_I16: { int16_t t; std::memcpy(&t, src, 2); v = (float)t; } break;
-                    default: std::memcpy(&v, src, 4); break;
-                }
-                out[(size_t)x + (size_t)c->nx * ((size_t)y + (size_t)c->ny * z)] = v;
-            }
+    // unbricked on the device in slabs of z-slices (<= 256 MiB of scratch), then copied out
+    const size_t vb = storage_size(c->storage), slice = (size_t)c->nx * c->ny * vb;
+    const uint32_t cz = (uint32_t)std::max<size_t>(1, std::min<size_t>(c->nz, (256u << 20) / slice));
+    void *tmp = nullptr;
+    HIP_TRY(c, hipMalloc(&tmp, slice * cz), "hipMalloc(readback)");
+    int rc = VR_OK;
+    for (uint32_t z0 = 0; z0 < c->nz && rc == VR_OK; z0 += cz) {
+        const uint32_t n = std::min(cz, c->nz - z0);
+        hipError_t e = launch_unbrick(c->storage, c->bricks, tmp, c->nx, c->ny, z0, n, nullptr);
+        if (e == hipSuccess)
+            e = hipMemcpy(static_cast<char *>(out) + slice * z0, tmp, slice * n, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = hip_fail(c, e, "read volume");
+    }
+    hipFree(tmp);
+    return rc;
+}
+
+int vr_debug_read_volume(vr_ctx *c, float *out)
+{
+    if (!c || !out) return fail(c, VR_EINVAL, "NULL argument");
+    const size_t n = (size_t)c->nx * c->ny * c->nz;
+    if (c->storage == ST_F32) return vr_debug_read_volume_native(c, out);
+    std::vector<unsigned char> host(n * storage_size(c->storage));
+    const int rc = vr_debug_read_volume_native(c, host.data());
+    if (rc) return rc;
+    for (size_t i = 0; i < n; ++i) {  // float(v) is exact for 8/16-bit voxels
+        switch (c->storage) {
+            case ST_U8: out[i] = (float)host[i]; break;
+            case ST_I8: out[i] = (float)(int8_t)host[i]; break;
+            case ST_U16: { uint16_t t; std::memcpy(&t, &host[2 * i], 2); out[i] = (float)t; } break;
+            default: { int16_t t; std::memcpy(&t, &host[2 * i], 2); out[i] = (float)t; } break;
+        }
+    }
     return VR_OK;
 }
 

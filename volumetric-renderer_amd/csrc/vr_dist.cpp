@@ -21,6 +21,8 @@
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
+#include "vr_frame_schedule.h"
+
 #include <cstring>
 #include <new>
 #include <string>
@@ -76,11 +78,27 @@ Rccl &rccl()
     return r;
 }
 
-struct Slot {
-    hipStream_t stream = nullptr;
+struct Buffers {
     void *shard = nullptr;  // shard_rows x W RGBA8
     void *gbuf = nullptr;   // rank 0: nranks shards, rank-major
-    hipEvent_t rendered = nullptr, gathered = nullptr, done = nullptr;
+};
+
+// Timing pairs (vr_dist_timing_enable): recorded per frame on the op's stream, read and freed
+// by vr_dist_timing_read.
+struct TimedOp {
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+};
+
+// HIP + RCCL executor of vr::sched::FrameSchedule (members defined below vr_dist).
+struct HipExec {
+    using Stream = hipStream_t;
+    using Event = hipEvent_t;
+    vr_dist *d = nullptr;
+    int record(Event e, Stream s);
+    int wait(Stream s, Event e);
+    int render(int slot, uint64_t frame, Stream s);
+    int gather(int slot, uint64_t frame, Stream s);
+    int assemble(int slot, uint64_t frame, void *frame_dev, Stream s);
 };
 
 }  // namespace
@@ -91,10 +109,12 @@ struct vr_dist {
     int nranks = 1, rank = 0;
     uint32_t row_block = 8, width = 0, height = 0, shard_rows = 0;
     ncclComm_t comm = nullptr;
-    hipStream_t comm_stream = nullptr;
-    hipEvent_t called = nullptr;
-    std::vector<Slot> slots;
-    uint64_t frame = 0;
+    std::vector<Buffers> bufs;  // per slot
+    vr::sched::FrameSchedule<HipExec> sched;
+    const vr_camera *cam = nullptr;  // the frame being issued
+    const vr_params *params = nullptr;
+    bool timing = false;
+    std::vector<TimedOp> t_render, t_gather;
     std::string err;
 };
 
@@ -128,25 +148,90 @@ int nccl_check(vr_dist *d, ncclResult_t r, const char *what)
         if (_rc != VR_OK) return _rc; \
     } while (0)
 
+// With timing on, a pair of timing events brackets the op on its stream.
+int timed_begin(vr_dist *d, std::vector<TimedOp> &v, hipStream_t s)
+{
+    if (!d->timing) return VR_OK;
+    TimedOp t;
+    DTRY(hip_check(d, hipEventCreate(&t.t0), "hipEventCreate"));
+    if (hipEventCreate(&t.t1) != hipSuccess) {
+        hipEventDestroy(t.t0);
+        return dfail(d, VR_EIO, "hipEventCreate");
+    }
+    v.push_back(t);
+    return hip_check(d, hipEventRecord(t.t0, s), "hipEventRecord");
+}
+int timed_end(vr_dist *d, std::vector<TimedOp> &v, hipStream_t s)
+{
+    if (!d->timing) return VR_OK;
+    return hip_check(d, hipEventRecord(v.back().t1, s), "hipEventRecord");
+}
+
+int HipExec::record(Event e, Stream s) { return hip_check(d, hipEventRecord(e, s), "hipEventRecord"); }
+int HipExec::wait(Stream s, Event e)
+{
+    return hip_check(d, hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent");
+}
+int HipExec::render(int slot, uint64_t, Stream s)
+{
+    vr_params q = *d->params;
+    q.frames_in_flight = (int32_t)d->sched.slots.size();
+    DTRY(timed_begin(d, d->t_render, s));
+    if (vr_render_device(d->ctx, d->cam, &q, d->bufs[slot].shard, VR_OUT_RGBA8, d->row_block,
+                         (uint32_t)d->rank, (uint32_t)d->nranks, s) != VR_OK)
+        return dfail(d, VR_EIO, std::string("render: ") + vr_last_error(d->ctx));
+    return timed_end(d, d->t_render, s);
+}
+int HipExec::gather(int slot, uint64_t, Stream s)
+{
+    const Buffers &b = d->bufs[slot];
+    DTRY(timed_begin(d, d->t_gather, s));
+    DTRY(nccl_check(d, rccl().gather(b.shard, d->rank == 0 ? b.gbuf : nullptr,
+                                     (size_t)d->shard_rows * d->width, ncclUint32, 0, d->comm, s),
+                    "ncclGather"));
+    return timed_end(d, d->t_gather, s);
+}
+int HipExec::assemble(int slot, uint64_t, void *frame_dev, Stream s)
+{
+    if (vr_assemble_rows(d->ctx, d->bufs[slot].gbuf, frame_dev, VR_OUT_RGBA8, d->row_block,
+                         (uint32_t)d->nranks, s) != VR_OK)
+        return dfail(d, VR_EIO, std::string("assemble: ") + vr_last_error(d->ctx));
+    return VR_OK;
+}
+
+void free_timing(vr_dist *d)
+{
+    for (auto *v : {&d->t_render, &d->t_gather}) {
+        for (auto &t : *v) {
+            hipEventDestroy(t.t0);
+            hipEventDestroy(t.t1);
+        }
+        v->clear();
+    }
+}
+
 void release(vr_dist *d)
 {
     hipSetDevice(d->device);
-    for (auto &s : d->slots) {
+    auto &S = d->sched;
+    for (auto &s : S.slots)
         if (s.stream) hipStreamSynchronize(s.stream);
-    }
-    if (d->comm_stream) hipStreamSynchronize(d->comm_stream);
+    if (S.comm) hipStreamSynchronize(S.comm);
     if (d->comm) rccl().comm_destroy(d->comm);
-    for (auto &s : d->slots) {
-        if (s.shard) hipFree(s.shard);
-        if (s.gbuf) hipFree(s.gbuf);
-        if (s.rendered) hipEventDestroy(s.rendered);
-        if (s.gathered) hipEventDestroy(s.gathered);
-        if (s.done) hipEventDestroy(s.done);
+    free_timing(d);
+    for (auto &b : d->bufs) {
+        if (b.shard) hipFree(b.shard);
+        if (b.gbuf) hipFree(b.gbuf);
+    }
+    for (auto &s : S.slots) {
+        for (hipEvent_t e : {s.rendered, s.gathered, s.done})
+            if (e) hipEventDestroy(e);
         if (s.stream) hipStreamDestroy(s.stream);
     }
-    if (d->called) hipEventDestroy(d->called);
-    if (d->comm_stream) hipStreamDestroy(d->comm_stream);
-    d->slots.clear();
+    if (S.called) hipEventDestroy(S.called);
+    if (S.comm) hipStreamDestroy(S.comm);
+    S.slots.clear();
+    d->bufs.clear();
 }
 
 int setup(vr_dist *d, const void *id, int frames)
@@ -156,17 +241,22 @@ int setup(vr_dist *d, const void *id, int frames)
     static_assert(sizeof(uid) == VR_DIST_ID_BYTES, "ncclUniqueId size");
     std::memcpy(&uid, id, sizeof(uid));
     DTRY(nccl_check(d, rccl().comm_init_rank(&d->comm, d->nranks, uid, d->rank), "ncclCommInitRank"));
-    DTRY(hip_check(d, hipStreamCreateWithFlags(&d->comm_stream, hipStreamNonBlocking),
+    auto &S = d->sched;
+    S.rank = d->rank;
+    DTRY(hip_check(d, hipStreamCreateWithFlags(&S.comm, hipStreamNonBlocking),
                    "hipStreamCreate(comm)"));
-    DTRY(hip_check(d, hipEventCreateWithFlags(&d->called, hipEventDisableTiming), "hipEventCreate"));
+    DTRY(hip_check(d, hipEventCreateWithFlags(&S.called, hipEventDisableTiming), "hipEventCreate"));
     const size_t shard_bytes = (size_t)d->shard_rows * d->width * 4;
-    d->slots.resize(frames);
-    for (auto &s : d->slots) {
+    S.slots.resize(frames);
+    d->bufs.resize(frames);
+    for (int k = 0; k < frames; ++k) {
+        auto &s = S.slots[k];
+        auto &b = d->bufs[k];
         DTRY(hip_check(d, hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking),
                        "hipStreamCreate(slot)"));
-        DTRY(hip_check(d, hipMalloc(&s.shard, shard_bytes), "hipMalloc(shard)"));
+        DTRY(hip_check(d, hipMalloc(&b.shard, shard_bytes), "hipMalloc(shard)"));
         if (d->rank == 0)
-            DTRY(hip_check(d, hipMalloc(&s.gbuf, shard_bytes * d->nranks), "hipMalloc(gather)"));
+            DTRY(hip_check(d, hipMalloc(&b.gbuf, shard_bytes * d->nranks), "hipMalloc(gather)"));
         for (hipEvent_t *e : {&s.rendered, &s.gathered, &s.done})
             DTRY(hip_check(d, hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate"));
     }
@@ -238,41 +328,50 @@ int vr_dist_render(vr_dist *d, const vr_camera *cam, const vr_params *p, void *f
     if (vr_get_size(d->ctx, &w, &h) != VR_OK || w != d->width || h != d->height)
         return dfail(d, VR_EINVAL, "the context was resized: create a new vr_dist");
     DTRY(hip_check(d, hipSetDevice(d->device), "hipSetDevice"));
-    hipStream_t caller = static_cast<hipStream_t>(stream);
-    Slot &s = d->slots[d->frame % d->slots.size()];
-    vr_params q = *p;
-    q.frames_in_flight = (int32_t)d->slots.size();
-    if (vr_render_device(d->ctx, cam, &q, s.shard, VR_OUT_RGBA8, d->row_block, (uint32_t)d->rank,
-                         (uint32_t)d->nranks, s.stream) != VR_OK)
-        return dfail(d, VR_EIO, std::string("render: ") + vr_last_error(d->ctx));
-    DTRY(hip_check(d, hipEventRecord(s.rendered, s.stream), "hipEventRecord"));
-    DTRY(hip_check(d, hipStreamWaitEvent(d->comm_stream, s.rendered, 0), "hipStreamWaitEvent"));
-    DTRY(nccl_check(d, rccl().gather(s.shard, d->rank == 0 ? s.gbuf : nullptr,
-                                     (size_t)d->shard_rows * d->width, ncclUint32, 0, d->comm,
-                                     d->comm_stream),
-                    "ncclGather"));
-    DTRY(hip_check(d, hipEventRecord(s.gathered, d->comm_stream), "hipEventRecord"));
-    DTRY(hip_check(d, hipStreamWaitEvent(s.stream, s.gathered, 0), "hipStreamWaitEvent"));
-    if (d->rank == 0) {
-        // the caller's earlier work on `stream` (e.g. reading frame_dev) precedes the write
-        DTRY(hip_check(d, hipEventRecord(d->called, caller), "hipEventRecord"));
-        DTRY(hip_check(d, hipStreamWaitEvent(s.stream, d->called, 0), "hipStreamWaitEvent"));
-        if (vr_assemble_rows(d->ctx, s.gbuf, frame_dev, VR_OUT_RGBA8, d->row_block,
-                             (uint32_t)d->nranks, s.stream) != VR_OK)
-            return dfail(d, VR_EIO, std::string("assemble: ") + vr_last_error(d->ctx));
-    }
-    DTRY(hip_check(d, hipEventRecord(s.done, s.stream), "hipEventRecord"));
-    DTRY(hip_check(d, hipStreamWaitEvent(caller, s.done, 0), "hipStreamWaitEvent"));
-    d->frame++;
-    return VR_OK;
+    d->cam = cam;
+    d->params = p;
+    HipExec x{d};
+    const int rc = d->sched.issue(x, static_cast<hipStream_t>(stream), frame_dev);
+    d->cam = nullptr;
+    d->params = nullptr;
+    return rc;
 }
 
 int vr_dist_synchronize(vr_dist *d)
 {
     if (!d) return dfail(nullptr, VR_EINVAL, "dist is NULL");
     DTRY(hip_check(d, hipSetDevice(d->device), "hipSetDevice"));
-    for (auto &s : d->slots) DTRY(hip_check(d, hipStreamSynchronize(s.stream), "hipStreamSynchronize"));
-    return hip_check(d, hipStreamSynchronize(d->comm_stream), "hipStreamSynchronize");
+    for (auto &s : d->sched.slots)
+        DTRY(hip_check(d, hipStreamSynchronize(s.stream), "hipStreamSynchronize"));
+    return hip_check(d, hipStreamSynchronize(d->sched.comm), "hipStreamSynchronize");
+}
+
+int vr_dist_timing_enable(vr_dist *d, int enable)
+{
+    if (!d) return dfail(nullptr, VR_EINVAL, "dist is NULL");
+    d->timing = enable != 0;
+    return VR_OK;
+}
+
+int vr_dist_timing_read(vr_dist *d, double *render_ms, double *gather_ms, uint64_t *frames)
+{
+    if (!d) return dfail(nullptr, VR_EINVAL, "dist is NULL");
+    DTRY(vr_dist_synchronize(d));
+    double acc[2] = {0.0, 0.0};
+    int i = 0;
+    for (auto *v : {&d->t_render, &d->t_gather}) {
+        for (auto &t : *v) {
+            float ms = 0.0f;
+            DTRY(hip_check(d, hipEventElapsedTime(&ms, t.t0, t.t1), "hipEventElapsedTime"));
+            acc[i] += ms;
+        }
+        ++i;
+    }
+    if (render_ms) *render_ms = acc[0];
+    if (gather_ms) *gather_ms = acc[1];
+    if (frames) *frames = d->t_render.size();
+    free_timing(d);
+    return VR_OK;
 }
 
 const char *vr_dist_last_error(const vr_dist *d) { return d ? d->err.c_str() : g_dist_err.c_str(); }

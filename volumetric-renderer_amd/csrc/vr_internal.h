@@ -152,6 +152,9 @@ constexpr uint32_t kPairMaxWaves = 24576;
 constexpr uint32_t kPairQuadMaxWaves = 6144;  // below: 4 lanes per ray
 hipError_t launch_brick_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,
                                     uint32_t ny, uint32_t nz, int storage, hipStream_t stream);
+// Bricked volume -> linear x-fastest voxels of the storage type, slices [z0, z0 + cz).
+hipError_t launch_unbrick(int storage, const void *bricks, void *dst, uint32_t nx, uint32_t ny,
+                          uint32_t z0, uint32_t cz, hipStream_t stream);
 // Synthetic volume into a LINEAR buffer of the storage type (then bricked).
 hipError_t launch_generate(int kind, int storage, void *dst_linear, uint32_t nx, uint32_t ny,
                            uint32_t nz, const float *params_dev, int nparams,

@@ -1475,6 +1475,29 @@ inline unsigned grid_for(size_t total)
     return (unsigned)(g > 2048 * 8 ? 2048 * 8 : (g == 0 ? 1 : g));
 }
 
+// Readback (vr_debug_read_volume*): voxel v(x, y, z) is component 0 of element (x, y, z) of the
+// bricked layout; slices [z0, z0 + cz) into a linear x-fastest buffer of the storage type.
+template <typename T>
+__global__ __launch_bounds__(256) void unbrick_kernel(const T *__restrict__ bricks,
+                                                     T *__restrict__ dst, uint32_t nx,
+                                                     uint32_t ny, uint32_t nbx, uint32_t nby,
+                                                     uint32_t z0, size_t count)
+{
+    constexpr size_t vpe = std::is_same<T, float>::value ? kF32VoxelsPerElement : 4;
+    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < count;
+         g += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t x = (uint32_t)(g % nx);
+        const size_t yz = g / nx;
+        const uint32_t y = (uint32_t)(yz % ny), z = z0 + (uint32_t)(yz / ny);
+        const uint32_t pi = x + kPad, pj = y + kPad, pk = z + kPad;
+        const size_t b = ((size_t)(pk >> kBrickShift) * nby + (pj >> kBrickShift)) * nbx +
+                         (pi >> kBrickShift);
+        const size_t l = ((size_t)(pk & (kBrick - 1)) * kStore + (pj & (kBrick - 1))) * kStore +
+                         (pi & (kBrick - 1));
+        dst[g] = bricks[(b * kBrickElems + l) * vpe];
+    }
+}
+
 template <typename SrcT>
 hipError_t brick_from(const void *src, void *dst, uint32_t nx, uint32_t ny, uint32_t nz,
                       int storage, hipStream_t s)
@@ -1524,6 +1547,20 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
     if (storage < 0 || storage > 4) return "march_kernel<?>";
     const int k = (shade ? 16 : 0) + (count ? 8 : 0) + (skip ? 4 : 0) + (gf ? 2 : 0) + (pipe ? 1 : 0);
     return names[storage * 32 + k].c_str();
+}
+
+hipError_t launch_unbrick(int storage, const void *bricks, void *dst, uint32_t nx, uint32_t ny,
+                          uint32_t z0, uint32_t cz, hipStream_t s)
+{
+    const size_t n = (size_t)nx * ny * cz;
+    const unsigned g = grid_for(n);
+    const uint32_t bx = bricks_for(nx), by = bricks_for(ny);
+    switch (storage) {
+        case ST_U8: case ST_I8: hipLaunchKernelGGL((unbrick_kernel<uint8_t>), dim3(g), dim3(256), 0, s, (const uint8_t *)bricks, (uint8_t *)dst, nx, ny, bx, by, z0, n); break;
+        case ST_U16: case ST_I16: hipLaunchKernelGGL((unbrick_kernel<uint16_t>), dim3(g), dim3(256), 0, s, (const uint16_t *)bricks, (uint16_t *)dst, nx, ny, bx, by, z0, n); break;
+        default: hipLaunchKernelGGL((unbrick_kernel<float>), dim3(g), dim3(256), 0, s, (const float *)bricks, (float *)dst, nx, ny, bx, by, z0, n); break;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_brick_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,

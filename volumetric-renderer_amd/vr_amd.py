@@ -70,7 +70,7 @@ class vr_dataset(C.Structure):
 ABI_SYMBOLS = [
     "vr_abi_version", "vr_params_default", "vr_create", "vr_destroy", "vr_last_error",
     "vr_resize", "vr_get_size", "vr_get_device", "vr_set_volume", "vr_set_volume_device", "vr_generate_volume",
-    "vr_volume_bytes", "vr_debug_read_volume", "vr_debug_volume_info",
+    "vr_volume_bytes", "vr_debug_read_volume", "vr_debug_read_volume_native", "vr_debug_volume_info",
     "vr_set_transfer_function", "vr_set_slicing", "vr_render", "vr_render_device",
     "vr_shard_rows", "vr_assemble_rows", "vr_count_work", "vr_timing_enable",
     "vr_timing_read", "vr_timing_reset", "vr_kernel_name",
@@ -87,7 +87,7 @@ HOST_SYMBOLS = [
 
 DIST_SYMBOLS = [
     "vr_dist_unique_id", "vr_dist_create", "vr_dist_render", "vr_dist_synchronize",
-    "vr_dist_last_error", "vr_dist_destroy",
+    "vr_dist_last_error", "vr_dist_destroy", "vr_dist_timing_enable", "vr_dist_timing_read",
 ]
 DIST_ID_BYTES = 128  # include/vr/vr_dist.h VR_DIST_ID_BYTES
 
@@ -129,11 +129,15 @@ def lib() -> C.CDLL:
         "vr_dist_synchronize": (i32, [vp]),
         "vr_dist_last_error": (C.c_char_p, [vp]),
         "vr_dist_destroy": (None, [vp]),
+        "vr_dist_timing_enable": (i32, [vp, i32]),
+        "vr_dist_timing_read": (i32, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                      C.POINTER(C.c_uint64)]),
         "vr_set_volume": (i32, [vp, vp, i32, u32, u32, u32, f32, f32]),
         "vr_set_volume_device": (i32, [vp, vp, i32, u32, u32, u32, f32, f32, vp]),
         "vr_generate_volume": (i32, [vp, i32, i32, u32, u32, u32, u32, C.POINTER(f32), C.POINTER(f32)]),
         "vr_volume_bytes": (C.c_uint64, [vp]),
         "vr_debug_read_volume": (i32, [vp, vp]),
+        "vr_debug_read_volume_native": (i32, [vp, vp]),
         "vr_debug_volume_info": (i32, [vp, C.POINTER(u32), C.POINTER(f32), C.POINTER(i32)]),
         "vr_set_transfer_function": (i32, [vp, C.POINTER(u32), u32]),
         "vr_set_slicing": (i32, [vp, C.POINTER(f32), C.POINTER(f32)]),
@@ -395,9 +399,17 @@ class OffscreenPass:
                                              C.byref(lo), C.byref(hi)), "vr_generate_volume")
         return float(lo.value), float(hi.value)
 
-    def read_volume(self) -> np.ndarray:
+    def read_volume(self, native: bool = False) -> np.ndarray:
+        """The resident volume as (nz, ny, nx) float32, or (native=True) in its storage type
+        (uint8/int8/uint16/int16/float32: 1/4 of the host memory for 8-bit volumes)."""
         dims, mm, st = self.volume_info()
-        out = np.empty((dims[2], dims[1], dims[0]), dtype=np.float32)
+        shape = (dims[2], dims[1], dims[0])
+        if native:
+            out = np.empty(shape, dtype=(np.uint8, np.int8, np.uint16, np.int16, np.float32)[st])
+            self._check(lib().vr_debug_read_volume_native(self._ctx, out.ctypes.data),
+                        "vr_debug_read_volume_native")
+            return out
+        out = np.empty(shape, dtype=np.float32)
         self._check(lib().vr_debug_read_volume(self._ctx, out.ctypes.data), "vr_debug_read_volume")
         return out
 
@@ -515,6 +527,17 @@ class DistFrames:
 
     def synchronize(self):
         self._check(lib().vr_dist_synchronize(self._d), "vr_dist_synchronize")
+
+    def timing_enable(self, on: bool = True):
+        self._check(lib().vr_dist_timing_enable(self._d, 1 if on else 0), "vr_dist_timing_enable")
+
+    def timing_read(self):
+        """(render ms, gather ms, frames) summed over the frames since timing was enabled (or
+        last read): HIP events around this rank's render and its ncclGather."""
+        r, g, n = C.c_double(), C.c_double(), C.c_uint64()
+        self._check(lib().vr_dist_timing_read(self._d, C.byref(r), C.byref(g), C.byref(n)),
+                    "vr_dist_timing_read")
+        return r.value, g.value, n.value
 
     def close(self):
         if getattr(self, "_d", None):
