@@ -1,19 +1,52 @@
 // offscreen_pass_hip.hpp — header-only C++ drop-in for Vol::Rendering::OffscreenPass
 // (reference: src/rendering/offscreen_pass.h:27-148) over the C ABI in vr.h.
 //
-// Same public method names, argument meaning and error behaviour as the reference: every
-// failure throws std::runtime_error (the reference throws on every failed vk* call), zero
-// framebuffer sizes are ignored, the constructor installs the 1x1x1 {0} volume and the
-// 1-texel 0xFFFFFFFF transfer function.  What changes at the boundary:
-//   * record(VkCommandBuffer, frame) becomes record(const Camera&) — the reference pulls the
-//     camera from Application::main() inside update_uniform_buffer (offscreen_pass.cpp:1155);
-//     here the caller passes Camera::get_view()/get_position() explicitly;
-//   * get_sampler()/get_image_view() become image(): the RGBA8 frame in host memory (or
-//     record_device() into a caller-owned device buffer) for the presentation layer.
-// No glm dependency: the caller converts glm types with glm::value_ptr.
+// The public surface is the reference's, with the same call shapes (offscreen_pass.h:40-54):
+//
+//   OffscreenPass(VulkanContext *context, uint32_t width, uint32_t height);
+//   void record(VkCommandBuffer command_buffer, uint32_t frame_index);
+//   void framebuffer_size_changed(uint32_t width, uint32_t height);
+//   void volume_dataset_changed(Vol::Data::Dataset &dataset);
+//   void slicing_changed(const glm::vec3 &min, const glm::vec3 &max);
+//   void transfer_function_changed(const std::vector<glm::uint32_t> &data);
+//   VkSampler get_sampler() const;   VkImageView get_image_view() const;
+//
+// so the reference's callers (vulkan_context.cpp:51, main_pass.cpp:91, imgui_context.cpp:67-74
+// and :130-135, importer.cpp:43-46, main_window.cpp:233-238 and :250-257) compile unchanged
+// against it (tests/shim/reference_call_shapes.cpp holds those lines verbatim).  The header
+// carries no Vulkan, glm or SDL dependency: the host's types come in through a Traits class,
+//
+//   struct Traits {
+//     using Context = VulkanContext;            // constructor's first argument
+//     using CommandBuffer = VkCommandBuffer;    // record()'s first argument
+//     using Sampler = VkSampler;  using ImageView = VkImageView;
+//     static Camera camera();                   // pulled once per record(), as
+//                                               // update_uniform_buffer pulls
+//                                               // Application::main().get_scene().get_camera()
+//                                               // (offscreen_pass.cpp:1155)
+//     struct Presenter {                        // the host's colour attachment + sampler
+//       Presenter(Context *, uint32_t w, uint32_t h);   // create_color_attachment & co.
+//       void resize(uint32_t w, uint32_t h);             // framebuffer_size_changed
+//       void present(CommandBuffer, uint32_t frame_index, const FrameImage &);
+//                                               // staging buffer + copy_buffer_to_image
+//                                               // (offscreen_pass.cpp:1379-1406)
+//       Sampler get_sampler() const;  ImageView get_image_view() const;
+//     };
+//   };
+//
+// and `using OffscreenPass = Vol::Rendering::Hip::BasicOffscreenPass<Traits>;`.  The HIP
+// ray-march renders each frame (the reference's cube draw + volume.frag) into R8G8B8A8_UNORM
+// pixels, get_image() is the handle to them, and the Presenter puts them where ImGui samples
+// them.  Error behaviour as the reference: every failure throws std::runtime_error, zero
+// framebuffer sizes are ignored (offscreen_pass.cpp:237-239), and construction installs the
+// 1x1x1 {0} volume and the 1-texel 0xFFFFFFFF transfer function (:118-119).
+//
+// `HeadlessTraits` (no Vulkan: frames stay in host memory, camera from a callback) serves the
+// CLI and tests; `OffscreenPass` below is BasicOffscreenPass<HeadlessTraits>.
 #pragma once
 
 #include <cstdint>
+#include <functional>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -34,35 +67,70 @@ struct Camera {
     float position[3];  // Camera::get_position (camera.cpp:36-40)
 };
 
-class OffscreenPass {
+// The frame record() produced: W*H R8G8B8A8_UNORM pixels (R in the low byte), row 0 at the
+// top, in host memory owned by the pass (valid until the next record() or resize).
+struct FrameImage {
+    const uint32_t *rgba8 = nullptr;
+    uint32_t width = 0, height = 0;
+    uint32_t frame_index = 0;  // the frame_index record() was called with
+    uint64_t frame = 0;        // frames recorded so far
+};
+
+// No Vulkan: frames stay in host memory; the camera comes from a settable callback.
+struct HeadlessTraits {
+    using Context = void;
+    using CommandBuffer = void *;
+    using Sampler = const FrameImage *;
+    using ImageView = const FrameImage *;
+    static std::function<Camera()> &camera_source()
+    {
+        static std::function<Camera()> f;
+        return f;
+    }
+    static Camera camera()
+    {
+        if (!camera_source()) throw std::runtime_error("HeadlessTraits: no camera source set");
+        return camera_source()();
+    }
+    struct Presenter {
+        FrameImage last;
+        Presenter(Context *, uint32_t, uint32_t) {}
+        void resize(uint32_t, uint32_t) { last = FrameImage{}; }
+        void present(CommandBuffer, uint32_t, const FrameImage &img) { last = img; }
+        Sampler get_sampler() const { return &last; }
+        ImageView get_image_view() const { return &last; }
+    };
+};
+
+template <class Traits>
+class BasicOffscreenPass {
   public:
-    OffscreenPass(uint32_t width, uint32_t height, int device = 0)
-        : ctx_(vr_create(device, width, height)), width_(width), height_(height)
+    using Context = typename Traits::Context;
+    using CommandBuffer = typename Traits::CommandBuffer;
+    using Sampler = typename Traits::Sampler;
+    using ImageView = typename Traits::ImageView;
+
+    // offscreen_pass.cpp:112-134 (the device is the ctx's: `device`, default 0)
+    explicit BasicOffscreenPass(Context *context, uint32_t width, uint32_t height, int device = 0)
+        : ctx_(vr_create(device, width, height)), presenter_(context, width, height),
+          width_(width), height_(height)
     {
         if (!ctx_) throw std::runtime_error(std::string("vr_create: ") + vr_last_error(nullptr));
         vr_params_default(&params_);
     }
-    ~OffscreenPass() { vr_destroy(ctx_); }
-    OffscreenPass(const OffscreenPass &) = delete;
-    OffscreenPass &operator=(const OffscreenPass &) = delete;
+    ~BasicOffscreenPass() { vr_destroy(ctx_); }
+    BasicOffscreenPass(const BasicOffscreenPass &) = delete;
+    BasicOffscreenPass &operator=(const BasicOffscreenPass &) = delete;
 
-    // offscreen_pass.cpp:163-230 + 1152-1171: one frame with the current state.
-    const std::vector<uint32_t> &record(const Camera &camera)
+    // offscreen_pass.cpp:163-230 + update_uniform_buffer :1152-1171: pull the camera, render
+    // the frame (HIP), hand it to the presenter for this command buffer.
+    void record(CommandBuffer command_buffer, uint32_t frame_index)
     {
-        vr_camera cam{};
-        for (int i = 0; i < 16; ++i) cam.view[i] = camera.view[i];
-        for (int i = 0; i < 3; ++i) cam.position[i] = camera.position[i];
-        image_.resize((size_t)width_ * height_);
-        check(vr_render(ctx_, &cam, &params_, image_.data(), VR_OUT_RGBA8));
-        return image_;
-    }
-    // Same into device memory on a HIP stream (no host round trip), e.g. for Vulkan interop.
-    void record_device(const Camera &camera, void *out_dev, void *hip_stream)
-    {
-        vr_camera cam{};
-        for (int i = 0; i < 16; ++i) cam.view[i] = camera.view[i];
-        for (int i = 0; i < 3; ++i) cam.position[i] = camera.position[i];
-        check(vr_render_device(ctx_, &cam, &params_, out_dev, VR_OUT_RGBA8, 16, 0, 1, hip_stream));
+        const Camera camera = Traits::camera();
+        render(camera);
+        FrameImage img = get_image();
+        img.frame_index = frame_index;
+        presenter_.present(command_buffer, frame_index, img);
     }
 
     void framebuffer_size_changed(uint32_t width, uint32_t height)  // :232-255
@@ -71,24 +139,68 @@ class OffscreenPass {
         check(vr_resize(ctx_, width, height));
         width_ = width;
         height_ = height;
+        image_.clear();
+        presenter_.resize(width, height);
     }
-    void volume_dataset_changed(Dataset &dataset)  // :257-269
+    // :257-269; DatasetT: Vol::Data::Dataset ({glm::u32vec3 dimensions; float min, max;
+    // std::vector<float> data}) or Hip::Dataset
+    template <class DatasetT>
+    void volume_dataset_changed(DatasetT &dataset)
     {
         check(vr_set_volume(ctx_, dataset.data.data(), VR_DTYPE_F32, dataset.dimensions[0],
                             dataset.dimensions[1], dataset.dimensions[2], dataset.min, dataset.max));
     }
-    void slicing_changed(const float min[3], const float max[3])  // :271-277
+    // :271-277; Vec3: glm::vec3 or anything indexable by [0..2]
+    template <class Vec3>
+    void slicing_changed(const Vec3 &min, const Vec3 &max)
     {
-        check(vr_set_slicing(ctx_, min, max));
+        const float a[3] = {(float)min[0], (float)min[1], (float)min[2]};
+        const float b[3] = {(float)max[0], (float)max[1], (float)max[2]};
+        check(vr_set_slicing(ctx_, a, b));
     }
     void transfer_function_changed(const std::vector<uint32_t> &data)  // :279-288
     {
         check(vr_set_transfer_function(ctx_, data.data(), (uint32_t)data.size()));
     }
 
+    // offscreen_pass.h:53-54: the presenter's sampler / view of the frame's image
+    Sampler get_sampler() const { return presenter_.get_sampler(); }
+    ImageView get_image_view() const { return presenter_.get_image_view(); }
+    // the image handle: the last frame's pixels (empty before the first record())
+    FrameImage get_image() const
+    {
+        FrameImage f;
+        f.rgba8 = image_.empty() ? nullptr : image_.data();
+        f.width = width_;
+        f.height = height_;
+        f.frame = frames_;
+        return f;
+    }
+
+    // One frame for an explicit camera into the pass's host image (no presenter).
+    const std::vector<uint32_t> &render(const Camera &camera)
+    {
+        vr_camera cam{};
+        for (int i = 0; i < 16; ++i) cam.view[i] = camera.view[i];
+        for (int i = 0; i < 3; ++i) cam.position[i] = camera.position[i];
+        image_.resize((size_t)width_ * height_);
+        check(vr_render(ctx_, &cam, &params_, image_.data(), VR_OUT_RGBA8));
+        ++frames_;
+        return image_;
+    }
+    // Same into device memory on a HIP stream (no host round trip), e.g. for Vulkan interop.
+    void render_device(const Camera &camera, void *out_dev, void *hip_stream)
+    {
+        vr_camera cam{};
+        for (int i = 0; i < 16; ++i) cam.view[i] = camera.view[i];
+        for (int i = 0; i < 3; ++i) cam.position[i] = camera.position[i];
+        check(vr_render_device(ctx_, &cam, &params_, out_dev, VR_OUT_RGBA8, 16, 0, 1, hip_stream));
+    }
+
     const std::vector<uint32_t> &image() const { return image_; }
     vr_params &params() { return params_; }  // step, ERT, shading (reference defaults)
     vr_ctx *handle() { return ctx_; }
+    typename Traits::Presenter &presenter() { return presenter_; }
 
   private:
     void check(int rc)
@@ -96,9 +208,21 @@ class OffscreenPass {
         if (rc != VR_OK) throw std::runtime_error(vr_last_error(ctx_));
     }
     vr_ctx *ctx_;
+    typename Traits::Presenter presenter_;
     uint32_t width_, height_;
+    uint64_t frames_ = 0;
     vr_params params_{};
     std::vector<uint32_t> image_;
+};
+
+// Headless form: OffscreenPass(nullptr, w, h) or OffscreenPass(w, h).
+class OffscreenPass : public BasicOffscreenPass<HeadlessTraits> {
+  public:
+    using BasicOffscreenPass<HeadlessTraits>::BasicOffscreenPass;
+    OffscreenPass(uint32_t width, uint32_t height, int device = 0)
+        : BasicOffscreenPass<HeadlessTraits>(nullptr, width, height, device)
+    {
+    }
 };
 
 }  // namespace Vol::Rendering::Hip

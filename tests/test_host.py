@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 import pyoracle
+import synth
 import vr_amd
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -79,12 +80,46 @@ def imgui_pack(rgba):
     return sat(rgba[0]) | sat(rgba[1]) << 8 | sat(rgba[2]) << 16 | sat(rgba[3]) << 24
 
 
+def _product_gradient(m):
+    """vr_gradient_* (the product's TF producer) with the given markers, built through the
+    marker API the UI uses (set the two end markers, add the inner ones)."""
+    g = vr_amd.Gradient()
+    c, a = m["color_markers"], m["alpha_markers"]
+    g.set_color_marker(0, c[0][0], c[0][1])
+    g.set_color_marker(1, c[-1][0], c[-1][1])
+    for loc, rgb in c[1:-1]:
+        i = g.add_color_marker(loc, rgb)
+        g.set_color_marker(i, loc, rgb)
+    g.set_alpha_marker(0, a[0][0], a[0][1])
+    g.set_alpha_marker(1, a[-1][0], a[-1][1])
+    for loc, al in a[1:-1]:
+        i = g.add_alpha_marker(loc, al)
+        g.set_alpha_marker(i, loc, al)
+    return g
+
+
+@pytest.mark.parametrize("name", ["tf1_256", "tf2_256", "tf_color_256", "tf1_7", "tf2_7", "tf_color_7"])
+def test_gradient_discretize_matches_golden_texels(name):
+    """Row f2: the product's Gradient::discretize equals, texel for texel, the golden vectors
+    of tests/golden/tf_golden.json -- an independent float32 restatement of gradient.cpp:64-108
+    (accumulated texel-centre locations), sample_markers (:471-485), lerp (:13-16) and ImGui's
+    published IM_F32_TO_INT8_SAT packing (tools/make_tf_golden.py).  TF-1 is the default
+    Gradient(), TF-2 the demo ramp, both as the benchmark uses them."""
+    gold = json.load(open(os.path.join(GOLD, "tf_golden.json")))[name]
+    tf = _product_gradient(gold).discretize(gold["count"])
+    assert tf.tolist() == gold["texels"]
+
+
+def test_tf_golden_fixture_is_reproducible():
+    import make_tf_golden
+    built = json.loads(json.dumps(make_tf_golden.build()))
+    assert built == json.load(open(os.path.join(GOLD, "tf_golden.json")))
+
+
 def test_default_gradient_discretize():
     tf = vr_amd.Gradient().discretize(256)
-    # texel centres (i + 0.5)/256, black -> white, alpha 1 (gradient.cpp:64-70, 90-108)
-    for i in (0, 1, 100, 255):
-        loc = np.float32(0.5 / 256) + np.float32(i) * np.float32(1 / 256)
-        assert tf[i] == imgui_pack([loc, loc, loc, 1.0]) or abs(int(tf[i] & 0xFF) - round(loc * 255)) <= 1
+    assert np.array_equal(tf, synth.tf1())
+    # texel centres, black -> white, alpha 1 (gradient.cpp:64-70, 90-108)
     assert all((t >> 24) == 255 for t in tf)
     assert (tf & 0xFF).tolist() == sorted((tf & 0xFF).tolist())
     assert tf[0] & 0xFF == 0 and tf[255] & 0xFF == 255
@@ -236,3 +271,23 @@ def test_csv_loader(tmp_path):
     bad.write_text("1,2,3\n4,5\n")
     with pytest.raises(RuntimeError, match="Inconsistant dimensions"):
         vr_amd.load_csv([str(bad)])
+
+
+def test_csv_loader_edge_cases(tmp_path):
+    """csv_file_parser.cpp:14-50 semantics: a trailing ',' adds no field, an empty field is a
+    std::stof error, std::stof reads a numeric prefix, negative values lower the 0-seeded min,
+    a slice with another row count is rejected."""
+    def w(name, text):
+        p = tmp_path / name
+        p.write_text(text)
+        return str(p)
+    ds = vr_amd.load_csv([w("a.csv", "1,2,\n-3,4.5x,\n"), w("b.csv", "  5,6\n7,8\n")])
+    assert ds.dims == (2, 2, 2)
+    assert ds.data.ravel().tolist() == [1, 2, -3, 4.5, 5, 6, 7, 8]
+    assert ds.vmin == -3.0 and ds.vmax == 8.0
+    with pytest.raises(RuntimeError):
+        vr_amd.load_csv([w("c.csv", "1,,2\n")])
+    with pytest.raises(RuntimeError, match="Inconsistant dimensions"):
+        vr_amd.load_csv([w("d.csv", "1,2\n3,4\n"), w("e.csv", "1,2\n")])
+    with pytest.raises(RuntimeError, match="Inconsistant dimensions"):
+        vr_amd.load_csv([w("f.csv", "1,2\n\n3,4\n")])

@@ -1,0 +1,35 @@
+"""The C++ drop-in (include/vr/offscreen_pass_hip.hpp) against the reference's call shapes.
+
+tests/shim/reference_call_shapes.cpp holds the reference's OffscreenPass call sites
+(vulkan_context.cpp:51, main_pass.cpp:91, imgui_context.cpp:55-75, importer.cpp:41-46,
+main_window.cpp:233-238 and :253-257) with stand-in Vulkan/glm/Application types.  CPU: it
+compiles and links against lib/libvr_amd.so.  GPU: the program drives two MainPass::render
+frames and checks the presenter received exactly vr_render's pixels for the same camera."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIBDIR = os.path.join(ROOT, "volumetric-renderer_amd", "lib")
+SRC = os.path.join(ROOT, "tests", "shim", "reference_call_shapes.cpp")
+EXE = os.path.join(LIBDIR, "reference_call_shapes")
+
+
+def build():
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    SRC, "-o", EXE, "-L", LIBDIR, "-lvr_amd", "-Wl,-rpath," + LIBDIR],
+                   check=True, capture_output=True, text=True)
+    return EXE
+
+
+def test_reference_call_shapes_compile_and_link():
+    assert os.path.exists(build())
+
+
+@pytest.mark.gpu
+def test_reference_call_shapes_present_the_hip_frame(gpu):
+    exe = EXE if os.path.exists(EXE) else build()
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "match=1" in r.stdout

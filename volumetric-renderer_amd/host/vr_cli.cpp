@@ -89,7 +89,7 @@ int main(int argc, char **argv)
         pass.params().ert_eps = ert;
 
         auto t0 = std::chrono::steady_clock::now();
-        for (int f = 0; f < frames; ++f) pass.record(cam);
+        for (int f = 0; f < frames; ++f) pass.render(cam);
         auto t1 = std::chrono::steady_clock::now();
         const double ms = std::chrono::duration<double, std::milli>(t1 - t0).count() / frames;
         const std::vector<uint32_t> &img = pass.image();

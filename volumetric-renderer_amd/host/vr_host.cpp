@@ -762,42 +762,57 @@ extern "C" int vr_nrrd_write_raw(const char *nhdr_path, const void *data, int dt
     return w == bytes ? 0 : herr(-1, "short write");
 }
 
+namespace {
+
+// One z-slice of a CSV volume (CsvFileParser::parse, csv_file_parser.cpp:14-50): each line is a
+// row, fields split on ',' the way std::getline splits them (a trailing ',' adds no field, an
+// empty field is a std::stof error), each field read by std::stof.  The row width is fixed by
+// the first row of the first slice; any other width is "Inconsistant dimensions" (the
+// reference's message), checked as each row completes.  Returns the slice's row count.
+uint32_t append_csv_slice(const char *path, std::vector<float> &data, float &vmin, float &vmax,
+                          bool first_slice, uint32_t &width)
+{
+    std::ifstream in(path);
+    std::string line;
+    uint32_t rows = 0;
+    while (std::getline(in, line)) {
+        uint32_t fields = 0;
+        for (size_t pos = 0; pos < line.size();) {
+            size_t end = line.find(',', pos);
+            if (end == std::string::npos) end = line.size();
+            const float v = std::stof(line.substr(pos, end - pos));
+            // Dataset{} seeds min = max = 0 (csv_file_parser.cpp:16); NaN never replaces them
+            vmin = std::min(vmin, v);
+            vmax = std::max(vmax, v);
+            data.push_back(v);
+            ++fields;
+            pos = end + 1;
+        }
+        if (first_slice && rows == 0)
+            width = fields;
+        else if (fields != width)
+            throw std::runtime_error("Inconsistant dimensions");
+        ++rows;
+    }
+    return rows;
+}
+
+}  // namespace
+
 extern "C" int vr_csv_load(const char *const *paths, size_t npaths, vr_dataset *out)
 {
     if (!out || (!paths && npaths)) return herr(-22, "NULL argument");
     std::memset(out, 0, sizeof(*out));
-    // Restates CsvFileParser::parse; Dataset{} seeds min = max = 0 (csv_file_parser.cpp:16)
     std::vector<float> data;
     float vmin = 0.0f, vmax = 0.0f;
-    uint32_t dx = 0, dy = 0, x = 0, y = 0, z = 0;
+    uint32_t dx = 0, dy = 0, z = 0;
     try {
-        std::string line, value_str;
-        for (size_t fi = 0; fi < npaths; ++fi) {
-            std::ifstream file(paths[fi]);
-            y = 0;
-            while (std::getline(file, line)) {
-                std::stringstream ss(line);
-                x = 0;
-                while (std::getline(ss, value_str, ',')) {
-                    const float value = std::stof(value_str);
-                    vmin = std::min(vmin, value);
-                    vmax = std::max(vmax, value);
-                    data.push_back(value);
-                    x++;
-                }
-                if (z == 0 && y == 0) {
-                    dx = x;
-                } else if (x != dx) {
-                    throw std::runtime_error("Inconsistant dimensions");
-                }
-                y++;
-            }
-            if (z == 0) {
-                dy = y;
-            } else if (y != dy) {
+        for (; z < npaths; ++z) {
+            const uint32_t rows = append_csv_slice(paths[z], data, vmin, vmax, z == 0, dx);
+            if (z == 0)
+                dy = rows;
+            else if (rows != dy)  // every slice has the first slice's row count
                 throw std::runtime_error("Inconsistant dimensions");
-            }
-            z++;
         }
     } catch (std::exception &e) {
         return herr(-1, e.what());
