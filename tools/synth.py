@@ -167,6 +167,8 @@ CAMERAS = {
     "rotB": dict(radius=2.0, rotate=(-300.0, -150.0)),
     "fill": dict(radius=1.6, rotate=None),
     "fill_oblique": dict(radius=1.6, rotate=(40.0, 25.0)),
+    # the diagonal view of the view sweeps (tools/view_sweep.py): rays cross brick rows and slabs
+    "diag": dict(radius=2.0, rotate=(180.0, 140.0)),
 }
 
 

@@ -28,6 +28,9 @@ struct vr_ctx {
     // volume (bricked, native storage type)
     void *bricks = nullptr;
     size_t brick_bytes = 0;
+    // the same voxels zero-padded and linear (march_lds_kernel's LDS staging source)
+    void *lin = nullptr;
+    size_t lin_bytes = 0;
     int storage = ST_F32;
     uint32_t nx = 1, ny = 1, nz = 1;
     float vmin = 0.0f, vmax = 1.0f;
@@ -311,20 +314,49 @@ int set_bricks(vr_ctx *c, int storage, uint32_t nx, uint32_t ny, uint32_t nz, vo
     return VR_OK;
 }
 
+// The zero-padded linear copy (MarchParams::lin) of a linear device source, on `s`.
+int set_lin(vr_ctx *c, int storage, int src_dtype, const void *src, uint32_t nx, uint32_t ny,
+            uint32_t nz, hipStream_t s)
+{
+    const size_t bytes = lin_elems(nx, ny, nz) * storage_size(storage);
+    if (!c->lin || c->lin_bytes != bytes) {
+        if (c->lin) hipFree(c->lin);
+        c->lin = nullptr;
+        c->lin_bytes = 0;
+        HIP_TRY(c, hipMalloc(&c->lin, bytes), "hipMalloc(linear volume)");
+        c->lin_bytes = bytes;
+    }
+    HIP_TRY(c, launch_pad_from_linear(src_dtype, src, c->lin, nx, ny, nz, storage, s), "pad kernel");
+    return VR_OK;
+}
+
+// LDS-staged march (march_lds_kernel): VR_LDS=1/0 overrides; needs the linear copy, the TF in
+// LDS and no empty-space skipping (that variant keeps the bricked kernels).
+bool use_lds(const vr_ctx *c, const vr_params *p)
+{
+    if (!c->lin || p->skip_empty || c->tf_n > 256) return false;
+    if (const char *e = std::getenv("VR_LDS")) return e[0] == '1';
+    return false;
+}
+
 int upload_tf(vr_ctx *c, const uint32_t *tf, uint32_t n)
 {
-    // texel i as {c_i, c_(i+1) - c_i} (0 for the last): tf_lookup's one-fma linear filter
-    std::vector<float4> lut(2 * (size_t)n);
+    // entry i + 1 = texel i as {c_i, c_(i+1) - c_i} (0 for the last), entries 0 and n + 1 the
+    // clamp-to-edge sentinels {c_0, 0} and {c_(n-1), 0}: tf_lookup's one-fma linear filter
+    std::vector<float4> col(n);
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t t = tf[i];
-        lut[2 * i] = make_float4(srgb_to_linear(t & 0xFFu), srgb_to_linear((t >> 8) & 0xFFu),
-                                 srgb_to_linear((t >> 16) & 0xFFu),
-                                 (float)((t >> 24) & 0xFFu) / 255.0f);
+        col[i] = make_float4(srgb_to_linear(t & 0xFFu), srgb_to_linear((t >> 8) & 0xFFu),
+                             srgb_to_linear((t >> 16) & 0xFFu), (float)((t >> 24) & 0xFFu) / 255.0f);
     }
+    std::vector<float4> lut(2 * ((size_t)n + 2), make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     for (uint32_t i = 0; i < n; ++i) {
-        const float4 a = lut[2 * i], b = i + 1 < n ? lut[2 * i + 2] : a;
-        lut[2 * i + 1] = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, b.w - a.w);
+        const float4 a = col[i], b = i + 1 < n ? col[i + 1] : a;
+        lut[2 * (i + 1)] = a;
+        lut[2 * (i + 1) + 1] = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, b.w - a.w);
     }
+    lut[0] = col[0];
+    lut[2 * ((size_t)n + 1)] = col[n - 1];
     if (c->tf && c->tf_n != n) {
         hipFree(c->tf);
         hipFree(c->tf_nz);
@@ -335,7 +367,7 @@ int upload_tf(vr_ctx *c, const uint32_t *tf, uint32_t n)
     nz[0] = 0;
     for (uint32_t i = 0; i < n; ++i) nz[i + 1] = nz[i] + ((tf[i] >> 24) != 0u ? 1u : 0u);
     if (!c->tf) {
-        HIP_TRY(c, hipMalloc(&c->tf, 2 * (size_t)n * sizeof(float4)), "hipMalloc(TF)");
+        HIP_TRY(c, hipMalloc(&c->tf, 2 * ((size_t)n + 2) * sizeof(float4)), "hipMalloc(TF)");
         HIP_TRY(c, hipMalloc(&c->tf_nz, (n + 1) * sizeof(uint32_t)), "hipMalloc(TF alpha prefix)");
     }
     HIP_TRY(c, hipMemcpy(c->tf, lut.data(), lut.size() * sizeof(float4), hipMemcpyHostToDevice),
@@ -464,6 +496,11 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.slab_default = c->smin[0] == 0.0f && c->smin[1] == 0.0f && c->smin[2] == 0.0f &&
                      c->smax[0] == 1.0f && c->smax[1] == 1.0f && c->smax[2] == 1.0f;
     P.pipelined = use_pipeline(p->shading != 0, P.tiles_x * P.tiles_y, c->brick_bytes);
+    P.lin = c->lin;
+    P.lpx = lin_pitch_x(c->nx);
+    P.lpy = c->ny + 2 * kPad;
+    P.lpz = c->nz + 2 * kPad;
+    P.lds = use_lds(c, p) ? 1 : 0;
     return VR_OK;
 }
 
@@ -721,6 +758,7 @@ void vr_destroy(vr_ctx *c)
     for (auto e : c->ev_pool) hipEventDestroy(e);
     if (c->built_ev) hipEventDestroy(c->built_ev);
     if (c->bricks) hipFree(c->bricks);
+    if (c->lin) hipFree(c->lin);
     if (c->tf) hipFree(c->tf);
     if (c->tf_nz) hipFree(c->tf_nz);
     if (c->brick_range) hipFree(c->brick_range);
@@ -781,6 +819,8 @@ int vr_set_volume_device(vr_ctx *c, const void *data_dev, int dtype, uint32_t nx
     if (rc) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
     HIP_TRY(c, launch_brick_from_linear(dtype, data_dev, dst, nx, ny, nz, st, s), "brick kernel");
+    rc = set_lin(c, st, dtype, data_dev, nx, ny, nz, s);
+    if (rc) return rc;
     HIP_TRY(c, hipStreamSynchronize(s), "brick kernel sync");
     c->storage = st;
     c->nx = nx;
@@ -878,8 +918,10 @@ int vr_generate_volume(vr_ctx *c, int kind, int dtype, uint32_t nx, uint32_t ny,
     int rc = set_bricks(c, st, nx, ny, nz, &dst);
     if (rc == VR_OK) {
         e = launch_brick_from_linear(src_dtype, lin, dst, nx, ny, nz, st, nullptr);
-        if (e == hipSuccess) e = hipDeviceSynchronize();
         if (e != hipSuccess) rc = hip_fail(c, e, "brick generated volume");
+        if (rc == VR_OK) rc = set_lin(c, st, src_dtype, lin, nx, ny, nz, nullptr);
+        if (rc == VR_OK && (e = hipDeviceSynchronize()) != hipSuccess)
+            rc = hip_fail(c, e, "brick generated volume");
     }
     hipFree(lin);
     if (rc) return rc;
@@ -999,7 +1041,7 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
     hipStream_t s = static_cast<hipStream_t>(stream);
     rc = ensure_derived(c, p, P, s);
     if (rc) return rc;
-    if (use_pair(P, p)) {  // L lanes per ray on 16 x (16 / L) tiles (march_pair_kernel)
+    if (!P.lds && use_pair(P, p)) {  // L lanes per ray on 16 x (16 / L) tiles (march_pair_kernel)
         // 4 lanes below kPairQuadMaxWaves (N = 8 C3 share: 0.151 -> 0.144 ms), else 2
         P.pair = P.tiles_x * P.tiles_y * (kThreadsPerTile / 64) < kPairQuadMaxWaves ? 4 : 2;
         if (const char *e = std::getenv("VR_PAIR_LANES")) P.pair = e[0] == '4' ? 4 : 2;
@@ -1186,6 +1228,7 @@ const char *vr_kernel_name(const vr_ctx *c, const vr_params *p)
     const uint32_t tiles = ((c->width + 15) / 16) * ((c->height + kMarchRows - 1) / kMarchRows);
     const bool pipe = use_pipeline(p && p->shading, tiles, c->brick_bytes) &&
                       !(p && p->skip_empty) && c->tf_n <= 256;
+    if (p && use_lds(c, p)) return march_lds_kernel_name(c->storage, p->shading != 0);
     return march_kernel_name(c->storage, p && p->shading != 0, false, p && p->skip_empty != 0, gf,
                              pipe);
 }

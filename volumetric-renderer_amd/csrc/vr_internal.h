@@ -107,12 +107,26 @@ struct MarchParams {
     // (24 B, same element index as the density); null -> formed from the stencil
     const float *grad;
     float inv_range;        // RN(1 / range) (div_fast)
+    // LDS-staged march (march_lds_kernel): the volume as a LINEAR x-fastest array of the
+    // storage type with kPad zero voxels on every side (padded index = logical + 2), row pitch
+    // lpx (a multiple of 4 voxels, so LDS-DMA chunks are aligned), lpy rows per slice
+    const void *lin;
+    uint32_t lpx, lpy, lpz;
+    int32_t lds;            // launch march_lds_kernel
 };
+
+// Padded linear layout of MarchParams::lin for an nx x ny x nz volume.
+inline uint32_t lin_pitch_x(uint32_t nx) { return (nx + 2 * kPad + 3) / 4 * 4; }
+inline size_t lin_elems(uint32_t nx, uint32_t ny, uint32_t nz)
+{
+    return (size_t)lin_pitch_x(nx) * (ny + 2 * kPad) * (nz + 2 * kPad);
+}
 
 // Launchers (vr_kernels.hip).  All asynchronous on `stream`.
 hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &p,
                         hipStream_t stream);
 const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bool gf, bool pipe);
+const char *march_lds_kernel_name(int storage, bool shade);
 // Wavefront count below which a launch uses the pipelined kernel (see build_params).
 constexpr uint32_t kPipelineMaxWaves = 24576;  // between N = 2 (16 K) and N = 1 (33 K) at 1080p
 constexpr size_t kPipelineMinBytes = 4ull << 30;  // large volumes: always pipelined
@@ -152,6 +166,9 @@ constexpr uint32_t kPairMaxWaves = 24576;
 constexpr uint32_t kPairQuadMaxWaves = 6144;  // below: 4 lanes per ray
 hipError_t launch_brick_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,
                                     uint32_t ny, uint32_t nz, int storage, hipStream_t stream);
+// Linear source (any NRRD element type) -> the zero-padded linear layout of MarchParams::lin.
+hipError_t launch_pad_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,
+                                  uint32_t ny, uint32_t nz, int storage, hipStream_t stream);
 // Bricked volume -> linear x-fastest voxels of the storage type, slices [z0, z0 + cz).
 hipError_t launch_unbrick(int storage, const void *bricks, void *dst, uint32_t nx, uint32_t ny,
                           uint32_t z0, uint32_t cz, hipStream_t stream);

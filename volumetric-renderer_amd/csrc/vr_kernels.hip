@@ -37,6 +37,7 @@ namespace {
 constexpr int kTile = 16;       // pixels per workgroup side
 constexpr int kThreads = 256;   // lane-pair kernel workgroup: 4 waves
 constexpr int kTfLds = 256;     // TF texels staged in LDS
+constexpr int kTfLut = 2 * (kTfLds + 2);  // float4s of the staged LUT (tf_lookup: + 2 sentinels)
 
 __device__ __forceinline__ float lerpf(float a, float b, float w) { return fmaf(w, b - a, a); }
 
@@ -82,6 +83,8 @@ __device__ __forceinline__ float tri8(float v000, float v100, float v010, float 
                                       float v101, float v011, float v111, float ax, float ay,
                                       float az)
 {
+    // scalar: packing the z = 0 / z = 1 halves into v_pk_fma_f32 pairs (8 instructions for 14)
+    // measured 2-7% slower (u8 C4 view sweep, profiles/r02/valu/packed_tri_ab.txt)
     const float c00 = lerpf(v000, v100, ax);
     const float c10 = lerpf(v010, v110, ax);
     const float c01 = lerpf(v001, v101, ax);
@@ -460,21 +463,22 @@ __device__ __forceinline__ float div_by_range(float x, const MarchParams &P)
     return x / P.range;
 }
 
-// 1D TF, linear filter, clamp-to-edge (offscreen_pass.cpp:1125-1150).  lut holds texel i as
-// {c_i, c_{i+1} - c_i} (difference 0 for the last texel, computed on the host with the same
-// IEEE subtraction), so lerp(c_i0, c_i1, w) = fma(w, c_i1 - c_i0, c_i0) is one fma per channel:
-// i0 = n - 1 (or u = n) reads difference 0 = the clamped c_(n-1); below the first texel
-// (u < 0) both clamped texels are c_0, so w is taken as 0.
+// 1D TF, linear filter, clamp-to-edge (offscreen_pass.cpp:1125-1150).  lut holds n + 2
+// entries {c, d} (float4 pairs): entry i + 1 is texel i as {c_i, c_(i+1) - c_i} (difference 0
+// for the last texel, computed on the host with the same IEEE subtraction), entry 0 = {c_0, 0}
+// and entry n + 1 = {c_(n-1), 0} are the clamp-to-edge sentinels.  With u clamped to [-1, n],
+// floor(u) = i0 lies in [-1, n] and lerp(c_i0, c_i1, w) = fma(w, d, c) is one fma per channel
+// with no index clamp: below the first texel centre (i0 = -1) and at u = n the sentinel's
+// difference 0 returns the edge texel for any w.  NaN t clamps to u = -1 (texel 0).
 __device__ __forceinline__ float4 tf_lookup(const float4 *lut, int n, float nf, float t)
 {
+    (void)n;
     float u = t * nf - 0.5f;
     u = fminf(fmaxf(u, -1.0f), nf);
     const float f = floorf(u);
-    float w = u - f;
-    int i0 = (int)f;
-    if (i0 < 0) w = 0.0f;
-    i0 = i0 < 0 ? 0 : (i0 > n - 1 ? n - 1 : i0);
-    const float4 a = lut[2 * i0], d = lut[2 * i0 + 1];
+    const float w = u - f;
+    const int e = (int)f + 1;
+    const float4 a = lut[2 * e], d = lut[2 * e + 1];
     return make_float4(fmaf(w, d.x, a.x), fmaf(w, d.y, a.y), fmaf(w, d.z, a.z),
                        fmaf(w, d.w, a.w));
 }
@@ -579,6 +583,32 @@ __device__ __forceinline__ bool block_tile(const MarchParams &P, uint32_t &tile_
     return true;
 }
 
+// Headlight Phong of one sample from its filtered central differences (gx, gy, gz): gradient
+// scaled to normalised coordinates, ndl = |n . dir|, rgb' = rgb (ka + kd ndl) + ks ndl^p; a
+// zero gradient leaves the colour unshaded.  The oracle's march_pixel, same operation order.
+__device__ __forceinline__ void phong(const MarchParams &P, float gx, float gy_, float gz,
+                                      float d0, float d1, float d2, float4 &s)
+{
+    const float wx = gx * P.fnx, wy = gy_ * P.fny, wz = gz * P.fnz;
+    const float g2 = wx * wx + wy * wy + wz * wz;
+    if (g2 > 0.0f) {
+        const float inv = 1.0f / sqrtf(g2);
+        const float ndl = fabsf((wx * d0 + wy * d1 + wz * d2) * inv);
+        const float kdiff = P.ka + P.kd * ndl;
+        // ndl^p by binary exponentiation (the oracle's powi): p uniform
+        float sp = 1.0f, b = ndl;
+        for (int e = P.spec_power; e;) {
+            if (e & 1) sp = sp * b;
+            e >>= 1;
+            if (e) b = b * b;
+        }
+        const float spec = P.ks * sp;
+        s.x = s.x * kdiff + spec;
+        s.y = s.y * kdiff + spec;
+        s.z = s.z * kdiff + spec;
+    }
+}
+
 #ifndef VR_EXP_NO_GRAD_LOADS
 #define VR_EXP_NO_GRAD_LOADS 0  // experiment builds: time without the difference-field loads
 #endif
@@ -603,24 +633,7 @@ __device__ __forceinline__ void shade_sample(const MarchParams &P, const char *_
         gradient<VT, PACKED>(vol, ce, c, pi & (kBrick - 1), pj & (kBrick - 1), pk & (kBrick - 1),
                              by_stride, bz_stride, ax, ay, az, gx, gy_, gz);
     }
-    const float wx = gx * P.fnx, wy = gy_ * P.fny, wz = gz * P.fnz;
-    const float g2 = wx * wx + wy * wy + wz * wz;
-    if (g2 > 0.0f) {
-        const float inv = 1.0f / sqrtf(g2);
-        const float ndl = fabsf((wx * d0 + wy * d1 + wz * d2) * inv);
-        const float kdiff = P.ka + P.kd * ndl;
-        // ndl^p by binary exponentiation (the oracle's powi): p uniform
-        float sp = 1.0f, b = ndl;
-        for (int e = P.spec_power; e;) {
-            if (e & 1) sp = sp * b;
-            e >>= 1;
-            if (e) b = b * b;
-        }
-        const float spec = P.ks * sp;
-        s.x = s.x * kdiff + spec;
-        s.y = s.y * kdiff + spec;
-        s.z = s.z * kdiff + spec;
-    }
+    phong(P, gx, gy_, gz, d0, d1, d2, s);
 }
 
 // PIPE: the loads of sample k + 1 are issued before sample k is filtered, shaded and
@@ -630,7 +643,7 @@ __device__ __forceinline__ void shade_sample(const MarchParams &P, const char *_
 template <typename VT, bool SHADE, bool COUNT, bool SKIP, bool GF, bool PIPE>
 __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, PIPE>)) void march_kernel(const MarchParams P)
 {
-    __shared__ float4 s_tf[2 * kTfLds];  // {texel, difference to the next} pairs
+    __shared__ float4 s_tf[kTfLut];  // {texel, difference to the next} pairs + sentinels
     const int tid = threadIdx.x;
 
     uint32_t tile_x, tile_y;
@@ -642,7 +655,7 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
 
     const bool tf_in_lds = P.tf_n <= kTfLds;
     if (tf_in_lds)
-        for (int i = tid; i < 2 * P.tf_n; i += (int)kThreadsPerTile) s_tf[i] = P.tf[i];
+        for (int i = tid; i < 2 * (P.tf_n + 2); i += (int)kThreadsPerTile) s_tf[i] = P.tf[i];
     __syncthreads();
     const long by_stride = (long)P.nbx * kBrickElems;  // elements between brick rows/slabs
     const long bz_stride = (long)P.nbx * P.nby * kBrickElems;
@@ -897,11 +910,11 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
 template <typename VT, bool SHADE, bool GF, int L>
 __global__ __launch_bounds__(kThreads) void march_pair_kernel(const MarchParams P)
 {
-    __shared__ float4 s_tf[2 * kTfLds];
+    __shared__ float4 s_tf[kTfLut];
     const int tid = threadIdx.x;
     uint32_t tile_x, tile_y;
     if (!block_tile(P, tile_x, tile_y)) return;
-    for (int i = tid; i < 2 * P.tf_n; i += kThreads) s_tf[i] = P.tf[i];
+    for (int i = tid; i < 2 * (P.tf_n + 2); i += kThreads) s_tf[i] = P.tf[i];
     __syncthreads();
     const long long wg_start = wall_clock64();
 #ifdef VR_WG_TIMES
@@ -1032,6 +1045,365 @@ __global__ __launch_bounds__(kThreads) void march_pair_kernel(const MarchParams 
     }
 }
 
+// ---- LDS-staged march (north_star: "hot bricks staged in LDS") --------------------------------
+// The tile's 256 rays advance in lock step by step index.  Per STAGE of S steps the workgroup
+// computes the box of voxels its live rays' trilinear footprints (and, shaded, the gradient
+// stencil) can touch in steps [k0, k0 + S), loads that box from the zero-padded LINEAR volume
+// (MarchParams::lin) into LDS with LDS-DMA (global_load_lds: coalesced rows, no VGPRs), and
+// every ray takes its S samples from LDS: the per-sample gather leaves the texture-data path
+// (TA/TD) for ds_read.  Two staging buffers: stage s + 1's box is predicted from the rays'
+// current positions and its DMA issued before stage s is marched, so the load overlaps the
+// march; one workgroup barrier per stage.  Same positions, predicates, voxels and operation
+// order as march_kernel: frames are bit-identical.  S adapts: halved while a box would not
+// fit, doubled while it fills less than a third of a buffer; a stage whose single-step box
+// still does not fit (rays far apart: zoomed-out views of big volumes) reads the linear volume
+// directly.
+#ifndef VR_LDS_BUF_BYTES
+#define VR_LDS_BUF_BYTES 16128  // x 2 + 8 KiB TF + 256 B = 40704 B: 4 workgroups (16 waves) per CU
+#endif
+#ifndef VR_LDS_S0
+#define VR_LDS_S0 8
+#endif
+#ifndef VR_LDS_SMAX
+#define VR_LDS_SMAX 64
+#endif
+#ifndef VR_LDS_MIN_WAVES
+#define VR_LDS_MIN_WAVES 4
+#endif
+constexpr int kLdsBufBytes = VR_LDS_BUF_BYTES;
+
+// LDS-DMA chunk per lane: 16 B (4 f32) or 4 B (4 x 8-bit, 2 x 16-bit); the box's x extent is a
+// whole number of chunks, aligned in the padded volume (row pitch lpx is a multiple of 4).
+template <typename T>
+struct LdsChunk {
+    static constexpr int kBytes = sizeof(T) == 4 ? 16 : 4;
+    static constexpr int kVox = kBytes / (int)sizeof(T);
+};
+
+template <typename T, typename IdxT>
+__device__ __forceinline__ float vox_f(const T *base, IdxT i)
+{
+    return (float)base[i];
+}
+
+// Ray state of the LDS march.
+struct LaneRay {
+    float p0, p1, p2, d0, d1, d2;
+    float T, cr, cg, cb;
+    int kin, nsteps;
+    bool alive;
+};
+
+// Steps [k0, k0 + S) of one ray, voxels from `base` (the staged box or, for a stage that does
+// not fit, the linear volume) with box origin (ox, oy, oz) in padded coordinates and row /
+// slice pitches py, pz.  Branch-free per step (as march_kernel's PIPE path): the predicates
+// set `alive` and `slab`, the voxel reads are unconditional (the box origin for a lane without
+// a sample, whose alpha is then 0: it composites +0 and leaves T), so the loop's trip count is
+// wave-uniform and only the shading of visible samples branches.
+template <typename T, bool SHADE, typename IdxT>
+__device__ __forceinline__ void lds_steps(const MarchParams &P, LaneRay &R, const float4 *s_tf,
+                                          const T *base, int ox, int oy, int oz, IdxT py,
+                                          IdxT pz, int k0, int S)
+{
+    for (int j = 0; j < S; ++j) {
+        if (!__any(R.alive)) break;
+        const int k = k0 + j;
+        // predicates as bitwise ops (no short-circuit branches)
+        const bool interior = (unsigned)(k - 1) < (unsigned)R.kin;  // k in [1, kin]
+        // volume.frag:31-37: the step bound, then the break if any component > 1 or < 0
+        const bool oob = (R.p0 > 1.0f) | (R.p1 > 1.0f) | (R.p2 > 1.0f) | (R.p0 < 0.0f) |
+                         (R.p1 < 0.0f) | (R.p2 < 0.0f);
+        R.alive = R.alive & (k < R.nsteps) & (interior | !oob);
+        // volume.frag:39-40 (strict)
+        const bool inslab = (R.p0 < P.smax[0]) & (R.p1 < P.smax[1]) & (R.p2 < P.smax[2]) &
+                            (R.p0 > P.smin[0]) & (R.p1 > P.smin[1]) & (R.p2 > P.smin[2]);
+        const bool slab = R.alive & (interior | inslab);
+        int i, jj, kk;
+        float ax, ay, az;
+        texel_coord(R.p0, P.fnx, i, ax);
+        texel_coord(R.p1, P.fny, jj, ay);
+        texel_coord(R.p2, P.fnz, kk, az);
+        const IdxT e0 = ((IdxT)(kk + kPad - oz)) * pz + (IdxT)(jj + kPad - oy) * py +
+                        (IdxT)(i + kPad - ox);
+        const IdxT e = slab ? e0 : (IdxT)0;
+        const float v0 = vox_f(base, e), v1 = vox_f(base, e + 1);
+        const float v2 = vox_f(base, e + py), v3 = vox_f(base, e + py + 1);
+        const float v4 = vox_f(base, e + pz), v5 = vox_f(base, e + pz + 1);
+        const float v6 = vox_f(base, e + pz + py), v7 = vox_f(base, e + pz + py + 1);
+        const float d = tri8(v0, v1, v2, v3, v4, v5, v6, v7, ax, ay, az);  // volume.frag:41
+        float4 sm = tf_lookup(s_tf, P.tf_n, P.tf_nf, div_by_range(d - P.vmin, P));  // :42-43
+        if (!slab) sm.w = 0.0f;
+        if (SHADE && sm.w > 0.0f) {
+            // central differences D_a(c) = v(c + e_a) - v(c - e_a) over the cell's corners
+            // (the oracle's grad_cell; march_kernel's stencil path, same operations)
+            const float v[8] = {v0, v1, v2, v3, v4, v5, v6, v7};
+            float Dx[8], Dy[8], Dz[8];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {  // rows (dy, dz) = (c & 1, c >> 1)
+                const IdxT r = e + (IdxT)(c & 1) * py + (IdxT)(c >> 1) * pz;
+                const int o = 2 * (c & 1) + 4 * (c >> 1);
+                Dx[o] = v[o + 1] - vox_f(base, r - 1);
+                Dx[o + 1] = vox_f(base, r + 2) - v[o];
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {  // columns (dx, dz) = (c & 1, c >> 1)
+                const IdxT r = e + (IdxT)(c & 1) + (IdxT)(c >> 1) * pz;
+                const int o = (c & 1) + 4 * (c >> 1);
+                Dy[o] = v[o + 2] - vox_f(base, r - py);
+                Dy[o + 2] = vox_f(base, r + 2 * py) - v[o];
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {  // columns (dx, dy) = (c & 1, c >> 1)
+                const IdxT r = e + (IdxT)(c & 1) + (IdxT)(c >> 1) * py;
+                const int o = (c & 1) + 2 * (c >> 1);
+                Dz[o] = v[o + 4] - vox_f(base, r - pz);
+                Dz[o + 4] = vox_f(base, r + 2 * pz) - v[o];
+            }
+            float gx, gy, gz;
+            grad_filter<true>(Dx, Dy, Dz, ax, ay, az, gx, gy, gz);
+            phong(P, gx, gy, gz, R.d0, R.d1, R.d2, sm);
+        }
+        // volume.frag:44-45 (a lane without a sample adds +0 and keeps T)
+        R.cr = R.cr + (sm.x * sm.w) * R.T;
+        R.cg = R.cg + (sm.y * sm.w) * R.T;
+        R.cb = R.cb + (sm.z * sm.w) * R.T;
+        R.T = R.T * (1.0f - sm.w);
+        if (R.T == 0.0f || R.T < P.ert_eps) R.alive = false;
+        // volume.frag:47
+        R.p0 = R.p0 + R.d0 * P.step;
+        R.p1 = R.p1 + R.d1 * P.step;
+        R.p2 = R.p2 + R.d2 * P.step;
+    }
+}
+
+// Packed 16-bit min over the wavefront (v_pk_min_u16 + DPP row shifts / broadcasts): each
+// 32-bit value holds two u16 keys, both minimised at once.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
+                                                                   __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t wave_pk_min_u16(uint32_t v)
+{
+    constexpr int id = -1;  // 0xFFFF,0xFFFF: the identity where a DPP source lane is invalid
+    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x111, 0xf, 0xf, false));
+    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x112, 0xf, 0xf, false));
+    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x114, 0xf, 0xf, false));
+    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x118, 0xf, 0xf, false));
+    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x142, 0xa, 0xf, false));
+    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x143, 0xc, 0xf, false));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// LDS-DMA of one chunk per lane to the wave-uniform LDS byte address `lds` + lane * CB, issued
+// from inline asm: hipcc then keeps it out of its own s_waitcnt bookkeeping (with the builtin
+// it drains vmcnt(0) before every LDS read of the TF, which would retire the next stage's
+// prefetch at the first step of the current one); the kernel waits vmcnt(0) itself before the
+// barrier that publishes the buffer.  M0 written and restored in the same statement.
+__device__ __forceinline__ uint32_t lds_addr(const char *p)
+{
+    return (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(size_t)(const __attribute__((address_space(3))) char *)p);
+}
+template <int CB>
+__device__ __forceinline__ void glds(const void *g, uint32_t lds)
+{
+    uint32_t keep;
+    if constexpr (CB == 16)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+
+// A stage's box in padded voxel coordinates: origin, extents (x in whole chunks).
+struct LdsBox {
+    int ox, oy, oz, Lx, Ly, Lz, nchunk;
+    bool empty;
+};
+
+template <typename T, bool SHADE>
+__global__ __launch_bounds__(kThreadsPerTile, VR_LDS_MIN_WAVES) void march_lds_kernel(const MarchParams P)
+{
+    constexpr int CB = LdsChunk<T>::kBytes, CV = LdsChunk<T>::kVox;
+    constexpr int kBufChunks = kLdsBufBytes / CB;
+    constexpr int kBufBytes = kBufChunks * CB;
+    constexpr int kTfBytes = kTfLut * 16, kRedBytes = 256;
+    // one LDS array (a second __shared__ object next to LDS-DMA staging can make hipcc drain
+    // vmcnt before every ds_read): TF pairs | reduction slots [2 rounds][4 waves][3] | 2 boxes
+    __shared__ __attribute__((aligned(16))) char smem[kTfBytes + kRedBytes + 2 * kBufBytes];
+    float4 *s_tf = reinterpret_cast<float4 *>(smem);
+    uint32_t *s_red = reinterpret_cast<uint32_t *>(smem + kTfBytes);
+    char *s_buf = smem + kTfBytes + kRedBytes;
+
+    const int tid = threadIdx.x;
+    uint32_t tile_x, tile_y;
+    if (!block_tile(P, tile_x, tile_y)) return;
+    const long long wg_start = wall_clock64();
+    for (int i = tid; i < 2 * (P.tf_n + 2); i += (int)kThreadsPerTile) s_tf[i] = P.tf[i];  // tf_n <= 256
+
+    const uint32_t wave = tid >> 6, lane = tid & 63;
+    const uint32_t ws = P.wave_w_shift, ww = 1u << ws, wh = 64u >> ws;
+    const uint32_t wpr = kTile >> ws;
+    const uint32_t px = tile_x * kTile + (wave % wpr) * ww + (lane & (ww - 1));
+    const uint32_t ly = tile_y * kMarchRows + (wave / wpr) * wh + (lane >> ws);
+    bool active = px < P.W && ly < P.local_rows;
+    const uint32_t blk = ly / P.row_block;
+    const uint32_t gy = (blk * P.nranks + P.rank) * P.row_block + (ly - blk * P.row_block);
+    active = active && gy < P.H;
+    float tex[3] = {0.f, 0.f, 0.f}, dir[3] = {0.f, 0.f, 0.f};
+    const bool covered = active && pixel_ray(P, px, gy, tex, dir);
+
+    LaneRay R;
+    R.p0 = tex[0];
+    R.p1 = tex[1];
+    R.p2 = tex[2];
+    R.d0 = dir[0];
+    R.d1 = dir[1];
+    R.d2 = dir[2];
+    R.T = 1.0f;
+    R.cr = R.cg = R.cb = 0.0f;
+    R.nsteps = covered ? P.nsteps : 0;
+    R.kin = (covered && P.slab_default) ? interior_steps(tex, dir, P.step, R.nsteps) : 0;
+    R.alive = covered && R.nsteps > 0;
+
+    const float fn[3] = {P.fnx, P.fny, P.fnz};
+    const int hi_cap[3] = {(int)P.nx + 3, (int)P.ny + 3, (int)P.nz + 3};  // padded [0, N + 3]
+    const T *lin = static_cast<const T *>(P.lin);
+    int rnd = 0;
+
+    // The box of voxels steps [k0 + a, k0 + a + n) of the live rays can read, predicted from
+    // their positions at step k0 (p_k = p_k0 + (k - k0) s, each float add off by <= 2^-24 for
+    // |p| < 2), clamped to [0, 1] (the bounds test breaks outside), texel coordinates
+    // p N - 0.5 with a margin for their float rounding; cells floor(u) .. floor(u) + 1, the
+    // gradient's stencil one more each side.  One workgroup barrier: it also orders every
+    // wave's earlier LDS reads and DMA waits before whatever follows it.
+    auto reduce_box = [&](int k0, int a, int n, LdsBox &B) {
+        uint32_t key[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        const int first = k0 + a, last = min(k0 + a + n, R.nsteps) - 1;
+        if (R.alive && first <= last) {
+            const float pp[3] = {R.p0, R.p1, R.p2}, dd[3] = {R.d0, R.d1, R.d2};
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const double sd = (double)(dd[c] * P.step);
+                const double q0 = (double)pp[c] + (double)(first - k0) * sd;
+                const double q1 = (double)pp[c] + (double)(last - k0) * sd;
+                const double m = (double)(last - k0 + 1) * 0x1p-23;
+                const double u0 = fmax(fmin(q0, q1) - m, 0.0), u1 = fmin(fmax(q0, q1) + m, 1.0);
+                const double cm = 1e-3 + (double)fn[c] * 0x1p-21;
+                int l = (int)floor(u0 * (double)fn[c] - 0.5 - cm) + kPad - (SHADE ? 1 : 0);
+                int h = (int)floor(u1 * (double)fn[c] - 0.5 + cm) + 1 + kPad + (SHADE ? 1 : 0);
+                l = max(l, 0);
+                h = min(h, hi_cap[c]);
+                if (l <= h) key[c] = (uint32_t)l | ((uint32_t)(0xFFFF - h) << 16);
+            }
+        }
+        uint32_t *slot = s_red + (rnd & 1) * 16 + wave * 4;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const uint32_t w = wave_pk_min_u16(key[c]);
+            if (lane == 0) slot[c] = w;
+        }
+        __syncthreads();
+        const uint32_t *r = s_red + (rnd & 1) * 16;
+        int lo[3], hi[3];
+        bool empty = false;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const uint32_t w = __builtin_amdgcn_readfirstlane(
+                pk_min_u16(pk_min_u16(r[c], r[4 + c]), pk_min_u16(r[8 + c], r[12 + c])));
+            lo[c] = (int)(w & 0xFFFFu);
+            hi[c] = 0xFFFF - (int)(w >> 16);
+            empty = empty || lo[c] > hi[c];
+        }
+        ++rnd;
+        B.empty = empty;
+        B.ox = lo[0] & ~(CV - 1);
+        const int ncx = (hi[0] - B.ox) / CV + 1;
+        B.Lx = ncx * CV;
+        B.oy = lo[1];
+        B.oz = lo[2];
+        B.Ly = hi[1] - lo[1] + 1;
+        B.Lz = hi[2] - lo[2] + 1;
+        B.nchunk = empty ? 0 : ncx * B.Ly * B.Lz;
+    };
+    // LDS-DMA of box B into buffer `buf`: chunk c = (z, y, cx) row-major -> byte c * CB, so a
+    // wave's 64 chunks land contiguously (LDS-DMA writes wave base + lane * CB).
+    auto stage = [&](const LdsBox &B, char *buf) {
+        const int ncx = B.Lx / CV;
+        const uint64_t mx = ((1ull << 40) + (uint64_t)ncx - 1) / (uint64_t)ncx;
+        const uint64_t my = ((1ull << 40) + (uint64_t)B.Ly - 1) / (uint64_t)B.Ly;
+        for (int c0 = (int)wave * 64; c0 < B.nchunk; c0 += 256) {
+            const int c = c0 + (int)lane;
+            if (c < B.nchunk) {
+                const uint32_t r = (uint32_t)(((uint64_t)c * mx) >> 40);
+                const uint32_t cx = (uint32_t)c - r * (uint32_t)ncx;
+                const uint32_t z = (uint32_t)(((uint64_t)r * my) >> 40);
+                const uint32_t y = r - z * (uint32_t)B.Ly;
+                const T *g = lin + (((size_t)(B.oz + (int)z) * P.lpy + (size_t)(B.oy + (int)y)) * P.lpx +
+                                    (size_t)B.ox + (size_t)cx * CV);
+                glds<CB>(g, lds_addr(buf + (size_t)c0 * CB));
+            }
+        }
+    };
+
+    // prologue: stage 0's box (halving S until it fits or S = 1)
+    int S = VR_LDS_S0, k0 = 0, b = 0;
+    LdsBox cur, nxt;
+    for (;;) {
+        reduce_box(0, 0, S, cur);
+        if (cur.empty || cur.nchunk <= kBufChunks || S == 1) break;
+        S >>= 1;
+    }
+    if (!cur.empty && cur.nchunk <= kBufChunks) stage(cur, s_buf);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    while (!cur.empty) {
+        // stage s + 1: predict its box, issue its DMA into the other buffer (free: every wave
+        // finished stage s - 1, which read it, before the reduction's barrier), then march
+        // stage s, whose DMA every wave waited for before that same barrier
+        int S2 = (cur.nchunk * 3 < kBufChunks && S < VR_LDS_SMAX) ? 2 * S : S;
+        for (;;) {
+            reduce_box(k0, S, S2, nxt);
+            if (nxt.empty || nxt.nchunk <= kBufChunks || S2 == 1) break;
+            S2 >>= 1;
+        }
+        if (!nxt.empty && nxt.nchunk <= kBufChunks) stage(nxt, s_buf + (b ^ 1) * kBufBytes);
+        if (cur.nchunk <= kBufChunks)
+            lds_steps<T, SHADE, int>(P, R, s_tf, reinterpret_cast<const T *>(s_buf + b * kBufBytes),
+                                     cur.ox, cur.oy, cur.oz, cur.Lx, cur.Lx * cur.Ly, k0, S);
+        else  // one step's footprint does not fit: this stage reads the linear volume
+            lds_steps<T, SHADE, long long>(P, R, s_tf, lin, 0, 0, 0, (long long)P.lpx,
+                                           (long long)P.lpx * P.lpy, k0, S);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        k0 += S;
+        S = S2;
+        cur = nxt;
+        b ^= 1;
+    }
+
+    if (P.tile_cost) {  // adaptive order: this tile's duration for the next launch
+        if (tid == 0)
+            P.tile_cost[tile_y * P.tiles_x + tile_x] =
+                (uint32_t)min(wall_clock64() - wg_start, 0x7FFFFFFFLL);
+    }
+    if (!active) return;
+    const float A = 1.0f - R.T;  // volume.frag:50 + blend (offscreen_pass.cpp:715-725)
+    const float omA = 1.0f - A;
+    const float o0 = R.cr * A + P.clear[0] * omA;
+    const float o1 = R.cg * A + P.clear[1] * omA;
+    const float o2 = R.cb * A + P.clear[2] * omA;
+    const float o3 = A * A + P.clear[3] * omA;
+    const size_t idx = (size_t)ly * P.W + px;
+    if (P.out_format == 0) {
+        static_cast<uint32_t *>(P.out)[idx] =
+            unorm8(o0) | (unorm8(o1) << 8) | (unorm8(o2) << 16) | (unorm8(o3) << 24);
+    } else {
+        static_cast<float4 *>(P.out)[idx] = make_float4(o0, o1, o2, o3);
+    }
+}
+
 // ---- adaptive tile order --------------------------------------------------------------------
 
 // One workgroup per XCD x over its tile list (the tiles of the super-tiles s = x (mod 8), as
@@ -1146,6 +1518,26 @@ __global__ __launch_bounds__(256) void brick_kernel(const SrcT *__restrict__ src
             q.v[3] = at(x, y + 1, z + 1);
             reinterpret_cast<Quad *>(dst)[g] = q;
         }
+    }
+}
+
+// ---- volume ingest: linear -> zero-padded linear (march_lds_kernel's staging source) ----------
+template <typename SrcT, typename DstT>
+__global__ __launch_bounds__(256) void pad_kernel(const SrcT *__restrict__ src,
+                                                  DstT *__restrict__ dst, uint32_t nx,
+                                                  uint32_t ny, uint32_t nz, uint32_t lpx,
+                                                  uint32_t lpy, size_t total)
+{
+    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+         g += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t px = (uint32_t)(g % lpx);
+        const size_t r = g / lpx;
+        const uint32_t py = (uint32_t)(r % lpy), pz = (uint32_t)(r / lpy);
+        const long x = (long)px - kPad, y = (long)py - kPad, z = (long)pz - kPad;
+        DstT v = (DstT)0;
+        if (x >= 0 && y >= 0 && z >= 0 && x < (long)nx && y < (long)ny && z < (long)nz)
+            v = (DstT)src[(size_t)x + (size_t)nx * ((size_t)y + (size_t)ny * (size_t)z)];
+        dst[g] = v;
     }
 }
 
@@ -1424,9 +1816,25 @@ hipError_t launch_pair_t(const MarchParams &p, hipStream_t stream)
     return hipGetLastError();
 }
 
+template <typename VT, bool SHADE>
+hipError_t launch_lds_t(const MarchParams &p, hipStream_t stream)
+{
+    const uint32_t nblocks = p.tile_perm ? p.nperm
+                             : p.tile_order >= 3 ? ((p.supers_total + 7) / 8) * 8 * kSuper * kSuper
+                                                 : p.tiles_x * p.tiles_y;
+    if (p.tiles_x * p.tiles_y == 0) return hipSuccess;
+    hipLaunchKernelGGL((march_lds_kernel<VT, SHADE>), dim3(nblocks), dim3(kThreadsPerTile), 0,
+                       stream, p);
+    return hipGetLastError();
+}
+
 template <typename VT>
 hipError_t launch_march_vt(bool shade, bool count, const MarchParams &p, hipStream_t s)
 {
+    if (p.lds && !count) {  // host: no skip-empty, tf_n <= kTfLds, lin present
+        if (shade) return launch_lds_t<VT, true>(p, s);
+        return launch_lds_t<VT, false>(p, s);
+    }
     if (p.pair) {  // host: not counting, no skip-empty, tf_n <= kTfLds, 16x8 tiles
         if (!shade) return launch_pair_t<VT, false, false>(p, s);
         if constexpr (kZPair<VT>)
@@ -1549,6 +1957,21 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
     return names[storage * 32 + k].c_str();
 }
 
+const char *march_lds_kernel_name(int storage, bool shade)
+{
+    static const std::vector<std::string> names = [] {
+        const char *types[5] = {"unsigned char", "signed char", "unsigned short", "short", "float"};
+        std::vector<std::string> v;
+        for (int t = 0; t < 5; ++t)
+            for (int sh = 0; sh < 2; ++sh)
+                v.push_back(std::string("void vr::(anonymous namespace)::march_lds_kernel<") + types[t] +
+                            (sh ? ", true" : ", false") + ">(vr::MarchParams)");
+        return v;
+    }();
+    if (storage < 0 || storage > 4) return "march_lds_kernel<?>";
+    return names[storage * 2 + (shade ? 1 : 0)].c_str();
+}
+
 hipError_t launch_unbrick(int storage, const void *bricks, void *dst, uint32_t nx, uint32_t ny,
                           uint32_t z0, uint32_t cz, hipStream_t s)
 {
@@ -1561,6 +1984,42 @@ hipError_t launch_unbrick(int storage, const void *bricks, void *dst, uint32_t n
         default: hipLaunchKernelGGL((unbrick_kernel<float>), dim3(g), dim3(256), 0, s, (const float *)bricks, (float *)dst, nx, ny, bx, by, z0, n); break;
     }
     return hipGetLastError();
+}
+
+template <typename SrcT>
+hipError_t pad_from(const void *src, void *dst, uint32_t nx, uint32_t ny, uint32_t nz,
+                    int storage, hipStream_t s)
+{
+    const uint32_t lpx = lin_pitch_x(nx), lpy = ny + 2 * kPad;
+    const size_t total = lin_elems(nx, ny, nz);
+    const SrcT *sp = static_cast<const SrcT *>(src);
+    const unsigned g = grid_for(total);
+    switch (storage) {
+        case ST_U8: hipLaunchKernelGGL((pad_kernel<SrcT, uint8_t>), dim3(g), dim3(256), 0, s, sp, (uint8_t *)dst, nx, ny, nz, lpx, lpy, total); break;
+        case ST_I8: hipLaunchKernelGGL((pad_kernel<SrcT, int8_t>), dim3(g), dim3(256), 0, s, sp, (int8_t *)dst, nx, ny, nz, lpx, lpy, total); break;
+        case ST_U16: hipLaunchKernelGGL((pad_kernel<SrcT, uint16_t>), dim3(g), dim3(256), 0, s, sp, (uint16_t *)dst, nx, ny, nz, lpx, lpy, total); break;
+        case ST_I16: hipLaunchKernelGGL((pad_kernel<SrcT, int16_t>), dim3(g), dim3(256), 0, s, sp, (int16_t *)dst, nx, ny, nz, lpx, lpy, total); break;
+        default: hipLaunchKernelGGL((pad_kernel<SrcT, float>), dim3(g), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, lpx, lpy, total); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_pad_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,
+                                  uint32_t ny, uint32_t nz, int storage, hipStream_t s)
+{
+    switch (src_dtype) {  // enum vr_dtype
+        case 1: return pad_from<int8_t>(src, dst, nx, ny, nz, storage, s);
+        case 2: return pad_from<uint8_t>(src, dst, nx, ny, nz, storage, s);
+        case 3: return pad_from<int16_t>(src, dst, nx, ny, nz, storage, s);
+        case 4: return pad_from<uint16_t>(src, dst, nx, ny, nz, storage, s);
+        case 5: return pad_from<int32_t>(src, dst, nx, ny, nz, storage, s);
+        case 6: return pad_from<uint32_t>(src, dst, nx, ny, nz, storage, s);
+        case 7: return pad_from<int64_t>(src, dst, nx, ny, nz, storage, s);
+        case 8: return pad_from<uint64_t>(src, dst, nx, ny, nz, storage, s);
+        case 9: return pad_from<float>(src, dst, nx, ny, nz, storage, s);
+        case 10: return pad_from<double>(src, dst, nx, ny, nz, storage, s);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_brick_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,
