@@ -183,3 +183,40 @@ if __name__ == "__main__":
             r = simulate(fn, n, vb, list(vc.view), list(vc.position), ntiles=60)
             print(f"{cname:13s} {lname:40s} lines/instr {r['lines_per_instr']:6.2f}  "
                   f"lines/sample {r['lines_per_sample']:.3f}")
+
+
+# ---- plain 8-bit layouts (round 2: cutting the yz-quad's 4x duplication) --------------------
+def brick_plain_u8(B, pad_to=4):
+    """u8 voxels one per element in (B+1)^3-element bricks (apron), brick stride rounded up to
+    pad_to bytes.  A sample = 2 x 16-B loads at 4-aligned addresses: floor4(e) covers rows
+    (y, z) and (y+1, z) at x, x+1 (offsets e, e+1, e+S, e+S+1 all < floor4(e) + 16 when
+    S <= 12); the second the same at z+1."""
+    S = B + 1
+    stride = (S ** 3 + pad_to - 1) // pad_to * pad_to
+
+    def fn(i, j, k, nb):
+        pi, pj, pk = i + 2, j + 2, k + 2
+        b = ((pk // B) * nb + (pj // B)) * nb + (pi // B)
+        e = b * stride + ((pk % B) * S + (pj % B)) * S + (pi % B)
+        e2 = e + S * S
+        return [(e & ~3, 16), (e2 & ~3, 16)]
+    return fn, stride / B ** 3
+
+
+def views_u8(n=256, ntiles=60, W=1024, H=1024):
+    sys.path.insert(0, os.path.join(ROOT, "volumetric-renderer_amd"))
+    import synth
+    cams = {"fill": synth.camera("fill"), "fill_oblique": synth.camera("fill_oblique"),
+            "side_x": synth.vr_amd.make_camera(radius=1.6, rotate=(360.0, 0.0)),
+            "diag": synth.vr_amd.make_camera(radius=2.0, rotate=(180.0, 140.0)),
+            "default": synth.camera("default")}
+    p8, f8 = brick_plain_u8(8)
+    p4, f4 = brick_plain_u8(4, 128)
+    layouts = {"yzquad8 (1 x dwordx2)": (brick_apron_yzquad(8, 1), 4 * (9 / 8) ** 3),
+               f"plain8 (2 x dwordx4)": (p8, f8), f"plain4/128B (2 x dwordx4)": (p4, f4)}
+    for cname, cam in cams.items():
+        vc = cam.to_vr_camera()
+        for lname, (fn, foot) in layouts.items():
+            r = simulate(fn, n, 1, list(vc.view), list(vc.position), W=W, H=H, ntiles=ntiles, tile=(16, 4))
+            print(f"{cname:13s} {lname:28s} x{foot:.2f}  lines/instr {r['lines_per_instr']:6.2f}  "
+                  f"lines/sample {r['lines_per_sample']:.3f}", flush=True)

@@ -294,7 +294,7 @@ int set_bricks(vr_ctx *c, int storage, uint32_t nx, uint32_t ny, uint32_t nz, vo
 {
     c->range_valid = c->dist_valid = false;  // the bricks are about to be rewritten
     c->grad_valid = false;
-    const size_t bytes = (size_t)bricks_for(nx) * bricks_for(ny) * bricks_for(nz) *
+    const size_t bytes = (size_t)bricks_for(nx, 0) * bricks_for(ny, 1) * bricks_for(nz, 2) *
                          kBrickElems * element_size(storage);
     if (c->bricks && c->brick_bytes == bytes) {
         *out = c->bricks;
@@ -450,8 +450,8 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.nx = c->nx;
     P.ny = c->ny;
     P.nz = c->nz;
-    P.nbx = bricks_for(c->nx);
-    P.nby = bricks_for(c->ny);
+    P.nbx = bricks_for(c->nx, 0);
+    P.nby = bricks_for(c->ny, 1);
     P.fnx = (float)c->nx;
     P.fny = (float)c->ny;
     P.fnz = (float)c->nz;
@@ -508,7 +508,7 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
 // the march that reads them.
 int ensure_skip(vr_ctx *c, MarchParams &P, hipStream_t s)
 {
-    const size_t nb = (size_t)bricks_for(c->nx) * bricks_for(c->ny) * bricks_for(c->nz);
+    const size_t nb = (size_t)bricks_for(c->nx, 0) * bricks_for(c->ny, 1) * bricks_for(c->nz, 2);
     if (nb > 0xFFFFFFFFull) return fail(c, VR_EINVAL, "skip_empty: too many bricks");
     if (c->nbricks_alloc != nb) {
         if (c->brick_range) hipFree(c->brick_range);
@@ -522,14 +522,15 @@ int ensure_skip(vr_ctx *c, MarchParams &P, hipStream_t s)
         c->nbricks_alloc = nb;
     }
     if (!c->range_valid) {
-        HIP_TRY(c, launch_brick_range(c->storage, c->bricks, (uint32_t)nb, c->brick_range, s),
+        HIP_TRY(c, launch_brick_range(c->storage, c->bricks, bricks_for(c->nx, 0), bricks_for(c->ny, 1),
+                                      bricks_for(c->nz, 2), c->brick_range, s),
                 "brick range kernel");
         c->range_valid = true;
         c->dist_valid = false;
     }
     if (!c->dist_valid) {
-        HIP_TRY(c, launch_skip_dist(c->brick_range, bricks_for(c->nx), bricks_for(c->ny),
-                                    bricks_for(c->nz), c->tf_nz, (int)c->tf_n, c->vmin,
+        HIP_TRY(c, launch_skip_dist(c->brick_range, bricks_for(c->nx, 0), bricks_for(c->ny, 1),
+                                    bricks_for(c->nz, 2), c->tf_nz, (int)c->tf_n, c->vmin,
                                     c->vmax - c->vmin, c->skip_dist, c->skip_dist + nb, s),
                 "skip distance kernels");
         c->dist_valid = true;

@@ -10,9 +10,9 @@ namespace vr {
 
 // ---- Bricked, paired-element volume layout in HBM --------------------------------------
 // The logical volume (nx, ny, nz) is shifted by kPad = 2 zero voxels on the low side of each
-// axis ("padded index" p = logical + 2) and cut into bricks of kBrick^3 = 8^3 base cells.
-// Brick b stores ELEMENTS for padded indices [8 b, 8 b + 8] on each axis (kStore = 9: a
-// 1-element apron), bricks ordered x-fastest in the brick grid, elements x-fastest in a brick.
+// axis ("padded index" p = logical + 2) and cut into bricks of kBX x kBY x kBZ (8^3) cells.
+// Brick b stores ELEMENTS for padded indices [8 b, 8 b + 8] on each axis (9: a 1-element
+// apron), bricks in brick_slot order, elements x-fastest in a brick.
 // An element holds more than one voxel, so that one wide load fetches a whole trilinear
 // footprint edge-on (the gather pipeline, not HBM, bounds this kernel: DESIGN.md):
 //   f32   (and 32/64-bit inputs, converted):  "z-pair"  element = {v(x,y,z), v(x,y,z+1)}, 8 B;
@@ -21,24 +21,97 @@ namespace vr {
 //         4 B (u8/i8) or 8 B (u16/i16); a sample = 1 load of elements x, x+1 (8 B / 16 B).
 // Voxels outside [0, N) are stored as 0: CLAMP_TO_BORDER/TRANSPARENT_BLACK without a bounds
 // test.  Memory: 2 x (9/8)^3 = 2.85x the f32 voxels, 4 x (9/8)^3 = 5.7x the 8/16-bit voxels.
-#ifndef VR_BRICK_SHIFT
-#define VR_BRICK_SHIFT 3  // 8^3 bricks (experiment builds may use 4: 16^3)
+// Brick geometry (compile-time): kBX x kBY x kBZ cells per brick, each axis storing cells + 1
+// elements (the apron); element (x, y, z) of a brick at (x + kEX (y + kEY z)), the brick padded
+// to kBrickElems.  Default 8^3 cells (9^3 = 729 elements).  Experiment builds may set
+// VR_BRICK_CELLS="bx,by,bz" (e.g. 15,7,8: 16-element rows = one 128-B line of f32 z-pairs) and
+// VR_BRICK_ALIGN (elements the brick size is rounded up to).
+#ifndef VR_BRICK_CELLS
+#define VR_BRICK_CELLS 8, 8, 8
 #endif
-constexpr int kBrickShift = VR_BRICK_SHIFT;
+#ifndef VR_BRICK_ALIGN
+#define VR_BRICK_ALIGN 1
+#endif
+constexpr int kBrickCells[3] = {VR_BRICK_CELLS};
+constexpr int kBX = kBrickCells[0], kBY = kBrickCells[1], kBZ = kBrickCells[2];
+constexpr int kEX = kBX + 1, kEY = kBY + 1, kEZ = kBZ + 1;  // elements per axis
+constexpr int kRowElems = kEX;                            // element stride of y
+constexpr int kSliceElems = kEX * kEY;                    // element stride of z
+constexpr int kBrickElems = (kEX * kEY * kEZ + VR_BRICK_ALIGN - 1) / VR_BRICK_ALIGN * VR_BRICK_ALIGN;
+constexpr bool kBrickPow2 = (kBX & (kBX - 1)) == 0 && (kBY & (kBY - 1)) == 0 && (kBZ & (kBZ - 1)) == 0;
 // VR_F32_PLAIN=1 (experiment builds): f32 elements hold one voxel (no z-pair duplication);
 // a sample is then 4 x 8-B loads (elements x, x+1 of the rows (y|y+1, z|z+1)).
 #ifndef VR_F32_PLAIN
 #define VR_F32_PLAIN 0
 #endif
 constexpr size_t kF32VoxelsPerElement = VR_F32_PLAIN ? 1 : 2;
-constexpr int kBrick = 1 << kBrickShift;
-constexpr int kStore = kBrick + 1;
-constexpr int kBrickElems = kStore * kStore * kStore;  // 729
 constexpr int kPad = 2;
 
-// Bricks per axis: fetch base indices lie in [1, N + 1] (march) and gradient taps reach one
-// element below and (in z-pair x/y) two above, i.e. padded [0, N + 3].
-inline uint32_t bricks_for(uint32_t n) { return (n + 3) / kBrick + 1; }
+// Brick memory order (north_star: "Z-ordered bricks").  kGroupShift = 0: bricks x-fastest over
+// the brick grid.  kGroupShift = g > 0: the grid is cut into groups of 2^g bricks per axis,
+// groups x-fastest, and the 2^3g bricks of a group in Morton (Z) order, so bricks near in 3-D
+// are near in memory (fewer distinct pages per wave-level load on oblique views).
+#ifndef VR_BRICK_GROUP_SHIFT
+#define VR_BRICK_GROUP_SHIFT 0
+#endif
+constexpr int kGroupShift = VR_BRICK_GROUP_SHIFT;
+constexpr uint32_t kGroupMask = (1u << kGroupShift) - 1;
+
+// Bricks along axis a (0 x, 1 y, 2 z) of an n-voxel axis: fetch base indices lie in [1, N + 1]
+// (march) and gradient taps reach one element below and (in z-pair x/y) two above, i.e.
+// padded [0, N + 3]; rounded up to whole brick groups.
+inline uint32_t bricks_for(uint32_t n, int a)
+{
+    return ((n + 3) / (uint32_t)kBrickCells[a] + 1 + kGroupMask) & ~kGroupMask;
+}
+
+// Bits 0..g-1 of v moved to bits 0, 3, 6, ... (one axis of a Morton code).
+__host__ __device__ __forceinline__ uint32_t morton_spread(uint32_t v)
+{
+    uint32_t r = 0;
+#pragma unroll
+    for (int t = 0; t < kGroupShift; ++t) r |= ((v >> t) & 1u) << (3 * t);
+    return r;
+}
+
+// Memory slot of brick (bx, by, bz) of an nbx x nby x * grid (whole groups per axis).
+__host__ __device__ __forceinline__ uint32_t brick_slot(uint32_t bx, uint32_t by, uint32_t bz,
+                                                        uint32_t nbx, uint32_t nby)
+{
+    if constexpr (kGroupShift == 0) {
+        return (bz * nby + by) * nbx + bx;
+    } else {
+        constexpr uint32_t G = kGroupShift;
+        const uint32_t grp = ((bz >> G) * (nby >> G) + (by >> G)) * (nbx >> G) + (bx >> G);
+        return (grp << (3 * G)) | morton_spread(bx & kGroupMask) |
+               (morton_spread(by & kGroupMask) << 1) | (morton_spread(bz & kGroupMask) << 2);
+    }
+}
+
+// Inverse of brick_slot.
+__host__ __device__ __forceinline__ void brick_coords(uint32_t slot, uint32_t nbx, uint32_t nby,
+                                                      uint32_t &bx, uint32_t &by, uint32_t &bz)
+{
+    if constexpr (kGroupShift == 0) {
+        bx = slot % nbx;
+        by = (slot / nbx) % nby;
+        bz = slot / (nbx * nby);
+    } else {
+        constexpr uint32_t G = kGroupShift;
+        const uint32_t grp = slot >> (3 * G), m = slot & ((1u << (3 * G)) - 1);
+        const uint32_t gx = nbx >> G, gy = nby >> G;
+        uint32_t lx = 0, ly = 0, lz = 0;
+#pragma unroll
+        for (int t = 0; t < (int)G; ++t) {
+            lx |= ((m >> (3 * t)) & 1u) << t;
+            ly |= ((m >> (3 * t + 1)) & 1u) << t;
+            lz |= ((m >> (3 * t + 2)) & 1u) << t;
+        }
+        bx = ((grp % gx) << G) | lx;
+        by = (((grp / gx) % gy) << G) | ly;
+        bz = ((grp / (gx * gy)) << G) | lz;
+    }
+}
 
 enum StorageType { ST_U8 = 0, ST_I8 = 1, ST_U16 = 2, ST_I16 = 3, ST_F32 = 4 };
 
@@ -191,8 +264,8 @@ constexpr int kSkipCap = 16;
 constexpr size_t kGradElemBytes = 24;
 hipError_t launch_grad_field(const float *bricks, float *grad, uint32_t nx, uint32_t ny,
                              uint32_t nz, hipStream_t stream);
-hipError_t launch_brick_range(int storage, const void *bricks, uint32_t nbricks,
-                              float2 *range_dev, hipStream_t stream);
+hipError_t launch_brick_range(int storage, const void *bricks, uint32_t nbx, uint32_t nby,
+                              uint32_t nbz, float2 *range_dev, hipStream_t stream);
 hipError_t launch_skip_dist(const float2 *range_dev, uint32_t nbx, uint32_t nby, uint32_t nbz,
                             const uint32_t *tf_nz_dev, int tf_n, float vmin, float vrange,
                             uint8_t *dist_dev, uint8_t *scratch_dev, hipStream_t stream);

@@ -70,11 +70,10 @@ constexpr int kQuadWords = sizeof(VT) == 1 ? 1 : 2;
 // volumes < 4 GiB measured slower on the shaded kernel and on the diagonal view.)
 __device__ __forceinline__ size_t cell_offset(int pi, int pj, int pk, uint32_t nbx, uint32_t nby)
 {
-    const uint32_t b = ((uint32_t)(pk >> kBrickShift) * nby + (uint32_t)(pj >> kBrickShift)) * nbx +
-                       (uint32_t)(pi >> kBrickShift);
-    const uint32_t l = ((uint32_t)(pk & (kBrick - 1)) * kStore + (uint32_t)(pj & (kBrick - 1))) * kStore +
-                       (uint32_t)(pi & (kBrick - 1));
-    return (size_t)b * (size_t)kBrickElems + l;
+    const uint32_t ux = (uint32_t)pi, uy = (uint32_t)pj, uz = (uint32_t)pk;
+    const uint32_t bx = ux / kBX, by = uy / kBY, bz = uz / kBZ;
+    const uint32_t l = ((uz - bz * kBZ) * kEY + (uy - by * kBY)) * kEX + (ux - bx * kBX);
+    return (size_t)brick_slot(bx, by, bz, nbx, nby) * (size_t)kBrickElems + l;
 }
 
 // Trilinear filter of a 2x2x2 cell given its voxels v[dz][dy][dx]: lerp x, then y, then z
@@ -172,13 +171,13 @@ struct Cell8 {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const f2a q = *reinterpret_cast<const f2a *>(
-                    base + (e + (size_t)((r & 1) * kStore + (r >> 1) * kStore * kStore)) * 4);
+                    base + (e + (size_t)((r & 1) * kRowElems + (r >> 1) * kSliceElems)) * 4);
                 v[2 * r] = q.x;
                 v[2 * r + 1] = q.y;
             }
         } else if constexpr (kZPair<VT>) {
             const f4a r0 = zpair_load2(base, e);
-            const f4a r1 = zpair_load2(base, e + kStore);
+            const f4a r1 = zpair_load2(base, e + kRowElems);
             v[0] = r0.x;
             v[4] = r0.y;
             v[1] = r0.z;
@@ -235,20 +234,41 @@ __device__ __forceinline__ void grad_filter(const float *dx, const float *dy, co
 
 template <typename VT, bool PACKED>
 __device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e,
-                                         const Cell8<VT> &c, int lx, int ly, int lz,
-                                         long by_stride, long bz_stride, float ax, float ay,
-                                         float az, float &gx, float &gy, float &gz)
+                                         const Cell8<VT> &c, int pi, int pj, int pk,
+                                         uint32_t nbx, uint32_t nby, long by_stride,
+                                         long bz_stride, float ax, float ay, float az, float &gx,
+                                         float &gy, float &gz)
 {
-    constexpr long S = kStore, S2 = (long)kStore * kStore, B = kBrickElems, L = kBrick - 1;
-    const long dxm = lx > 0 ? -1 : (L - B);
-    const long dxp = lx < L ? 2 : (B - (L - 1));
-    const long dym = ly > 0 ? -S : (L * S - by_stride);
-    const long dzm = lz > 0 ? -S2 : (L * S2 - bz_stride);
+    constexpr long S = kRowElems, S2 = kSliceElems, B = kBrickElems;
+    constexpr long Lx = kBX - 1, Ly = kBY - 1, Lz = kBZ - 1;
+    const int lx = pi % kBX, ly = pj % kBY, lz = pk % kBZ;
+    // element-index deltas of the taps one element below / two above the cell's low corner;
+    // a tap outside the brick reads the neighbouring brick (constant strides in x-fastest
+    // brick order, the neighbour's slot otherwise)
+    long dxm, dxp, dym, dyp, dzm, dzp;
+    if constexpr (kGroupShift == 0) {
+        dxm = lx > 0 ? -1 : (Lx - B);
+        dxp = lx < Lx ? 2 : (B - (Lx - 1));
+        dym = ly > 0 ? -S : (Ly * S - by_stride);
+        dyp = ly < Ly ? 2 * S : (by_stride - (Ly - 1) * S);
+        dzm = lz > 0 ? -S2 : (Lz * S2 - bz_stride);
+        dzp = lz < Lz ? 2 * S2 : (bz_stride - (Lz - 1) * S2);
+    } else {
+        auto cross = [&](int ox, int oy, int oz) {
+            return (long)cell_offset(pi + ox, pj + oy, pk + oz, nbx, nby) - (long)e;
+        };
+        dxm = lx > 0 ? -1 : cross(-1, 0, 0);
+        dxp = lx < Lx ? 2 : cross(2, 0, 0);
+        dym = ly > 0 ? -S : cross(0, -1, 0);
+        dyp = ly < Ly ? 2 * S : cross(0, 2, 0);
+        dzm = lz > 0 ? -S2 : cross(0, 0, -1);
+        dzp = lz < Lz ? 2 * S2 : cross(0, 0, 2);
+    }
+    (void)dyp;
+    (void)dzp;
     const float *v = c.v;
     float Dx[8], Dy[8], Dz[8];
     if constexpr (kZPair<VT> && VR_F32_PLAIN) {
-        const long dyp = ly < L ? 2 * S : (by_stride - (L - 1) * S);
-        const long dzp = lz < L ? 2 * S2 : (bz_stride - (L - 1) * S2);
         auto ld1 = [&](long o) { return *reinterpret_cast<const float *>(base + (e + o) * 4); };
         auto ld2 = [&](long o) { return *reinterpret_cast<const f2a *>(base + (e + o) * 4); };
 #pragma unroll
@@ -279,7 +299,6 @@ __device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e
             Dz[o + 5] = q.y - v[o + 1];
         }
     } else if constexpr (kZPair<VT>) {
-        const long dyp = ly < L ? 2 * S : (by_stride - (L - 1) * S);
         // z-pairs (.x = z, .y = z + 1) of the x - 1 and x + 2 columns, rows y and y + 1
         const f2a xm0 = zpair_load1(base, e + dxm), xm1 = zpair_load1(base, e + dxm + S);
         const f2a xp0 = zpair_load1(base, e + dxp), xp1 = zpair_load1(base, e + dxp + S);
@@ -340,7 +359,7 @@ __device__ __forceinline__ void grad_field(const char *__restrict__ gbase, size_
     float Dx[8], Dy[8], Dz[8];
 #pragma unroll
     for (int dy_ = 0; dy_ < 2; ++dy_) {
-        const char *row = gbase + (e + (size_t)dy_ * kStore) * kGradElemBytes;
+        const char *row = gbase + (e + (size_t)dy_ * kRowElems) * kGradElemBytes;
         const f4a r0 = *reinterpret_cast<const f4a *>(row);       // Dx(x) z,z+1  Dy(x) z,z+1
         const f4a r1 = *reinterpret_cast<const f4a *>(row + 16);  // Dz(x) z,z+1  Dx(x+1) z,z+1
         const f4a r2 = *reinterpret_cast<const f4a *>(row + 32);  // Dy(x+1) ...  Dz(x+1) ...
@@ -630,8 +649,8 @@ __device__ __forceinline__ void shade_sample(const MarchParams &P, const char *_
     } else if constexpr (GF) {  // f32: precomputed difference field
         grad_field<PACKED>(reinterpret_cast<const char *>(P.grad), ce, ax, ay, az, gx, gy_, gz);
     } else {
-        gradient<VT, PACKED>(vol, ce, c, pi & (kBrick - 1), pj & (kBrick - 1), pk & (kBrick - 1),
-                             by_stride, bz_stride, ax, ay, az, gx, gy_, gz);
+        gradient<VT, PACKED>(vol, ce, c, pi, pj, pk, P.nbx, P.nby, by_stride, bz_stride, ax, ay,
+                             az, gx, gy_, gz);
     }
     phong(P, gx, gy_, gz, d0, d1, d2, s);
 }
@@ -775,9 +794,8 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
             if (SKIP) {
                 // skip_empty: distance (in bricks) from the cell's brick to the nearest brick
                 // that can produce a visible sample (classify_kernel); cached per brick
-                const uint32_t bb = ((uint32_t)(pk >> kBrickShift) * P.nby +
-                                     (uint32_t)(pj >> kBrickShift)) * P.nbx +
-                                    (uint32_t)(pi >> kBrickShift);
+                const uint32_t bb = ((uint32_t)pk / kBZ * P.nby + (uint32_t)pj / kBY) * P.nbx +
+                                    (uint32_t)pi / kBX;
                 if (bb != cur_brick) {
                     cur_brick = bb;
                     cur_dist = P.skip_dist[bb];
@@ -797,17 +815,17 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
                     // coordinate u = p N - 0.5, brick of u: (floor(u) + 2) >> 3), advancing p
                     // with the same float additions as the reference loop, so the first
                     // non-empty sample is reached at the bit-identical position.
-                    const float reach = (float)((int)(dist - 1) * kBrick);
                     float kf = (float)min(nsteps - 1 - it, kMaxLeap);
-                    const int bi[3] = {pi >> kBrickShift, pj >> kBrickShift, pk >> kBrickShift};
+                    const int bi[3] = {pi / kBX, pj / kBY, pk / kBZ};
                     const float pp[3] = {p0, p1, p2}, dd[3] = {d0, d1, d2};
                     const float fn[3] = {P.fnx, P.fny, P.fnz};
 #pragma unroll
                     for (int a = 0; a < 3; ++a) {
                         const float u = pp[a] * fn[a] - 0.5f;
+                        const float reach = (float)((int)(dist - 1) * kBrickCells[a]);
                         const float room = dd[a] > 0.0f
-                                               ? (float)((bi[a] + 1) * kBrick - kPad) + reach - u
-                                               : u - (float)(bi[a] * kBrick - kPad) + reach;
+                                               ? (float)((bi[a] + 1) * kBrickCells[a] - kPad) + reach - u
+                                               : u - (float)(bi[a] * kBrickCells[a] - kPad) + reach;
                         // NaN (axis not moving) is ignored by fminf
                         kf = fminf(kf, (room - leap_margin[a]) * inv_du[a]);
                     }
@@ -1491,12 +1509,12 @@ __global__ __launch_bounds__(256) void brick_kernel(const SrcT *__restrict__ src
     for (size_t bidx = blockIdx.x; bidx < nbricks; bidx += gridDim.x)
     for (uint32_t l = threadIdx.x; l < (uint32_t)kBrickElems; l += blockDim.x) {
         const size_t g = bidx * kBrickElems + l;
-        const uint32_t lx = l % kStore, lyz = l / kStore, lyy = lyz % kStore, lz = lyz / kStore;
-        const uint32_t bx = (uint32_t)(bidx % nbx), byz = (uint32_t)(bidx / nbx);
-        const uint32_t by = byz % nby, bz = byz / nby;
-        const long x = (long)bx * kBrick + lx - kPad;
-        const long y = (long)by * kBrick + lyy - kPad;
-        const long z = (long)bz * kBrick + lz - kPad;
+        const uint32_t lx = l % kEX, lyz = l / kEX, lyy = lyz % kEY, lz = lyz / kEY;
+        uint32_t bx, by, bz;
+        brick_coords((uint32_t)bidx, nbx, nby, bx, by, bz);
+        const long x = (long)bx * kBX + lx - kPad;
+        const long y = (long)by * kBY + lyy - kPad;
+        const long z = (long)bz * kBZ + lz - kPad;
         auto at = [&](long xx, long yy, long zz) -> DstT {
             if (xx < 0 || yy < 0 || zz < 0 || xx >= (long)nx || yy >= (long)ny || zz >= (long)nz)
                 return (DstT)0;
@@ -1625,7 +1643,7 @@ __global__ __launch_bounds__(256) void minmax_kernel(const VT *__restrict__ vol,
 // ---- f32 gradient field (shading) ------------------------------------------------------------
 
 // Voxel at padded coordinates (p = logical + kPad) from the bricked z-pair density: component
-// 0 of the element at p in brick p >> kBrickShift; 0 outside the logical volume.
+// 0 of the element at p (cell_offset); 0 outside the logical volume.
 __device__ __forceinline__ float padded_voxel(const float *__restrict__ bricks, int px, int py,
                                               int pz, uint32_t nx, uint32_t ny, uint32_t nz,
                                               uint32_t nbx, uint32_t nby)
@@ -1650,10 +1668,10 @@ __global__ __launch_bounds__(256) void grad_field_kernel(const float *__restrict
     for (size_t bidx = blockIdx.x; bidx < nbricks; bidx += gridDim.x)
     for (uint32_t l = threadIdx.x; l < (uint32_t)kBrickElems; l += blockDim.x) {
         const size_t g = bidx * kBrickElems + l;
-        const uint32_t lx = l % kStore, lyz = l / kStore, lyy = lyz % kStore, lz = lyz / kStore;
-        const uint32_t bx = (uint32_t)(bidx % nbx), byz = (uint32_t)(bidx / nbx);
-        const uint32_t by = byz % nby, bz = byz / nby;
-        const int x = (int)(bx * kBrick + lx), y = (int)(by * kBrick + lyy), z = (int)(bz * kBrick + lz);
+        const uint32_t lx = l % kEX, lyz = l / kEX, lyy = lyz % kEY, lz = lyz / kEY;
+        uint32_t bx, by, bz;
+        brick_coords((uint32_t)bidx, nbx, nby, bx, by, bz);
+        const int x = (int)(bx * kBX + lx), y = (int)(by * kBY + lyy), z = (int)(bz * kBZ + lz);
         float out[6];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -1680,6 +1698,7 @@ __global__ __launch_bounds__(256) void grad_field_kernel(const float *__restrict
 template <typename VT>
 __global__ __launch_bounds__(256) void brick_range_kernel(const VT *__restrict__ bricks,
                                                           uint32_t nbricks, uint32_t per_brick,
+                                                          uint32_t nbx, uint32_t nby,
                                                           float2 *__restrict__ range)
 {
     const uint32_t lane = threadIdx.x & 63;
@@ -1700,7 +1719,10 @@ __global__ __launch_bounds__(256) void brick_range_kernel(const VT *__restrict__
         hi = fmaxf(hi, __shfl_xor(hi, off, 64));
     }
     const bool any_nan = __ballot(nan) != 0;
-    if (lane == 0) range[b] = any_nan ? make_float2(NAN, NAN) : make_float2(lo, hi);
+    // range is indexed by the brick grid (x-fastest), whatever the memory order
+    uint32_t bx, by, bz;
+    brick_coords(b, nbx, nby, bx, by, bz);
+    if (lane == 0) range[(bz * nby + by) * nbx + bx] = any_nan ? make_float2(NAN, NAN) : make_float2(lo, hi);
 }
 
 // One thread per brick: 0 if the brick can produce a visible sample, kSkipCap if EMPTY.
@@ -1898,11 +1920,7 @@ __global__ __launch_bounds__(256) void unbrick_kernel(const T *__restrict__ bric
         const size_t yz = g / nx;
         const uint32_t y = (uint32_t)(yz % ny), z = z0 + (uint32_t)(yz / ny);
         const uint32_t pi = x + kPad, pj = y + kPad, pk = z + kPad;
-        const size_t b = ((size_t)(pk >> kBrickShift) * nby + (pj >> kBrickShift)) * nbx +
-                         (pi >> kBrickShift);
-        const size_t l = ((size_t)(pk & (kBrick - 1)) * kStore + (pj & (kBrick - 1))) * kStore +
-                         (pi & (kBrick - 1));
-        dst[g] = bricks[(b * kBrickElems + l) * vpe];
+        dst[g] = bricks[cell_offset((int)pi, (int)pj, (int)pk, nbx, nby) * vpe];
     }
 }
 
@@ -1910,7 +1928,7 @@ template <typename SrcT>
 hipError_t brick_from(const void *src, void *dst, uint32_t nx, uint32_t ny, uint32_t nz,
                       int storage, hipStream_t s)
 {
-    const uint32_t nbx = bricks_for(nx), nby = bricks_for(ny), nbz = bricks_for(nz);
+    const uint32_t nbx = bricks_for(nx, 0), nby = bricks_for(ny, 1), nbz = bricks_for(nz, 2);
     const size_t total = (size_t)nbx * nby * nbz * kBrickElems;  // elements
     const SrcT *sp = static_cast<const SrcT *>(src);
     switch (storage) {
@@ -1977,7 +1995,7 @@ hipError_t launch_unbrick(int storage, const void *bricks, void *dst, uint32_t n
 {
     const size_t n = (size_t)nx * ny * cz;
     const unsigned g = grid_for(n);
-    const uint32_t bx = bricks_for(nx), by = bricks_for(ny);
+    const uint32_t bx = bricks_for(nx, 0), by = bricks_for(ny, 1);
     switch (storage) {
         case ST_U8: case ST_I8: hipLaunchKernelGGL((unbrick_kernel<uint8_t>), dim3(g), dim3(256), 0, s, (const uint8_t *)bricks, (uint8_t *)dst, nx, ny, bx, by, z0, n); break;
         case ST_U16: case ST_I16: hipLaunchKernelGGL((unbrick_kernel<uint16_t>), dim3(g), dim3(256), 0, s, (const uint16_t *)bricks, (uint16_t *)dst, nx, ny, bx, by, z0, n); break;
@@ -2084,17 +2102,18 @@ hipError_t launch_assemble(const void *gathered, void *out, int out_format, uint
     return hipGetLastError();
 }
 
-hipError_t launch_brick_range(int storage, const void *bricks, uint32_t nbricks,
-                              float2 *range_dev, hipStream_t s)
+hipError_t launch_brick_range(int storage, const void *bricks, uint32_t nbx, uint32_t nby,
+                              uint32_t nbz, float2 *range_dev, hipStream_t s)
 {
+    const uint32_t nbricks = nbx * nby * nbz;
     const unsigned g = (nbricks + 3) / 4;
     const uint32_t per = kBrickElems * (uint32_t)voxels_per_element(storage);
     switch (storage) {
-        case ST_U8: hipLaunchKernelGGL((brick_range_kernel<uint8_t>), dim3(g), dim3(256), 0, s, (const uint8_t *)bricks, nbricks, per, range_dev); break;
-        case ST_I8: hipLaunchKernelGGL((brick_range_kernel<int8_t>), dim3(g), dim3(256), 0, s, (const int8_t *)bricks, nbricks, per, range_dev); break;
-        case ST_U16: hipLaunchKernelGGL((brick_range_kernel<uint16_t>), dim3(g), dim3(256), 0, s, (const uint16_t *)bricks, nbricks, per, range_dev); break;
-        case ST_I16: hipLaunchKernelGGL((brick_range_kernel<int16_t>), dim3(g), dim3(256), 0, s, (const int16_t *)bricks, nbricks, per, range_dev); break;
-        default: hipLaunchKernelGGL((brick_range_kernel<float>), dim3(g), dim3(256), 0, s, (const float *)bricks, nbricks, per, range_dev); break;
+        case ST_U8: hipLaunchKernelGGL((brick_range_kernel<uint8_t>), dim3(g), dim3(256), 0, s, (const uint8_t *)bricks, nbricks, per, nbx, nby, range_dev); break;
+        case ST_I8: hipLaunchKernelGGL((brick_range_kernel<int8_t>), dim3(g), dim3(256), 0, s, (const int8_t *)bricks, nbricks, per, nbx, nby, range_dev); break;
+        case ST_U16: hipLaunchKernelGGL((brick_range_kernel<uint16_t>), dim3(g), dim3(256), 0, s, (const uint16_t *)bricks, nbricks, per, nbx, nby, range_dev); break;
+        case ST_I16: hipLaunchKernelGGL((brick_range_kernel<int16_t>), dim3(g), dim3(256), 0, s, (const int16_t *)bricks, nbricks, per, nbx, nby, range_dev); break;
+        default: hipLaunchKernelGGL((brick_range_kernel<float>), dim3(g), dim3(256), 0, s, (const float *)bricks, nbricks, per, nbx, nby, range_dev); break;
     }
     return hipGetLastError();
 }
@@ -2102,7 +2121,7 @@ hipError_t launch_brick_range(int storage, const void *bricks, uint32_t nbricks,
 hipError_t launch_grad_field(const float *bricks, float *grad, uint32_t nx, uint32_t ny,
                              uint32_t nz, hipStream_t s)
 {
-    const uint32_t nbx = bricks_for(nx), nby = bricks_for(ny), nbz = bricks_for(nz);
+    const uint32_t nbx = bricks_for(nx, 0), nby = bricks_for(ny, 1), nbz = bricks_for(nz, 2);
     const size_t total = (size_t)nbx * nby * nbz * kBrickElems;
     hipLaunchKernelGGL(grad_field_kernel, dim3(grid_bricks(total)), dim3(256), 0, s, bricks, grad,
                        nx, ny, nz, nbx, nby, total);
