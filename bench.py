@@ -63,7 +63,8 @@ CONFIGS = {
                shading=0, ert=0.0, seed=1, workload="C1: 64^3 f32, 256x256 (the CPU plumbing case)"),
     "c5": dict(dims=(2048, 2048, 2048), dtype=np.uint8, W=4096, H=4096, cam="fill", tf="tf2",
                shading=0, ert=0.0, seed=11,
-               workload="C5: 2048^3 u8 bricked (49.5 GB resident in HBM), 4096x4096"),
+               workload="C5: 2048^3 u8 bricked (plain 7x8x8-cell bricks, 12.4 GB resident in HBM), "
+                        "4096x4096"),
 }
 
 
@@ -520,6 +521,7 @@ def main():
                 "reference_equivalent_samples_per_frame": ref_samples,
                 "shaded_samples_per_frame": fstats["shaded_samples"],
                 "rays_per_frame": fstats["rays"],
+                "volume_resident_bytes": rp.volume_bytes(),
             },
             "roofline": {
                 "bound": "hbm",

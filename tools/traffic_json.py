@@ -14,7 +14,7 @@ import json
 import os
 import sys
 
-CONFIGS = ("c3", "c3_ref", "c3_default", "c2", "c4")
+CONFIGS = ("c3", "c3_ref", "c3_default", "c2", "c4", "c5")
 
 
 def frame_kernel(name):

@@ -294,8 +294,8 @@ int set_bricks(vr_ctx *c, int storage, uint32_t nx, uint32_t ny, uint32_t nz, vo
 {
     c->range_valid = c->dist_valid = false;  // the bricks are about to be rewritten
     c->grad_valid = false;
-    const size_t bytes = (size_t)bricks_for(nx, 0) * bricks_for(ny, 1) * bricks_for(nz, 2) *
-                         kBrickElems * element_size(storage);
+    const size_t bytes = (size_t)bricks_for(nx, 0, storage) * bricks_for(ny, 1, storage) *
+                         bricks_for(nz, 2, storage) * brick_elems(storage) * element_size(storage);
     if (c->bricks && c->brick_bytes == bytes) {
         *out = c->bricks;
         return VR_OK;
@@ -306,7 +306,7 @@ int set_bricks(vr_ctx *c, int storage, uint32_t nx, uint32_t ny, uint32_t nz, vo
         c->brick_bytes = 0;
     }
     void *p = nullptr;
-    hipError_t e = hipMalloc(&p, bytes);
+    hipError_t e = hipMalloc(&p, bytes + kBrickSlackBytes);  // wide loads past the last brick
     if (e != hipSuccess) return hip_fail(c, e, "hipMalloc(volume bricks)");
     c->bricks = p;
     c->brick_bytes = bytes;
@@ -398,15 +398,17 @@ int check_params(vr_ctx *c, const vr_params *p)
 // Pipelined march (two samples of a ray in flight, vr_kernels.hip PIPE): always for shaded
 // frames (-6% over the view sweep); for unshaded launches of fewer than kPipelineMaxWaves
 // wavefronts -- one rank's share of a multi-GPU frame -- where per-ray latency, not the
-// chip's throughput, bounds the kernel (N = 8 rank share: 0.153 -> 0.094 ms); and for
-// volumes of >= kPipelineMinBytes bricked bytes, whose gathers miss the caches more
-// (C4 1024^3 u8 -12%, C5 2048^3 u8 -9%; a 256^3 u8 or 512^3 f32 full frame loses).
-// VR_PIPELINE=0/1 overrides (A/B).
-bool use_pipeline(bool shading, uint32_t tiles, size_t volume_bytes)
+// chip's throughput, bounds the kernel (N = 8 rank share: 0.153 -> 0.094 ms); and for large
+// volumes, whose gathers miss the caches more: >= kPipelineMinBytes bricked bytes, or
+// >= kPipelineMinVoxels voxels (C4 1024^3 u8 in plain bricks, 1.6 GB: 421 -> 451 Gsamples/s,
+// every view 7-10% faster serially; C2 256^3 u8 loses 4%, a 512^3 f32 full frame loses on
+// oblique views).  VR_PIPELINE=0/1 overrides (A/B).
+bool use_pipeline(bool shading, uint32_t tiles, const vr_ctx *c)
 {
     if (const char *e = std::getenv("VR_PIPELINE")) return e[0] == '1';
+    const size_t voxels = (size_t)c->nx * c->ny * c->nz;
     return shading || tiles * (kThreadsPerTile / 64) < kPipelineMaxWaves ||
-           volume_bytes >= kPipelineMinBytes;
+           c->brick_bytes >= kPipelineMinBytes || voxels >= kPipelineMinVoxels;
 }
 
 // Lane-pair march (two lanes per ray, each lane pipelined) for SHADED launches of fewer than
@@ -450,8 +452,8 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.nx = c->nx;
     P.ny = c->ny;
     P.nz = c->nz;
-    P.nbx = bricks_for(c->nx, 0);
-    P.nby = bricks_for(c->ny, 1);
+    P.nbx = bricks_for(c->nx, 0, c->storage);
+    P.nby = bricks_for(c->ny, 1, c->storage);
     P.fnx = (float)c->nx;
     P.fny = (float)c->ny;
     P.fnz = (float)c->nz;
@@ -495,7 +497,7 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.out_format = out_format;
     P.slab_default = c->smin[0] == 0.0f && c->smin[1] == 0.0f && c->smin[2] == 0.0f &&
                      c->smax[0] == 1.0f && c->smax[1] == 1.0f && c->smax[2] == 1.0f;
-    P.pipelined = use_pipeline(p->shading != 0, P.tiles_x * P.tiles_y, c->brick_bytes);
+    P.pipelined = use_pipeline(p->shading != 0, P.tiles_x * P.tiles_y, c);
     P.lin = c->lin;
     P.lpx = lin_pitch_x(c->nx);
     P.lpy = c->ny + 2 * kPad;
@@ -508,7 +510,7 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
 // the march that reads them.
 int ensure_skip(vr_ctx *c, MarchParams &P, hipStream_t s)
 {
-    const size_t nb = (size_t)bricks_for(c->nx, 0) * bricks_for(c->ny, 1) * bricks_for(c->nz, 2);
+    const size_t nb = (size_t)bricks_for(c->nx, 0, c->storage) * bricks_for(c->ny, 1, c->storage) * bricks_for(c->nz, 2, c->storage);
     if (nb > 0xFFFFFFFFull) return fail(c, VR_EINVAL, "skip_empty: too many bricks");
     if (c->nbricks_alloc != nb) {
         if (c->brick_range) hipFree(c->brick_range);
@@ -522,15 +524,15 @@ int ensure_skip(vr_ctx *c, MarchParams &P, hipStream_t s)
         c->nbricks_alloc = nb;
     }
     if (!c->range_valid) {
-        HIP_TRY(c, launch_brick_range(c->storage, c->bricks, bricks_for(c->nx, 0), bricks_for(c->ny, 1),
-                                      bricks_for(c->nz, 2), c->brick_range, s),
+        HIP_TRY(c, launch_brick_range(c->storage, c->bricks, bricks_for(c->nx, 0, c->storage), bricks_for(c->ny, 1, c->storage),
+                                      bricks_for(c->nz, 2, c->storage), c->brick_range, s),
                 "brick range kernel");
         c->range_valid = true;
         c->dist_valid = false;
     }
     if (!c->dist_valid) {
-        HIP_TRY(c, launch_skip_dist(c->brick_range, bricks_for(c->nx, 0), bricks_for(c->ny, 1),
-                                    bricks_for(c->nz, 2), c->tf_nz, (int)c->tf_n, c->vmin,
+        HIP_TRY(c, launch_skip_dist(c->brick_range, bricks_for(c->nx, 0, c->storage), bricks_for(c->ny, 1, c->storage),
+                                    bricks_for(c->nz, 2, c->storage), c->tf_nz, (int)c->tf_n, c->vmin,
                                     c->vmax - c->vmin, c->skip_dist, c->skip_dist + nb, s),
                 "skip distance kernels");
         c->dist_valid = true;
@@ -1227,7 +1229,7 @@ const char *vr_kernel_name(const vr_ctx *c, const vr_params *p)
     const bool gf = p && p->shading && c->storage == ST_F32 && c->grad && c->grad_valid;
     // the full frame (row_block 16, one rank), as vr_render launches it
     const uint32_t tiles = ((c->width + 15) / 16) * ((c->height + kMarchRows - 1) / kMarchRows);
-    const bool pipe = use_pipeline(p && p->shading, tiles, c->brick_bytes) &&
+    const bool pipe = use_pipeline(p && p->shading, tiles, c) &&
                       !(p && p->skip_empty) && c->tf_n <= 256;
     if (p && use_lds(c, p)) return march_lds_kernel_name(c->storage, p->shading != 0);
     return march_kernel_name(c->storage, p && p->shading != 0, false, p && p->skip_empty != 0, gf,

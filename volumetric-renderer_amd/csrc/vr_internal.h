@@ -6,39 +6,60 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace vr {
 
-// ---- Bricked, paired-element volume layout in HBM --------------------------------------
+// ---- Bricked volume layout in HBM ----------------------------------------------------------
 // The logical volume (nx, ny, nz) is shifted by kPad = 2 zero voxels on the low side of each
-// axis ("padded index" p = logical + 2) and cut into bricks of kBX x kBY x kBZ (8^3) cells.
-// Brick b stores ELEMENTS for padded indices [8 b, 8 b + 8] on each axis (9: a 1-element
-// apron), bricks in brick_slot order, elements x-fastest in a brick.
-// An element holds more than one voxel, so that one wide load fetches a whole trilinear
-// footprint edge-on (the gather pipeline, not HBM, bounds this kernel: DESIGN.md):
-//   f32   (and 32/64-bit inputs, converted):  "z-pair"  element = {v(x,y,z), v(x,y,z+1)}, 8 B;
-//         a sample = 2 x 16-B loads (elements x, x+1 of rows y and y+1).
-//   8/16-bit integers: "yz-quad" element = {v(y,z), v(y,z+1), v(y+1,z), v(y+1,z+1)} at x,
-//         4 B (u8/i8) or 8 B (u16/i16); a sample = 1 load of elements x, x+1 (8 B / 16 B).
+// axis ("padded index" p = logical + 2) and cut into bricks of BX x BY x BZ cells (BrickGeom
+// below).  A brick stores ELEMENTS for padded indices [B b, B b + B] on each axis (B + 1: a
+// 1-element apron), bricks in brick_slot order, elements x-fastest in a brick, so every
+// trilinear footprint lies in one brick.  Per storage type:
+//   f32 (and 32/64-bit inputs, converted): "z-pair" element = {v(x,y,z), v(x,y,z+1)}, 8 B, in
+//         8^3-cell bricks; a sample = 2 x 16-B loads (elements x, x+1 of rows y and y+1).
+//         2 x (9/8)^3 = 2.85x the f32 voxels.
+//   16-bit: "yz-quad" element = {v(y,z), v(y,z+1), v(y+1,z), v(y+1,z+1)} at x, 8 B, in 8^3
+//         bricks; a sample = 1 x 16-B load of elements x, x+1.  4 x (9/8)^3 = 5.7x.
+//   8-bit: plain voxels in 7 x 8 x 8-cell bricks (8-B rows, 648-B bricks); a sample = 2 x
+//         16-B loads (rows y, y+1 of slices z and z+1, from the 4-aligned address at or below
+//         the cell).  8 x 9 x 9 / (7 x 8 x 8) = 1.45x the voxels (VR_U8_PLAIN=0: yz-quads).
 // Voxels outside [0, N) are stored as 0: CLAMP_TO_BORDER/TRANSPARENT_BLACK without a bounds
-// test.  Memory: 2 x (9/8)^3 = 2.85x the f32 voxels, 4 x (9/8)^3 = 5.7x the 8/16-bit voxels.
-// Brick geometry (compile-time): kBX x kBY x kBZ cells per brick, each axis storing cells + 1
-// elements (the apron); element (x, y, z) of a brick at (x + kEX (y + kEY z)), the brick padded
-// to kBrickElems.  Default 8^3 cells (9^3 = 729 elements).  Experiment builds may set
-// VR_BRICK_CELLS="bx,by,bz" (e.g. 15,7,8: 16-element rows = one 128-B line of f32 z-pairs) and
-// VR_BRICK_ALIGN (elements the brick size is rounded up to).
+// test.
+// Brick geometry (compile-time): BX x BY x BZ cells per brick, each axis storing cells + 1
+// elements (the apron); element (x, y, z) of a brick at x + EX (y + EY z), the brick padded to
+// Elems.  f32 and 16-bit volumes use GeomWide (default 8^3 cells, 9^3 = 729 elements), 8-bit
+// volumes GeomByte.  Experiment builds may set VR_BRICK_CELLS="bx,by,bz" (e.g. 15,7,8: 16-element
+// rows = one 128-B line of f32 z-pairs) and VR_BRICK_ALIGN (elements a brick is rounded up to).
 #ifndef VR_BRICK_CELLS
 #define VR_BRICK_CELLS 8, 8, 8
 #endif
 #ifndef VR_BRICK_ALIGN
 #define VR_BRICK_ALIGN 1
 #endif
-constexpr int kBrickCells[3] = {VR_BRICK_CELLS};
-constexpr int kBX = kBrickCells[0], kBY = kBrickCells[1], kBZ = kBrickCells[2];
-constexpr int kEX = kBX + 1, kEY = kBY + 1, kEZ = kBZ + 1;  // elements per axis
-constexpr int kRowElems = kEX;                            // element stride of y
-constexpr int kSliceElems = kEX * kEY;                    // element stride of z
-constexpr int kBrickElems = (kEX * kEY * kEZ + VR_BRICK_ALIGN - 1) / VR_BRICK_ALIGN * VR_BRICK_ALIGN;
-constexpr bool kBrickPow2 = (kBX & (kBX - 1)) == 0 && (kBY & (kBY - 1)) == 0 && (kBZ & (kBZ - 1)) == 0;
+template <int X, int Y, int Z>
+struct BrickGeom {
+    static constexpr int BX = X, BY = Y, BZ = Z;
+    static constexpr int EX = X + 1, EY = Y + 1, EZ = Z + 1;  // elements per axis
+    static constexpr int Row = EX, Slice = EX * EY;           // element strides of y, z
+    static constexpr int Elems = (EX * EY * EZ + VR_BRICK_ALIGN - 1) / VR_BRICK_ALIGN * VR_BRICK_ALIGN;
+    __host__ __device__ static constexpr int cells(int a) { return a == 0 ? X : (a == 1 ? Y : Z); }
+};
+using GeomWide = BrickGeom<VR_BRICK_CELLS>;
+// 8-bit volumes (VR_U8_PLAIN = 1): one voxel per element, bricks of 7 x 8 x 8 cells, so a brick
+// row is 8 bytes and a 648-B brick keeps every row 4-aligned: one dwordx4 from the 4-aligned
+// address at or below the cell's element holds elements x, x + 1 of rows y and y + 1 (byte
+// offsets s, s+1, s+8, s+9 with s = x mod 4 <= 3), a second one the same at z + 1.
+// VR_U8_PLAIN = 0: yz-quad elements in GeomWide bricks (one 8-B load, 5.7x the voxels).
+#ifndef VR_U8_PLAIN
+#define VR_U8_PLAIN 1
+#endif
+#ifndef VR_U8_BRICK_CELLS
+#define VR_U8_BRICK_CELLS 7, 8, 8
+#endif
+using GeomByte = std::conditional_t<VR_U8_PLAIN != 0, BrickGeom<VR_U8_BRICK_CELLS>, GeomWide>;
+// wide loads of the last brick read up to this many bytes past its end
+constexpr size_t kBrickSlackBytes = 64;
 // VR_F32_PLAIN=1 (experiment builds): f32 elements hold one voxel (no z-pair duplication);
 // a sample is then 4 x 8-B loads (elements x, x+1 of the rows (y|y+1, z|z+1)).
 #ifndef VR_F32_PLAIN
@@ -56,14 +77,6 @@ constexpr int kPad = 2;
 #endif
 constexpr int kGroupShift = VR_BRICK_GROUP_SHIFT;
 constexpr uint32_t kGroupMask = (1u << kGroupShift) - 1;
-
-// Bricks along axis a (0 x, 1 y, 2 z) of an n-voxel axis: fetch base indices lie in [1, N + 1]
-// (march) and gradient taps reach one element below and (in z-pair x/y) two above, i.e.
-// padded [0, N + 3]; rounded up to whole brick groups.
-inline uint32_t bricks_for(uint32_t n, int a)
-{
-    return ((n + 3) / (uint32_t)kBrickCells[a] + 1 + kGroupMask) & ~kGroupMask;
-}
 
 // Bits 0..g-1 of v moved to bits 0, 3, 6, ... (one axis of a Morton code).
 __host__ __device__ __forceinline__ uint32_t morton_spread(uint32_t v)
@@ -126,8 +139,26 @@ inline size_t storage_size(int st)
         default: return 4;
     }
 }
-inline size_t voxels_per_element(int st) { return st == ST_F32 ? kF32VoxelsPerElement : 4; }
+inline bool byte_storage(int st) { return st == ST_U8 || st == ST_I8; }
+inline size_t voxels_per_element(int st)
+{
+    return st == ST_F32 ? kF32VoxelsPerElement : (byte_storage(st) && VR_U8_PLAIN ? 1 : 4);
+}
 inline size_t element_size(int st) { return storage_size(st) * voxels_per_element(st); }
+// Brick geometry of storage type st: cells along axis a (0 x, 1 y, 2 z), elements per brick.
+inline int brick_cells(int st, int a)
+{
+    return byte_storage(st) ? GeomByte::cells(a) : GeomWide::cells(a);
+}
+inline size_t brick_elems(int st) { return byte_storage(st) ? GeomByte::Elems : GeomWide::Elems; }
+
+// Bricks along axis a of an n-voxel axis: fetch base indices lie in [1, N + 1] (march) and
+// gradient taps reach one element below and (in z-pair x/y) two above, i.e. padded [0, N + 3];
+// rounded up to whole brick groups.
+inline uint32_t bricks_for(uint32_t n, int a, int st)
+{
+    return ((n + 3) / (uint32_t)brick_cells(st, a) + 1 + kGroupMask) & ~kGroupMask;
+}
 
 // ---- Kernel parameters (one frame) -------------------------------------------------------
 struct MarchParams {
@@ -203,6 +234,7 @@ const char *march_lds_kernel_name(int storage, bool shade);
 // Wavefront count below which a launch uses the pipelined kernel (see build_params).
 constexpr uint32_t kPipelineMaxWaves = 24576;  // between N = 2 (16 K) and N = 1 (33 K) at 1080p
 constexpr size_t kPipelineMinBytes = 4ull << 30;  // large volumes: always pipelined
+constexpr size_t kPipelineMinVoxels = 1ull << 29;
 // march_kernel tiles: 16 pixels wide, kMarchRows tall, one lane per pixel (experiment
 // builds may set VR_MARCH_ROWS=32: 512-thread workgroups whose 8 wavefronts share one CU's L1)
 #ifndef VR_MARCH_ROWS

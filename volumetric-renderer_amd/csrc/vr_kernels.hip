@@ -60,20 +60,28 @@ typedef uint32_t u4a __attribute__((ext_vector_type(4))) __attribute__((aligned(
 template <typename VT>
 constexpr bool kZPair = std::is_same<VT, float>::value;
 // bytes per element; 32-bit words per element (quad layouts)
+// 8-bit volumes stored one voxel per element (VR_U8_PLAIN, vr_internal.h)
 template <typename VT>
-constexpr int kElemBytes = kZPair<VT> ? 4 * (int)kF32VoxelsPerElement : 4 * (int)sizeof(VT);
+constexpr bool kPlainByte = sizeof(VT) == 1 && VR_U8_PLAIN;
+template <typename VT>
+constexpr int kElemBytes = kZPair<VT> ? 4 * (int)kF32VoxelsPerElement
+                                      : (kPlainByte<VT> ? 1 : 4 * (int)sizeof(VT));
+template <typename VT>
+using GeomOf = std::conditional_t<sizeof(VT) == 1, GeomByte, GeomWide>;
 template <typename VT>
 constexpr int kQuadWords = sizeof(VT) == 1 ? 1 : 2;
 
 // Element index of padded cell (pi, pj, pk) in the bricked layout (vr_internal.h).  64-bit:
 // a 2048^3 volume has 257^3 x 729 elements.  (A 32-bit index with SGPR-base loads for
 // volumes < 4 GiB measured slower on the shaded kernel and on the diagonal view.)
+template <typename VT>
 __device__ __forceinline__ size_t cell_offset(int pi, int pj, int pk, uint32_t nbx, uint32_t nby)
 {
+    using G = GeomOf<VT>;
     const uint32_t ux = (uint32_t)pi, uy = (uint32_t)pj, uz = (uint32_t)pk;
-    const uint32_t bx = ux / kBX, by = uy / kBY, bz = uz / kBZ;
-    const uint32_t l = ((uz - bz * kBZ) * kEY + (uy - by * kBY)) * kEX + (ux - bx * kBX);
-    return (size_t)brick_slot(bx, by, bz, nbx, nby) * (size_t)kBrickElems + l;
+    const uint32_t bx = ux / G::BX, by = uy / G::BY, bz = uz / G::BZ;
+    const uint32_t l = ((uz - bz * G::BZ) * G::EY + (uy - by * G::BY)) * G::EX + (ux - bx * G::BX);
+    return (size_t)brick_slot(bx, by, bz, nbx, nby) * (size_t)G::Elems + l;
 }
 
 // Trilinear filter of a 2x2x2 cell given its voxels v[dz][dy][dx]: lerp x, then y, then z
@@ -103,6 +111,15 @@ __device__ __forceinline__ f2v tri8x2(f2v v000, f2v v100, f2v v010, f2v v110, f2
     const f2v c0 = lerp2(c00, c10, ay);
     const f2v c1 = lerp2(c01, c11, ay);
     return lerp2(c0, c1, az);
+}
+
+// Byte b of w as the voxel value (float of an 8-bit integer is exact).
+template <typename VT>
+__device__ __forceinline__ float byte_value(uint32_t w, int b)
+{
+    const uint32_t u = (w >> (8 * b)) & 0xFFu;
+    if constexpr (std::is_signed<VT>::value) return (float)(int)(int8_t)u;
+    return (float)u;
 }
 
 // Component c of a yz-quad element held in 32-bit words w (c: 0 (y,z), 1 (y,z+1), 2 (y+1,z),
@@ -171,13 +188,13 @@ struct Cell8 {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const f2a q = *reinterpret_cast<const f2a *>(
-                    base + (e + (size_t)((r & 1) * kRowElems + (r >> 1) * kSliceElems)) * 4);
+                    base + (e + (size_t)((r & 1) * GeomWide::Row + (r >> 1) * GeomWide::Slice)) * 4);
                 v[2 * r] = q.x;
                 v[2 * r + 1] = q.y;
             }
         } else if constexpr (kZPair<VT>) {
             const f4a r0 = zpair_load2(base, e);
-            const f4a r1 = zpair_load2(base, e + kRowElems);
+            const f4a r1 = zpair_load2(base, e + GeomWide::Row);
             v[0] = r0.x;
             v[4] = r0.y;
             v[1] = r0.z;
@@ -186,6 +203,22 @@ struct Cell8 {
             v[6] = r1.y;
             v[3] = r1.z;
             v[7] = r1.w;
+        } else if constexpr (kPlainByte<VT>) {
+            // one dwordx4 per slice from the 4-aligned address at or below e (bricks and rows
+            // are 4-aligned: s = e mod 4 = x mod 4): bytes s, s+1 = row y, s+8, s+9 = row y+1
+            const size_t a = e & ~(size_t)3;
+            const uint32_t sh = (uint32_t)e & 3u;
+            const u4a q0 = *reinterpret_cast<const u4a *>(base + a);
+            const u4a q1 = *reinterpret_cast<const u4a *>(base + a + GeomByte::Slice);
+            const uint32_t w[4] = {__builtin_amdgcn_alignbyte(q0.y, q0.x, sh),
+                                   __builtin_amdgcn_alignbyte(q0.w, q0.z, sh),
+                                   __builtin_amdgcn_alignbyte(q1.y, q1.x, sh),
+                                   __builtin_amdgcn_alignbyte(q1.w, q1.z, sh)};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {  // r = dy + 2 dz
+                v[2 * r] = byte_value<VT>(w[r], 0);
+                v[2 * r + 1] = byte_value<VT>(w[r], 1);
+            }
         } else {
             constexpr int QW = kQuadWords<VT>;
             uint32_t w[2 * QW];
@@ -239,9 +272,10 @@ __device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e
                                          long bz_stride, float ax, float ay, float az, float &gx,
                                          float &gy, float &gz)
 {
-    constexpr long S = kRowElems, S2 = kSliceElems, B = kBrickElems;
-    constexpr long Lx = kBX - 1, Ly = kBY - 1, Lz = kBZ - 1;
-    const int lx = pi % kBX, ly = pj % kBY, lz = pk % kBZ;
+    using G = GeomOf<VT>;
+    constexpr long S = G::Row, S2 = G::Slice, B = G::Elems;
+    constexpr long Lx = G::BX - 1, Ly = G::BY - 1, Lz = G::BZ - 1;
+    const int lx = pi % G::BX, ly = pj % G::BY, lz = pk % G::BZ;
     // element-index deltas of the taps one element below / two above the cell's low corner;
     // a tap outside the brick reads the neighbouring brick (constant strides in x-fastest
     // brick order, the neighbour's slot otherwise)
@@ -255,7 +289,7 @@ __device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e
         dzp = lz < Lz ? 2 * S2 : (bz_stride - (Lz - 1) * S2);
     } else {
         auto cross = [&](int ox, int oy, int oz) {
-            return (long)cell_offset(pi + ox, pj + oy, pk + oz, nbx, nby) - (long)e;
+            return (long)cell_offset<VT>(pi + ox, pj + oy, pk + oz, nbx, nby) - (long)e;
         };
         dxm = lx > 0 ? -1 : cross(-1, 0, 0);
         dxp = lx < Lx ? 2 : cross(2, 0, 0);
@@ -313,6 +347,38 @@ __device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e
         Dy[4] = v[6] - ym.y;  Dy[5] = v[7] - ym.w;  Dy[6] = yp.y - v[4];  Dy[7] = yp.w - v[5];
         Dz[0] = v[4] - zm0.x; Dz[1] = v[5] - zm0.z; Dz[2] = v[6] - zm1.x; Dz[3] = v[7] - zm1.z;
         Dz[4] = zp0.y - v[0]; Dz[5] = zp0.w - v[1]; Dz[6] = zp1.y - v[2]; Dz[7] = zp1.w - v[3];
+    } else if constexpr (kPlainByte<VT>) {
+        // the 24 outer voxels one byte load each (8-bit shading is off the benchmarked path)
+        auto ld = [&](long o) {
+            return byte_value<VT>((uint32_t)*reinterpret_cast<const uint8_t *>(base + e + o), 0);
+        };
+#pragma unroll
+        for (int dz_ = 0; dz_ < 2; ++dz_)
+#pragma unroll
+            for (int dy_ = 0; dy_ < 2; ++dy_) {
+                const int o = 2 * dy_ + 4 * dz_;
+                const long r = dy_ * S + dz_ * S2;
+                Dx[o] = v[o + 1] - ld(dxm + r);
+                Dx[o + 1] = ld(dxp + r) - v[o];
+            }
+#pragma unroll
+        for (int dz_ = 0; dz_ < 2; ++dz_)
+#pragma unroll
+            for (int dx_ = 0; dx_ < 2; ++dx_) {
+                const int o = dx_ + 4 * dz_;
+                const long r = dx_ + dz_ * S2;
+                Dy[o] = v[o + 2] - ld(dym + r);
+                Dy[o + 2] = ld(dyp + r) - v[o];
+            }
+#pragma unroll
+        for (int dy_ = 0; dy_ < 2; ++dy_)
+#pragma unroll
+            for (int dx_ = 0; dx_ < 2; ++dx_) {
+                const int o = dx_ + 2 * dy_;
+                const long r = dx_ + dy_ * S;
+                Dz[o] = v[o + 4] - ld(dzm + r);
+                Dz[o + 4] = ld(dzp + r) - v[o];
+            }
     } else {
         constexpr int QW = kQuadWords<VT>;
         uint32_t xm[QW], xp[QW], ym[2 * QW], yp[2 * QW], zm[2 * QW], zp[2 * QW];
@@ -359,7 +425,7 @@ __device__ __forceinline__ void grad_field(const char *__restrict__ gbase, size_
     float Dx[8], Dy[8], Dz[8];
 #pragma unroll
     for (int dy_ = 0; dy_ < 2; ++dy_) {
-        const char *row = gbase + (e + (size_t)dy_ * kRowElems) * kGradElemBytes;
+        const char *row = gbase + (e + (size_t)dy_ * GeomWide::Row) * kGradElemBytes;
         const f4a r0 = *reinterpret_cast<const f4a *>(row);       // Dx(x) z,z+1  Dy(x) z,z+1
         const f4a r1 = *reinterpret_cast<const f4a *>(row + 16);  // Dz(x) z,z+1  Dx(x+1) z,z+1
         const f4a r2 = *reinterpret_cast<const f4a *>(row + 32);  // Dy(x+1) ...  Dz(x+1) ...
@@ -676,8 +742,9 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
     if (tf_in_lds)
         for (int i = tid; i < 2 * (P.tf_n + 2); i += (int)kThreadsPerTile) s_tf[i] = P.tf[i];
     __syncthreads();
-    const long by_stride = (long)P.nbx * kBrickElems;  // elements between brick rows/slabs
-    const long bz_stride = (long)P.nbx * P.nby * kBrickElems;
+    using G = GeomOf<VT>;
+    const long by_stride = (long)P.nbx * G::Elems;  // elements between brick rows/slabs
+    const long bz_stride = (long)P.nbx * P.nby * G::Elems;
 
     // wavefront -> (ww x wh) pixels, ww = 2^wave_w_shift, together tiling the 16 x kMarchRows tile
     const uint32_t wave = tid >> 6, lane = tid & 63;
@@ -740,7 +807,7 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
             S.pi = i + kPad;
             S.pj = j + kPad;
             S.pk = kk + kPad;
-            S.ce = cell_offset(S.pi, S.pj, S.pk, P.nbx, P.nby);
+            S.ce = cell_offset<VT>(S.pi, S.pj, S.pk, P.nbx, P.nby);
             S.c.load(vol, S.ce);
         };
         auto consume = [&](const Stage &S) -> bool {  // true: the ray ends (T == 0 or ERT)
@@ -794,8 +861,8 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
             if (SKIP) {
                 // skip_empty: distance (in bricks) from the cell's brick to the nearest brick
                 // that can produce a visible sample (classify_kernel); cached per brick
-                const uint32_t bb = ((uint32_t)pk / kBZ * P.nby + (uint32_t)pj / kBY) * P.nbx +
-                                    (uint32_t)pi / kBX;
+                const uint32_t bb = ((uint32_t)pk / G::BZ * P.nby + (uint32_t)pj / G::BY) * P.nbx +
+                                    (uint32_t)pi / G::BX;
                 if (bb != cur_brick) {
                     cur_brick = bb;
                     cur_dist = P.skip_dist[bb];
@@ -816,16 +883,17 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
                     // with the same float additions as the reference loop, so the first
                     // non-empty sample is reached at the bit-identical position.
                     float kf = (float)min(nsteps - 1 - it, kMaxLeap);
-                    const int bi[3] = {pi / kBX, pj / kBY, pk / kBZ};
+                    const int bi[3] = {pi / G::BX, pj / G::BY, pk / G::BZ};
                     const float pp[3] = {p0, p1, p2}, dd[3] = {d0, d1, d2};
                     const float fn[3] = {P.fnx, P.fny, P.fnz};
 #pragma unroll
                     for (int a = 0; a < 3; ++a) {
                         const float u = pp[a] * fn[a] - 0.5f;
-                        const float reach = (float)((int)(dist - 1) * kBrickCells[a]);
+                        const int bc = G::cells(a);
+                        const float reach = (float)((int)(dist - 1) * bc);
                         const float room = dd[a] > 0.0f
-                                               ? (float)((bi[a] + 1) * kBrickCells[a] - kPad) + reach - u
-                                               : u - (float)(bi[a] * kBrickCells[a] - kPad) + reach;
+                                               ? (float)((bi[a] + 1) * bc - kPad) + reach - u
+                                               : u - (float)(bi[a] * bc - kPad) + reach;
                         // NaN (axis not moving) is ignored by fminf
                         kf = fminf(kf, (room - leap_margin[a]) * inv_du[a]);
                     }
@@ -838,7 +906,7 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
                     it += k;
                 }
             } else {
-                const size_t ce = cell_offset(pi, pj, pk, P.nbx, P.nby);
+                const size_t ce = cell_offset<VT>(pi, pj, pk, P.nbx, P.nby);
                 Cell8<VT> c;
                 c.load(vol, ce);
                 const float d = c.tri(ax, ay, az);
@@ -938,8 +1006,9 @@ __global__ __launch_bounds__(kThreads) void march_pair_kernel(const MarchParams 
 #ifdef VR_WG_TIMES
     const unsigned long long wg_t0 = wg_start;
 #endif
-    const long by_stride = (long)P.nbx * kBrickElems;
-    const long bz_stride = (long)P.nbx * P.nby * kBrickElems;
+    using G = GeomOf<VT>;
+    const long by_stride = (long)P.nbx * G::Elems;
+    const long bz_stride = (long)P.nbx * P.nby * G::Elems;
 
     // L lanes per ray; wavefront = 16 x (4 / L) pixels; workgroup tile 16 x (16 / L)
     const uint32_t wave = tid >> 6, lane = tid & 63, q = lane / L, half = lane % L;
@@ -987,7 +1056,7 @@ __global__ __launch_bounds__(kThreads) void march_pair_kernel(const MarchParams 
         S.pi = i + kPad;
         S.pj = j + kPad;
         S.pk = kk + kPad;
-        S.ce = cell_offset(S.pi, S.pj, S.pk, P.nbx, P.nby);
+        S.ce = cell_offset<VT>(S.pi, S.pj, S.pk, P.nbx, P.nby);
         S.c.load(vol, S.ce);
     };
     // this lane's sample -> exchange -> the pair's two samples composited in order; true: the
@@ -1499,29 +1568,29 @@ template <typename SrcT, typename DstT>
 __global__ __launch_bounds__(256) void brick_kernel(const SrcT *__restrict__ src,
                                                     DstT *__restrict__ dst, uint32_t nx,
                                                     uint32_t ny, uint32_t nz, uint32_t nbx,
-                                                    uint32_t nby, size_t total)
+                                                    uint32_t nby, size_t nbricks)
 {
     constexpr bool zpair = std::is_same<DstT, float>::value;
+    using G = GeomOf<DstT>;
     // a workgroup per brick (grid-stride over bricks), its threads over the brick's elements:
     // brick coordinates once per brick, element coordinates by constant divisors, and each
     // brick's elements written contiguously
-    const size_t nbricks = total / kBrickElems;
     for (size_t bidx = blockIdx.x; bidx < nbricks; bidx += gridDim.x)
-    for (uint32_t l = threadIdx.x; l < (uint32_t)kBrickElems; l += blockDim.x) {
-        const size_t g = bidx * kBrickElems + l;
-        const uint32_t lx = l % kEX, lyz = l / kEX, lyy = lyz % kEY, lz = lyz / kEY;
+    for (uint32_t l = threadIdx.x; l < (uint32_t)G::Elems; l += blockDim.x) {
+        const size_t g = bidx * G::Elems + l;
+        const uint32_t lx = l % G::EX, lyz = l / G::EX, lyy = lyz % G::EY, lz = lyz / G::EY;
         uint32_t bx, by, bz;
         brick_coords((uint32_t)bidx, nbx, nby, bx, by, bz);
-        const long x = (long)bx * kBX + lx - kPad;
-        const long y = (long)by * kBY + lyy - kPad;
-        const long z = (long)bz * kBZ + lz - kPad;
+        const long x = (long)bx * G::BX + lx - kPad;
+        const long y = (long)by * G::BY + lyy - kPad;
+        const long z = (long)bz * G::BZ + lz - kPad;
         auto at = [&](long xx, long yy, long zz) -> DstT {
             if (xx < 0 || yy < 0 || zz < 0 || xx >= (long)nx || yy >= (long)ny || zz >= (long)nz)
                 return (DstT)0;
             return (DstT)src[(size_t)xx + (size_t)nx * ((size_t)yy + (size_t)ny * (size_t)zz)];
         };
         // one store per element (a u8 quad is one dword, not four byte stores)
-        if constexpr (zpair && VR_F32_PLAIN) {
+        if constexpr ((zpair && VR_F32_PLAIN) || kPlainByte<DstT>) {
             dst[g] = at(x, y, z);
         } else if constexpr (zpair) {
             reinterpret_cast<float2 *>(dst)[g] = make_float2(at(x, y, z), at(x, y, z + 1));
@@ -1651,7 +1720,7 @@ __device__ __forceinline__ float padded_voxel(const float *__restrict__ bricks, 
     if (px < kPad || py < kPad || pz < kPad || px >= (int)nx + kPad || py >= (int)ny + kPad ||
         pz >= (int)nz + kPad)
         return 0.0f;
-    return bricks[kF32VoxelsPerElement * cell_offset(px, py, pz, nbx, nby)];
+    return bricks[kF32VoxelsPerElement * cell_offset<float>(px, py, pz, nbx, nby)];
 }
 
 // One thread per stored element: D_e(p) = v(p + e) - v(p - e) (the oracle's dvox) for the
@@ -1659,19 +1728,19 @@ __device__ __forceinline__ float padded_voxel(const float *__restrict__ bricks, 
 __global__ __launch_bounds__(256) void grad_field_kernel(const float *__restrict__ bricks,
                                                          float *__restrict__ grad, uint32_t nx,
                                                          uint32_t ny, uint32_t nz, uint32_t nbx,
-                                                         uint32_t nby, size_t total)
+                                                         uint32_t nby, size_t nbricks)
 {
+    using G = GeomWide;
     // a workgroup per brick (grid-stride over bricks), its threads over the brick's elements:
     // brick coordinates once per brick, element coordinates by constant divisors, and each
     // brick's elements written contiguously
-    const size_t nbricks = total / kBrickElems;
     for (size_t bidx = blockIdx.x; bidx < nbricks; bidx += gridDim.x)
-    for (uint32_t l = threadIdx.x; l < (uint32_t)kBrickElems; l += blockDim.x) {
-        const size_t g = bidx * kBrickElems + l;
-        const uint32_t lx = l % kEX, lyz = l / kEX, lyy = lyz % kEY, lz = lyz / kEY;
+    for (uint32_t l = threadIdx.x; l < (uint32_t)G::Elems; l += blockDim.x) {
+        const size_t g = bidx * G::Elems + l;
+        const uint32_t lx = l % G::EX, lyz = l / G::EX, lyy = lyz % G::EY, lz = lyz / G::EY;
         uint32_t bx, by, bz;
         brick_coords((uint32_t)bidx, nbx, nby, bx, by, bz);
-        const int x = (int)(bx * kBX + lx), y = (int)(by * kBY + lyy), z = (int)(bz * kBZ + lz);
+        const int x = (int)(bx * G::BX + lx), y = (int)(by * G::BY + lyy), z = (int)(bz * G::BZ + lz);
         float out[6];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -1893,9 +1962,8 @@ hipError_t launch_march_vt(bool shade, bool count, const MarchParams &p, hipStre
 }
 
 // workgroups for the per-brick kernels (brick_kernel, grad_field_kernel): one per brick
-inline unsigned grid_bricks(size_t total_elems)
+inline unsigned grid_bricks(size_t nb)
 {
-    const size_t nb = total_elems / kBrickElems;
     return (unsigned)(nb > 65536 ? 65536 : (nb == 0 ? 1 : nb));
 }
 
@@ -1913,14 +1981,15 @@ __global__ __launch_bounds__(256) void unbrick_kernel(const T *__restrict__ bric
                                                      uint32_t ny, uint32_t nbx, uint32_t nby,
                                                      uint32_t z0, size_t count)
 {
-    constexpr size_t vpe = std::is_same<T, float>::value ? kF32VoxelsPerElement : 4;
+    constexpr size_t vpe = std::is_same<T, float>::value ? kF32VoxelsPerElement
+                                                         : (kPlainByte<T> ? 1 : 4);
     for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < count;
          g += (size_t)gridDim.x * blockDim.x) {
         const uint32_t x = (uint32_t)(g % nx);
         const size_t yz = g / nx;
         const uint32_t y = (uint32_t)(yz % ny), z = z0 + (uint32_t)(yz / ny);
         const uint32_t pi = x + kPad, pj = y + kPad, pk = z + kPad;
-        dst[g] = bricks[cell_offset((int)pi, (int)pj, (int)pk, nbx, nby) * vpe];
+        dst[g] = bricks[cell_offset<T>((int)pi, (int)pj, (int)pk, nbx, nby) * vpe];
     }
 }
 
@@ -1928,8 +1997,9 @@ template <typename SrcT>
 hipError_t brick_from(const void *src, void *dst, uint32_t nx, uint32_t ny, uint32_t nz,
                       int storage, hipStream_t s)
 {
-    const uint32_t nbx = bricks_for(nx, 0), nby = bricks_for(ny, 1), nbz = bricks_for(nz, 2);
-    const size_t total = (size_t)nbx * nby * nbz * kBrickElems;  // elements
+    const uint32_t nbx = bricks_for(nx, 0, storage), nby = bricks_for(ny, 1, storage),
+                   nbz = bricks_for(nz, 2, storage);
+    const size_t total = (size_t)nbx * nby * nbz;  // bricks
     const SrcT *sp = static_cast<const SrcT *>(src);
     switch (storage) {
         case ST_U8: hipLaunchKernelGGL((brick_kernel<SrcT, uint8_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (uint8_t *)dst, nx, ny, nz, nbx, nby, total); break;
@@ -1995,7 +2065,7 @@ hipError_t launch_unbrick(int storage, const void *bricks, void *dst, uint32_t n
 {
     const size_t n = (size_t)nx * ny * cz;
     const unsigned g = grid_for(n);
-    const uint32_t bx = bricks_for(nx, 0), by = bricks_for(ny, 1);
+    const uint32_t bx = bricks_for(nx, 0, storage), by = bricks_for(ny, 1, storage);
     switch (storage) {
         case ST_U8: case ST_I8: hipLaunchKernelGGL((unbrick_kernel<uint8_t>), dim3(g), dim3(256), 0, s, (const uint8_t *)bricks, (uint8_t *)dst, nx, ny, bx, by, z0, n); break;
         case ST_U16: case ST_I16: hipLaunchKernelGGL((unbrick_kernel<uint16_t>), dim3(g), dim3(256), 0, s, (const uint16_t *)bricks, (uint16_t *)dst, nx, ny, bx, by, z0, n); break;
@@ -2107,7 +2177,7 @@ hipError_t launch_brick_range(int storage, const void *bricks, uint32_t nbx, uin
 {
     const uint32_t nbricks = nbx * nby * nbz;
     const unsigned g = (nbricks + 3) / 4;
-    const uint32_t per = kBrickElems * (uint32_t)voxels_per_element(storage);
+    const uint32_t per = (uint32_t)(brick_elems(storage) * voxels_per_element(storage));
     switch (storage) {
         case ST_U8: hipLaunchKernelGGL((brick_range_kernel<uint8_t>), dim3(g), dim3(256), 0, s, (const uint8_t *)bricks, nbricks, per, nbx, nby, range_dev); break;
         case ST_I8: hipLaunchKernelGGL((brick_range_kernel<int8_t>), dim3(g), dim3(256), 0, s, (const int8_t *)bricks, nbricks, per, nbx, nby, range_dev); break;
@@ -2121,8 +2191,9 @@ hipError_t launch_brick_range(int storage, const void *bricks, uint32_t nbx, uin
 hipError_t launch_grad_field(const float *bricks, float *grad, uint32_t nx, uint32_t ny,
                              uint32_t nz, hipStream_t s)
 {
-    const uint32_t nbx = bricks_for(nx, 0), nby = bricks_for(ny, 1), nbz = bricks_for(nz, 2);
-    const size_t total = (size_t)nbx * nby * nbz * kBrickElems;
+    const uint32_t nbx = bricks_for(nx, 0, ST_F32), nby = bricks_for(ny, 1, ST_F32),
+                   nbz = bricks_for(nz, 2, ST_F32);
+    const size_t total = (size_t)nbx * nby * nbz;  // bricks
     hipLaunchKernelGGL(grad_field_kernel, dim3(grid_bricks(total)), dim3(256), 0, s, bricks, grad,
                        nx, ny, nz, nbx, nby, total);
     return hipGetLastError();
