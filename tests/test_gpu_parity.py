@@ -460,6 +460,42 @@ def test_kernel_variants_bit_identical(rp, monkeypatch, shading):
     check(imgs[0], ref)
 
 
+@pytest.mark.parametrize("np_dtype", [np.float32, np.uint8, np.int16])
+def test_lds_staged_kernel_bit_identical(rp, monkeypatch, np_dtype):
+    """The opt-in LDS-staged march (VR_LDS=1 at upload and render: per-stage voxel boxes
+    DMA'd into LDS from a zero-padded linear copy) renders the bricked gather's bytes, shaded
+    and unshaded; without VR_LDS no linear copy is kept."""
+    W, H = 88, 70
+    rp.framebuffer_size_changed(W, H)
+    vol = synth.gaussians_numpy((37, 30, 43), seed=23)
+    if np_dtype != np.float32:
+        info = np.iinfo(np_dtype)
+        vol = np.clip(np.rint(vol / vol.max() * info.max), info.min, info.max).astype(np_dtype)
+    else:
+        vol = vol.astype(np.float32)
+    tf = synth.tf_band(0.1, 0.9)
+    base_bytes = None
+    for lds in ("0", "1"):
+        monkeypatch.setenv("VR_LDS", lds)
+        rp.volume_dataset_changed(synth.dataset(vol))
+        rp.transfer_function_changed(tf)
+        imgs = []
+        for shading in (0, 1):
+            for camname in ("rotA", "fill_oblique"):
+                cam = synth.camera(camname).to_vr_camera()
+                imgs.append(rp.render(cam, vr_amd.default_params(shading=shading, ert_eps=1e-4),
+                                      vr_amd.OUT_RGBA32F))
+        if base_bytes is None:
+            base_bytes = imgs
+            assert "lds" not in rp.kernel_name(vr_amd.default_params()), "no linear copy without VR_LDS"
+        else:
+            assert "lds" in rp.kernel_name(vr_amd.default_params())
+            for a, b in zip(base_bytes, imgs):
+                assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), np_dtype
+    monkeypatch.delenv("VR_LDS")
+    rp.volume_dataset_changed(synth.dataset(vol))  # later tests: no linear copy
+
+
 def test_frames_in_flight_on_streams_are_identical(rp):
     """Frames rendered back to back on 3 streams (frames_in_flight = 3, own output buffer per
     stream, adaptive tile order per stream) equal the serial frame byte for byte.  Right

@@ -318,6 +318,15 @@ int set_bricks(vr_ctx *c, int storage, uint32_t nx, uint32_t ny, uint32_t nz, vo
 int set_lin(vr_ctx *c, int storage, int src_dtype, const void *src, uint32_t nx, uint32_t ny,
             uint32_t nz, hipStream_t s)
 {
+    // only for the opt-in LDS-staged kernel (VR_LDS=1 at upload): it measured slower than the
+    // bricked gather (profiles/r02/lds_staging), and the copy costs memory and an upload pass
+    const char *want = std::getenv("VR_LDS");
+    if (!want || want[0] != '1') {
+        if (c->lin) hipFree(c->lin);
+        c->lin = nullptr;
+        c->lin_bytes = 0;
+        return VR_OK;
+    }
     const size_t bytes = lin_elems(nx, ny, nz) * storage_size(storage);
     if (!c->lin || c->lin_bytes != bytes) {
         if (c->lin) hipFree(c->lin);
