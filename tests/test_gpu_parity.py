@@ -126,6 +126,54 @@ def test_native_dtypes(rp, np_dtype):
     check(img, ref)
 
 
+@pytest.mark.parametrize("np_dtype", [np.uint8, np.int8])
+def test_byte_layouts_plain_and_quad_identical(rp, monkeypatch, np_dtype):
+    """8-bit volumes are bricked as yz-quads up to kQuadMaxVoxels voxels and as plain 7x8x8-cell
+    bricks above (vr_internal.h); both layouts, forced through VR_U8_LAYOUT at upload, read
+    back the volume exactly and render the same bytes -- single lane, pipelined, lane pairs,
+    shaded (stencil gradient across brick boundaries and the border), skip-empty -- and match
+    the oracle."""
+    base = synth.gaussians_numpy((45, 31, 38), seed=29)
+    info = np.iinfo(np_dtype)
+    vol = np.clip(np.rint(info.min + base / base.max() * (int(info.max) - int(info.min))),
+                  info.min, info.max).astype(np_dtype)
+    W, H = 72, 56
+    rp.framebuffer_size_changed(W, H)
+    tf = synth.tf_band(0.2, 0.95)
+    combos = [dict(shading=0, skip_empty=0), dict(shading=1, skip_empty=0),
+              dict(shading=0, skip_empty=1), dict(shading=1, skip_empty=1)]
+    envs = [dict(VR_PIPELINE="0", VR_PAIR="0"), dict(VR_PIPELINE="1", VR_PAIR="0"),
+            dict(VR_PAIR="1", VR_PAIR_LANES="2")]
+    out = {}
+    for layout in ("quad", "plain"):
+        monkeypatch.setenv("VR_U8_LAYOUT", layout)
+        rp.volume_dataset_changed(synth.dataset(vol))
+        monkeypatch.delenv("VR_U8_LAYOUT")
+        assert ("Quad8" in rp.kernel_name(vr_amd.default_params())) == (layout == "quad")
+        rp.transfer_function_changed(tf)
+        assert np.array_equal(rp.read_volume(), vol.astype(np.float32)), layout
+        for camname in ("rotA", "fill_oblique"):
+            cam = synth.camera(camname).to_vr_camera()
+            for c in combos:
+                for env in envs if not c["skip_empty"] else envs[:1]:
+                    for k, v in env.items():
+                        monkeypatch.setenv(k, v)
+                    img = rp.render(cam, vr_amd.default_params(ert_eps=1e-4, **c), vr_amd.OUT_RGBA32F)
+                    for k in env:
+                        monkeypatch.delenv(k)
+                    key = (camname, tuple(c.items()), tuple(env.items()))
+                    out.setdefault(key, []).append(img)
+    for key, (a, b) in out.items():
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), key
+    cam = synth.camera("rotA").to_vr_camera()
+    ds = synth.dataset(vol)
+    for shading in (0, 1):
+        p = vr_amd.default_params(shading=shading, ert_eps=1e-4)
+        ref, _ = oracle_render(vol.astype(np.float32), ds.vmin, ds.vmax, tf, cam, W, H, p)
+        check(out[("rotA", (("shading", shading), ("skip_empty", 0)),
+                   (("VR_PIPELINE", "0"), ("VR_PAIR", "0")))][1], ref)
+
+
 def test_row_block_sharding_assembles_exactly(rp):
     """Image-space sharding (multi-GPU path) on one device: every rank's shard rendered
     separately, gathered rank-major, assembled == the single-rank frame, bit for bit."""

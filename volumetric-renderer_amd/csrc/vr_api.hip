@@ -32,6 +32,7 @@ struct vr_ctx {
     void *lin = nullptr;
     size_t lin_bytes = 0;
     int storage = ST_F32;
+    int layout = ST_F32;  // brick layout code (storage | kQuadFlag for 8-bit yz-quads)
     uint32_t nx = 1, ny = 1, nz = 1;
     float vmin = 0.0f, vmax = 1.0f;
     // transfer function (decoded, linear float RGBA)
@@ -290,6 +291,18 @@ struct SplitMix {
     float uniform() { return (float)(next() >> 40) * (1.0f / 16777216.0f); }
 };
 
+// Brick layout of an nx x ny x nz volume of storage type st (vr_internal.h kQuadFlag): 8-bit
+// volumes of at most kQuadMaxVoxels voxels in yz-quads, larger ones in plain bricks.
+// VR_U8_LAYOUT=quad|plain overrides (A/B, tests).
+int brick_layout(int st, uint32_t nx, uint32_t ny, uint32_t nz)
+{
+    if (!VR_U8_PLAIN || (st != ST_U8 && st != ST_I8)) return st;
+    bool quad = (size_t)nx * ny * nz <= kQuadMaxVoxels;
+    if (const char *e = std::getenv("VR_U8_LAYOUT")) quad = e[0] == 'q';
+    return quad ? (st | kQuadFlag) : st;
+}
+
+// (Re)allocate the bricked volume for layout code `storage`.
 int set_bricks(vr_ctx *c, int storage, uint32_t nx, uint32_t ny, uint32_t nz, void **out)
 {
     c->range_valid = c->dist_valid = false;  // the bricks are about to be rewritten
@@ -461,8 +474,8 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.nx = c->nx;
     P.ny = c->ny;
     P.nz = c->nz;
-    P.nbx = bricks_for(c->nx, 0, c->storage);
-    P.nby = bricks_for(c->ny, 1, c->storage);
+    P.nbx = bricks_for(c->nx, 0, c->layout);
+    P.nby = bricks_for(c->ny, 1, c->layout);
     P.fnx = (float)c->nx;
     P.fny = (float)c->ny;
     P.fnz = (float)c->nz;
@@ -519,7 +532,7 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
 // the march that reads them.
 int ensure_skip(vr_ctx *c, MarchParams &P, hipStream_t s)
 {
-    const size_t nb = (size_t)bricks_for(c->nx, 0, c->storage) * bricks_for(c->ny, 1, c->storage) * bricks_for(c->nz, 2, c->storage);
+    const size_t nb = (size_t)bricks_for(c->nx, 0, c->layout) * bricks_for(c->ny, 1, c->layout) * bricks_for(c->nz, 2, c->layout);
     if (nb > 0xFFFFFFFFull) return fail(c, VR_EINVAL, "skip_empty: too many bricks");
     if (c->nbricks_alloc != nb) {
         if (c->brick_range) hipFree(c->brick_range);
@@ -533,15 +546,15 @@ int ensure_skip(vr_ctx *c, MarchParams &P, hipStream_t s)
         c->nbricks_alloc = nb;
     }
     if (!c->range_valid) {
-        HIP_TRY(c, launch_brick_range(c->storage, c->bricks, bricks_for(c->nx, 0, c->storage), bricks_for(c->ny, 1, c->storage),
-                                      bricks_for(c->nz, 2, c->storage), c->brick_range, s),
+        HIP_TRY(c, launch_brick_range(c->layout, c->bricks, bricks_for(c->nx, 0, c->layout), bricks_for(c->ny, 1, c->layout),
+                                      bricks_for(c->nz, 2, c->layout), c->brick_range, s),
                 "brick range kernel");
         c->range_valid = true;
         c->dist_valid = false;
     }
     if (!c->dist_valid) {
-        HIP_TRY(c, launch_skip_dist(c->brick_range, bricks_for(c->nx, 0, c->storage), bricks_for(c->ny, 1, c->storage),
-                                    bricks_for(c->nz, 2, c->storage), c->tf_nz, (int)c->tf_n, c->vmin,
+        HIP_TRY(c, launch_skip_dist(c->brick_range, bricks_for(c->nx, 0, c->layout), bricks_for(c->ny, 1, c->layout),
+                                    bricks_for(c->nz, 2, c->layout), c->tf_nz, (int)c->tf_n, c->vmin,
                                     c->vmax - c->vmin, c->skip_dist, c->skip_dist + nb, s),
                 "skip distance kernels");
         c->dist_valid = true;
@@ -827,14 +840,16 @@ int vr_set_volume_device(vr_ctx *c, const void *data_dev, int dtype, uint32_t nx
     int rc = wait_idle(c);
     if (rc) return rc;
     void *dst = nullptr;
-    rc = set_bricks(c, st, nx, ny, nz, &dst);
+    const int lay = brick_layout(st, nx, ny, nz);
+    rc = set_bricks(c, lay, nx, ny, nz, &dst);
     if (rc) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    HIP_TRY(c, launch_brick_from_linear(dtype, data_dev, dst, nx, ny, nz, st, s), "brick kernel");
+    HIP_TRY(c, launch_brick_from_linear(dtype, data_dev, dst, nx, ny, nz, lay, s), "brick kernel");
     rc = set_lin(c, st, dtype, data_dev, nx, ny, nz, s);
     if (rc) return rc;
     HIP_TRY(c, hipStreamSynchronize(s), "brick kernel sync");
     c->storage = st;
+    c->layout = lay;
     c->nx = nx;
     c->ny = ny;
     c->nz = nz;
@@ -927,9 +942,10 @@ int vr_generate_volume(vr_ctx *c, int kind, int dtype, uint32_t nx, uint32_t ny,
     }
     const int src_dtype = st == ST_U8 ? VR_DTYPE_U8 : (st == ST_U16 ? VR_DTYPE_U16 : VR_DTYPE_F32);
     void *dst = nullptr;
-    int rc = set_bricks(c, st, nx, ny, nz, &dst);
+    const int lay = brick_layout(st, nx, ny, nz);
+    int rc = set_bricks(c, lay, nx, ny, nz, &dst);
     if (rc == VR_OK) {
-        e = launch_brick_from_linear(src_dtype, lin, dst, nx, ny, nz, st, nullptr);
+        e = launch_brick_from_linear(src_dtype, lin, dst, nx, ny, nz, lay, nullptr);
         if (e != hipSuccess) rc = hip_fail(c, e, "brick generated volume");
         if (rc == VR_OK) rc = set_lin(c, st, src_dtype, lin, nx, ny, nz, nullptr);
         if (rc == VR_OK && (e = hipDeviceSynchronize()) != hipSuccess)
@@ -944,6 +960,7 @@ int vr_generate_volume(vr_ctx *c, int kind, int dtype, uint32_t nx, uint32_t ny,
         return f;
     };
     c->storage = st;
+    c->layout = lay;
     c->nx = nx;
     c->ny = ny;
     c->nz = nz;
@@ -969,7 +986,7 @@ int vr_debug_read_volume_native(vr_ctx *c, void *out)
     int rc = VR_OK;
     for (uint32_t z0 = 0; z0 < c->nz && rc == VR_OK; z0 += cz) {
         const uint32_t n = std::min(cz, c->nz - z0);
-        hipError_t e = launch_unbrick(c->storage, c->bricks, tmp, c->nx, c->ny, z0, n, nullptr);
+        hipError_t e = launch_unbrick(c->layout, c->bricks, tmp, c->nx, c->ny, z0, n, nullptr);
         if (e == hipSuccess)
             e = hipMemcpy(static_cast<char *>(out) + slice * z0, tmp, slice * n, hipMemcpyDeviceToHost);
         if (e != hipSuccess) rc = hip_fail(c, e, "read volume");
@@ -1069,7 +1086,7 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
         if (!e0 || !e1) return fail(c, VR_EIO, "hipEventCreate failed");
         HIP_TRY(c, hipEventRecord(e0, s), "hipEventRecord");
     }
-    HIP_TRY(c, launch_march(c->storage, p->shading != 0, false, P, s), "march kernel launch");
+    HIP_TRY(c, launch_march(c->layout, p->shading != 0, false, P, s), "march kernel launch");
     if (c->timing) {
         HIP_TRY(c, hipEventRecord(e1, s), "hipEventRecord");
         c->ev_pending.emplace_back(e0, e1);
@@ -1183,7 +1200,7 @@ int vr_count_work(vr_ctx *c, const vr_camera *cam, const vr_params *p, uint32_t 
     rc = ensure_derived(c, p, P, nullptr);
     if (rc) return rc;
     HIP_TRY(c, hipMemset(c->counters, 0, 8 * sizeof(unsigned long long)), "hipMemset(counters)");
-    HIP_TRY(c, launch_march(c->storage, p->shading != 0, true, P, nullptr), "march (count) launch");
+    HIP_TRY(c, launch_march(c->layout, p->shading != 0, true, P, nullptr), "march (count) launch");
     unsigned long long h[5];
     HIP_TRY(c, hipMemcpy(h, c->counters, sizeof(h), hipMemcpyDeviceToHost), "hipMemcpy(counters)");
     out->rays = h[0];
@@ -1241,7 +1258,7 @@ const char *vr_kernel_name(const vr_ctx *c, const vr_params *p)
     const bool pipe = use_pipeline(p && p->shading, tiles, c) &&
                       !(p && p->skip_empty) && c->tf_n <= 256;
     if (p && use_lds(c, p)) return march_lds_kernel_name(c->storage, p->shading != 0);
-    return march_kernel_name(c->storage, p && p->shading != 0, false, p && p->skip_empty != 0, gf,
+    return march_kernel_name(c->layout, p && p->shading != 0, false, p && p->skip_empty != 0, gf,
                              pipe);
 }
 

@@ -127,11 +127,23 @@ __host__ __device__ __forceinline__ void brick_coords(uint32_t slot, uint32_t nb
 }
 
 enum StorageType { ST_U8 = 0, ST_I8 = 1, ST_U16 = 2, ST_I16 = 3, ST_F32 = 4 };
+// Brick layout code = storage type | kQuadFlag: 8-bit voxels kept in yz-quad elements (GeomWide
+// bricks, one 8-B load per sample) instead of plain 7x8x8-cell bricks.  Volumes of at most
+// kQuadMaxVoxels voxels use it (the quads, 5.7x the voxels, stay cache-resident: C2 256^3
+// 459 against 420 Gsamples/s plain); larger ones the plain bricks (C4 HBM 5.70 -> 1.89 GB per
+// frame).  The layout code is what the brick helpers below and the march launchers take.
+constexpr int kQuadFlag = 0x10;
+constexpr size_t kQuadMaxVoxels = 1ull << 25;
+// kernel-side tag type of 8-bit voxels T in yz-quad elements
+template <typename T>
+struct Quad8 {
+    T v;
+};
 
-// Bytes of one voxel / of one element of storage type st.
+// Bytes of one voxel of storage type (or layout code) st.
 inline size_t storage_size(int st)
 {
-    switch (st) {
+    switch (st & 0xF) {
         case ST_U8:
         case ST_I8: return 1;
         case ST_U16:
@@ -139,13 +151,17 @@ inline size_t storage_size(int st)
         default: return 4;
     }
 }
-inline bool byte_storage(int st) { return st == ST_U8 || st == ST_I8; }
+// layout code st holds plain 8-bit voxels (one per element, GeomByte bricks)
+inline bool byte_storage(int st)
+{
+    return VR_U8_PLAIN && !(st & kQuadFlag) && (st == ST_U8 || st == ST_I8);
+}
 inline size_t voxels_per_element(int st)
 {
-    return st == ST_F32 ? kF32VoxelsPerElement : (byte_storage(st) && VR_U8_PLAIN ? 1 : 4);
+    return st == ST_F32 ? kF32VoxelsPerElement : (byte_storage(st) ? 1 : 4);
 }
 inline size_t element_size(int st) { return storage_size(st) * voxels_per_element(st); }
-// Brick geometry of storage type st: cells along axis a (0 x, 1 y, 2 z), elements per brick.
+// Brick geometry of layout code st: cells along axis a (0 x, 1 y, 2 z), elements per brick.
 inline int brick_cells(int st, int a)
 {
     return byte_storage(st) ? GeomByte::cells(a) : GeomWide::cells(a);

@@ -60,14 +60,28 @@ typedef uint32_t u4a __attribute__((ext_vector_type(4))) __attribute__((aligned(
 template <typename VT>
 constexpr bool kZPair = std::is_same<VT, float>::value;
 // bytes per element; 32-bit words per element (quad layouts)
+// VT is the voxel type, or Quad8<T> for 8-bit voxels in yz-quads (vr_internal.h kQuadFlag);
+// Vox<VT> the voxel type either way
+template <typename VT>
+struct VoxOf {
+    using type = VT;
+};
+template <typename T>
+struct VoxOf<Quad8<T>> {
+    using type = T;
+};
+template <typename VT>
+using Vox = typename VoxOf<VT>::type;
+template <typename VT>
+constexpr bool kIsQuad8 = !std::is_same<VT, Vox<VT>>::value;
 // 8-bit volumes stored one voxel per element (VR_U8_PLAIN, vr_internal.h)
 template <typename VT>
-constexpr bool kPlainByte = sizeof(VT) == 1 && VR_U8_PLAIN;
+constexpr bool kPlainByte = sizeof(VT) == 1 && VR_U8_PLAIN && !kIsQuad8<VT>;
 template <typename VT>
 constexpr int kElemBytes = kZPair<VT> ? 4 * (int)kF32VoxelsPerElement
                                       : (kPlainByte<VT> ? 1 : 4 * (int)sizeof(VT));
 template <typename VT>
-using GeomOf = std::conditional_t<sizeof(VT) == 1, GeomByte, GeomWide>;
+using GeomOf = std::conditional_t<kPlainByte<VT>, GeomByte, GeomWide>;
 template <typename VT>
 constexpr int kQuadWords = sizeof(VT) == 1 ? 1 : 2;
 
@@ -118,7 +132,7 @@ template <typename VT>
 __device__ __forceinline__ float byte_value(uint32_t w, int b)
 {
     const uint32_t u = (w >> (8 * b)) & 0xFFu;
-    if constexpr (std::is_signed<VT>::value) return (float)(int)(int8_t)u;
+    if constexpr (std::is_signed<Vox<VT>>::value) return (float)(int)(int8_t)u;
     return (float)u;
 }
 
@@ -129,11 +143,11 @@ __device__ __forceinline__ float qc(const uint32_t *w, int c)
 {
     if constexpr (sizeof(VT) == 1) {
         const uint32_t b = (w[0] >> (8 * c)) & 0xFFu;
-        if constexpr (std::is_signed<VT>::value) return (float)(int)(int8_t)b;
+        if constexpr (std::is_signed<Vox<VT>>::value) return (float)(int)(int8_t)b;
         return (float)b;
     } else {
         const uint32_t h = (w[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
-        if constexpr (std::is_signed<VT>::value) return (float)(int)(int16_t)h;
+        if constexpr (std::is_signed<Vox<VT>>::value) return (float)(int)(int16_t)h;
         return (float)h;
     }
 }
@@ -1566,12 +1580,13 @@ __global__ __launch_bounds__(256) void order_tiles_kernel(const uint32_t *__rest
 // 4 yz-quad), 0 outside the logical volume (border).
 template <typename SrcT, typename DstT>
 __global__ __launch_bounds__(256) void brick_kernel(const SrcT *__restrict__ src,
-                                                    DstT *__restrict__ dst, uint32_t nx,
+                                                    Vox<DstT> *__restrict__ dst, uint32_t nx,
                                                     uint32_t ny, uint32_t nz, uint32_t nbx,
                                                     uint32_t nby, size_t nbricks)
 {
     constexpr bool zpair = std::is_same<DstT, float>::value;
     using G = GeomOf<DstT>;
+    using V = Vox<DstT>;
     // a workgroup per brick (grid-stride over bricks), its threads over the brick's elements:
     // brick coordinates once per brick, element coordinates by constant divisors, and each
     // brick's elements written contiguously
@@ -1584,10 +1599,10 @@ __global__ __launch_bounds__(256) void brick_kernel(const SrcT *__restrict__ src
         const long x = (long)bx * G::BX + lx - kPad;
         const long y = (long)by * G::BY + lyy - kPad;
         const long z = (long)bz * G::BZ + lz - kPad;
-        auto at = [&](long xx, long yy, long zz) -> DstT {
+        auto at = [&](long xx, long yy, long zz) -> V {
             if (xx < 0 || yy < 0 || zz < 0 || xx >= (long)nx || yy >= (long)ny || zz >= (long)nz)
-                return (DstT)0;
-            return (DstT)src[(size_t)xx + (size_t)nx * ((size_t)yy + (size_t)ny * (size_t)zz)];
+                return (V)0;
+            return (V)src[(size_t)xx + (size_t)nx * ((size_t)yy + (size_t)ny * (size_t)zz)];
         };
         // one store per element (a u8 quad is one dword, not four byte stores)
         if constexpr ((zpair && VR_F32_PLAIN) || kPlainByte<DstT>) {
@@ -1595,8 +1610,8 @@ __global__ __launch_bounds__(256) void brick_kernel(const SrcT *__restrict__ src
         } else if constexpr (zpair) {
             reinterpret_cast<float2 *>(dst)[g] = make_float2(at(x, y, z), at(x, y, z + 1));
         } else {
-            struct alignas(4 * sizeof(DstT)) Quad {
-                DstT v[4];
+            struct alignas(4 * sizeof(V)) Quad {
+                V v[4];
             };
             Quad q;
             q.v[0] = at(x, y, z);
@@ -1923,8 +1938,8 @@ template <typename VT>
 hipError_t launch_march_vt(bool shade, bool count, const MarchParams &p, hipStream_t s)
 {
     if (p.lds && !count) {  // host: no skip-empty, tf_n <= kTfLds, lin present
-        if (shade) return launch_lds_t<VT, true>(p, s);
-        return launch_lds_t<VT, false>(p, s);
+        if (shade) return launch_lds_t<Vox<VT>, true>(p, s);
+        return launch_lds_t<Vox<VT>, false>(p, s);
     }
     if (p.pair) {  // host: not counting, no skip-empty, tf_n <= kTfLds, 16x8 tiles
         if (!shade) return launch_pair_t<VT, false, false>(p, s);
@@ -1976,8 +1991,8 @@ inline unsigned grid_for(size_t total)
 // Readback (vr_debug_read_volume*): voxel v(x, y, z) is component 0 of element (x, y, z) of the
 // bricked layout; slices [z0, z0 + cz) into a linear x-fastest buffer of the storage type.
 template <typename T>
-__global__ __launch_bounds__(256) void unbrick_kernel(const T *__restrict__ bricks,
-                                                     T *__restrict__ dst, uint32_t nx,
+__global__ __launch_bounds__(256) void unbrick_kernel(const Vox<T> *__restrict__ bricks,
+                                                     Vox<T> *__restrict__ dst, uint32_t nx,
                                                      uint32_t ny, uint32_t nbx, uint32_t nby,
                                                      uint32_t z0, size_t count)
 {
@@ -2004,6 +2019,8 @@ hipError_t brick_from(const void *src, void *dst, uint32_t nx, uint32_t ny, uint
     switch (storage) {
         case ST_U8: hipLaunchKernelGGL((brick_kernel<SrcT, uint8_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (uint8_t *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_I8: hipLaunchKernelGGL((brick_kernel<SrcT, int8_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (int8_t *)dst, nx, ny, nz, nbx, nby, total); break;
+        case ST_U8 | kQuadFlag: hipLaunchKernelGGL((brick_kernel<SrcT, Quad8<uint8_t>>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (uint8_t *)dst, nx, ny, nz, nbx, nby, total); break;
+        case ST_I8 | kQuadFlag: hipLaunchKernelGGL((brick_kernel<SrcT, Quad8<int8_t>>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (int8_t *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_U16: hipLaunchKernelGGL((brick_kernel<SrcT, uint16_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (uint16_t *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_I16: hipLaunchKernelGGL((brick_kernel<SrcT, int16_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (int16_t *)dst, nx, ny, nz, nbx, nby, total); break;
         default: hipLaunchKernelGGL((brick_kernel<SrcT, float>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
@@ -2019,6 +2036,8 @@ hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &
     switch (storage) {
         case ST_U8: return launch_march_vt<uint8_t>(shade, count, p, stream);
         case ST_I8: return launch_march_vt<int8_t>(shade, count, p, stream);
+        case ST_U8 | kQuadFlag: return launch_march_vt<Quad8<uint8_t>>(shade, count, p, stream);
+        case ST_I8 | kQuadFlag: return launch_march_vt<Quad8<int8_t>>(shade, count, p, stream);
         case ST_U16: return launch_march_vt<uint16_t>(shade, count, p, stream);
         case ST_I16: return launch_march_vt<int16_t>(shade, count, p, stream);
         case ST_F32: return launch_march_vt<float>(shade, count, p, stream);
@@ -2028,11 +2047,13 @@ hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &
 
 const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bool gf, bool pipe)
 {
-    // demangled names as rocprofv3 reports them (kernel-trace "Kernel_Name")
+    // demangled names as rocprofv3 reports them (kernel-trace "Kernel_Name"); storage is the
+    // layout code (8-bit yz-quads: the Quad8 instantiations)
     static const std::vector<std::string> names = [] {
-        const char *types[5] = {"unsigned char", "signed char", "unsigned short", "short", "float"};
+        const char *types[7] = {"unsigned char", "signed char", "unsigned short", "short", "float",
+                                "vr::Quad8<unsigned char>", "vr::Quad8<signed char>"};
         std::vector<std::string> v;
-        for (int t = 0; t < 5; ++t)
+        for (int t = 0; t < 7; ++t)
             for (int k = 0; k < 32; ++k) {
                 std::string n = std::string("void vr::(anonymous namespace)::march_kernel<") + types[t];
                 for (int bit = 4; bit >= 0; --bit) n += (k >> bit) & 1 ? ", true" : ", false";
@@ -2040,7 +2061,8 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
             }
         return v;
     }();
-    if (storage < 0 || storage > 4) return "march_kernel<?>";
+    if (storage & kQuadFlag) storage = 5 + (storage & 0xF);
+    if (storage < 0 || storage > 6) return "march_kernel<?>";
     const int k = (shade ? 16 : 0) + (count ? 8 : 0) + (skip ? 4 : 0) + (gf ? 2 : 0) + (pipe ? 1 : 0);
     return names[storage * 32 + k].c_str();
 }
@@ -2056,6 +2078,7 @@ const char *march_lds_kernel_name(int storage, bool shade)
                             (sh ? ", true" : ", false") + ">(vr::MarchParams)");
         return v;
     }();
+    storage &= 0xF;  // the voxel type: the LDS kernel reads the linear copy
     if (storage < 0 || storage > 4) return "march_lds_kernel<?>";
     return names[storage * 2 + (shade ? 1 : 0)].c_str();
 }
@@ -2068,6 +2091,7 @@ hipError_t launch_unbrick(int storage, const void *bricks, void *dst, uint32_t n
     const uint32_t bx = bricks_for(nx, 0, storage), by = bricks_for(ny, 1, storage);
     switch (storage) {
         case ST_U8: case ST_I8: hipLaunchKernelGGL((unbrick_kernel<uint8_t>), dim3(g), dim3(256), 0, s, (const uint8_t *)bricks, (uint8_t *)dst, nx, ny, bx, by, z0, n); break;
+        case ST_U8 | kQuadFlag: case ST_I8 | kQuadFlag: hipLaunchKernelGGL((unbrick_kernel<Quad8<uint8_t>>), dim3(g), dim3(256), 0, s, (const uint8_t *)bricks, (uint8_t *)dst, nx, ny, bx, by, z0, n); break;
         case ST_U16: case ST_I16: hipLaunchKernelGGL((unbrick_kernel<uint16_t>), dim3(g), dim3(256), 0, s, (const uint16_t *)bricks, (uint16_t *)dst, nx, ny, bx, by, z0, n); break;
         default: hipLaunchKernelGGL((unbrick_kernel<float>), dim3(g), dim3(256), 0, s, (const float *)bricks, (float *)dst, nx, ny, bx, by, z0, n); break;
     }
@@ -2178,7 +2202,7 @@ hipError_t launch_brick_range(int storage, const void *bricks, uint32_t nbx, uin
     const uint32_t nbricks = nbx * nby * nbz;
     const unsigned g = (nbricks + 3) / 4;
     const uint32_t per = (uint32_t)(brick_elems(storage) * voxels_per_element(storage));
-    switch (storage) {
+    switch (storage & 0xF) {  // the voxels of every element, whatever the layout
         case ST_U8: hipLaunchKernelGGL((brick_range_kernel<uint8_t>), dim3(g), dim3(256), 0, s, (const uint8_t *)bricks, nbricks, per, nbx, nby, range_dev); break;
         case ST_I8: hipLaunchKernelGGL((brick_range_kernel<int8_t>), dim3(g), dim3(256), 0, s, (const int8_t *)bricks, nbricks, per, nbx, nby, range_dev); break;
         case ST_U16: hipLaunchKernelGGL((brick_range_kernel<uint16_t>), dim3(g), dim3(256), 0, s, (const uint16_t *)bricks, nbricks, per, nbx, nby, range_dev); break;
