@@ -23,6 +23,7 @@
 //    volumes >= 4 GiB; lane-group variant for small shaded launches with serial frames;
 //  * fp contraction is OFF (pragma below + -ffp-contract=off): every fused multiply-add is
 //    an explicit fmaf(), matching the CPU oracle's operation order bit for bit.
+#include "vr_exact_math.h"
 #include "vr_internal.h"
 
 #include <string>
@@ -691,15 +692,24 @@ __device__ __forceinline__ void phong(const MarchParams &P, float gx, float gy_,
     const float wx = gx * P.fnx, wy = gy_ * P.fny, wz = gz * P.fnz;
     const float g2 = wx * wx + wy * wy + wz * wz;
     if (g2 > 0.0f) {
-        const float inv = 1.0f / sqrtf(g2);
+        const float inv = inv_sqrt_ieee(g2);  // 1.0f / sqrtf(g2), vr_exact_math.h
         const float ndl = fabsf((wx * d0 + wy * d1 + wz * d2) * inv);
         const float kdiff = P.ka + P.kd * ndl;
-        // ndl^p by binary exponentiation (the oracle's powi): p uniform
+        // ndl^p by binary exponentiation (the oracle's powi): p uniform.  The default p = 16
+        // unrolled: powi squares four times and multiplies 1 by the result (exact), so
+        // ((ndl^2)^2)^2)^2 is its value bit for bit, without the loop's scalar branches.
         float sp = 1.0f, b = ndl;
-        for (int e = P.spec_power; e;) {
-            if (e & 1) sp = sp * b;
-            e >>= 1;
-            if (e) b = b * b;
+        if (P.spec_power == 16) {
+            b = b * b;
+            b = b * b;
+            b = b * b;
+            sp = b * b;
+        } else {
+            for (int e = P.spec_power; e;) {
+                if (e & 1) sp = sp * b;
+                e >>= 1;
+                if (e) b = b * b;
+            }
         }
         const float spec = P.ks * sp;
         s.x = s.x * kdiff + spec;
