@@ -431,12 +431,39 @@ __device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e
     grad_filter<PACKED>(Dx, Dy, Dz, ax, ay, az, gx, gy, gz);
 }
 
+#ifndef VR_GRAD_ZPACK
+#define VR_GRAD_ZPACK 1  // A/B: 0 = (Dx, Dy)-packed tri8x2 + scalar Dz
+#endif
 // Gradient from the precomputed f32 field: the cell's 8 corners of {Dx, Dy, Dz}, rows y and
 // y + 1 of elements x, x + 1 (48 B each: 3 x 16-B loads), filtered as grad_filter.
 template <bool PACKED>
 __device__ __forceinline__ void grad_field(const char *__restrict__ gbase, size_t e, float ax,
                                            float ay, float az, float &gx, float &gy, float &gz)
 {
+#if VR_GRAD_ZPACK
+    if constexpr (PACKED) {
+        // Each axis filtered with its z = 0 / z = 1 halves as packed pairs, which the field's
+        // element layout already holds adjacent ({D(z), D(z+1)}): lerp2 over x of rows y and
+        // y + 1 gives {c00, c01} and {c10, c11}, lerp2 over y {c0, c1}, then the z lerp --
+        // tri8's IEEE operations per element, without repacking (Dx, Dy) pairs.
+        const char *row0 = gbase + e * kGradElemBytes;
+        const char *row1 = row0 + (size_t)GeomWide::Row * kGradElemBytes;
+        const f4a a0 = *reinterpret_cast<const f4a *>(row0);       // Dx(x) z,z+1  Dy(x) z,z+1
+        const f4a a1 = *reinterpret_cast<const f4a *>(row0 + 16);  // Dz(x) z,z+1  Dx(x+1) z,z+1
+        const f4a a2 = *reinterpret_cast<const f4a *>(row0 + 32);  // Dy(x+1) ...  Dz(x+1) ...
+        const f4a b0 = *reinterpret_cast<const f4a *>(row1);
+        const f4a b1 = *reinterpret_cast<const f4a *>(row1 + 16);
+        const f4a b2 = *reinterpret_cast<const f4a *>(row1 + 32);
+        auto axis = [&](f2v y0x0, f2v y0x1, f2v y1x0, f2v y1x1) {
+            const f2v q = lerp2(lerp2(y0x0, y0x1, ax), lerp2(y1x0, y1x1, ax), ay);
+            return lerpf(q.x, q.y, az);
+        };
+        gx = axis(f2v{a0.x, a0.y}, f2v{a1.z, a1.w}, f2v{b0.x, b0.y}, f2v{b1.z, b1.w});
+        gy = axis(f2v{a0.z, a0.w}, f2v{a2.x, a2.y}, f2v{b0.z, b0.w}, f2v{b2.x, b2.y});
+        gz = axis(f2v{a1.x, a1.y}, f2v{a2.z, a2.w}, f2v{b1.x, b1.y}, f2v{b2.z, b2.w});
+        return;
+    }
+#endif
     float Dx[8], Dy[8], Dz[8];
 #pragma unroll
     for (int dy_ = 0; dy_ < 2; ++dy_) {
