@@ -660,12 +660,21 @@ __device__ unsigned int g_wg_count;
 #ifndef VR_SKIP_MIN_WAVES
 #define VR_SKIP_MIN_WAVES 1
 #endif
+#ifndef VR_PIPE_DEPTH
+#define VR_PIPE_DEPTH 2  // samples of a ray in flight in the PIPE kernels (2 or 3)
+#endif
 #ifndef VR_PIPE_MIN_WAVES
 #define VR_PIPE_MIN_WAVES 1
 #endif
+// The pipelined shaded kernel with the difference field (the C3 headline kernel): 6 waves
+// (78 VGPRs, no spills) against 5 unconstrained (84): C3 +1.1% (309 -> 313 Gsamples/s, three
+// alternating rounds), side view -4.5% (profiles/r02/pipeline/min_waves6_*).
+#ifndef VR_PIPE_GF_MIN_WAVES
+#define VR_PIPE_GF_MIN_WAVES 6
+#endif
 template <bool COUNT, bool SKIP, bool GF, bool PIPE>
 constexpr int kMarchMinWaves =
-    PIPE ? VR_PIPE_MIN_WAVES
+    PIPE ? (GF ? VR_PIPE_GF_MIN_WAVES : VR_PIPE_MIN_WAVES)
          : (GF ? 1 : (COUNT ? 4 : (SKIP ? VR_SKIP_MIN_WAVES : VR_MARCH_MIN_WAVES)));
 
 #ifndef VR_SKIP_PACKED_GRADIENT
@@ -880,6 +889,27 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
             p1 = p1 + d1 * P.step;
             p2 = p2 + d2 * P.step;
         };
+#if VR_PIPE_DEPTH == 3
+        // three stages in rotation: the loads of samples k+1 and k+2 in flight while sample k
+        // is consumed (a stage is consumed only if every earlier one was in bounds and the ray
+        // has not terminated, as in the two-stage form)
+        Stage A, B, C;
+        int k = 0;
+        prep(A, k);
+        advance();
+        prep(B, ++k);
+        while (A.ok) {
+            advance();
+            prep(C, ++k);
+            if (consume(A) || !B.ok) break;
+            advance();
+            prep(A, ++k);
+            if (consume(B) || !C.ok) break;
+            advance();
+            prep(B, ++k);
+            if (consume(C)) break;
+        }
+#else
         Stage A, B;
         int k = 0;
         prep(A, k);
@@ -891,6 +921,7 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
             prep(A, ++k);
             if (consume(B)) break;
         }
+#endif
     } else
     for (int it = 0; it < nsteps; ++it) {
         const bool interior = (unsigned)(it - 1) < (unsigned)kin;  // it in [1, kin]
