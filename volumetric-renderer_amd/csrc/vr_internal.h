@@ -50,6 +50,9 @@ using GeomWide = BrickGeom<VR_BRICK_CELLS>;
 // row is 8 bytes and a 648-B brick keeps every row 4-aligned: one dwordx4 from the 4-aligned
 // address at or below the cell's element holds elements x, x + 1 of rows y and y + 1 (byte
 // offsets s, s+1, s+8, s+9 with s = x mod 4 <= 3), a second one the same at z + 1.
+// VR_U8_BRICK_CELLS="3,8,8" (experiment builds): 4-byte rows, one dwordx2 per slice (half the
+// bytes per sample), 1.69x the voxels: C4 +1.5%, C5 +-0, views -2..+4%
+// (profiles/r02/u8_geometry/).
 // VR_U8_PLAIN = 0: yz-quad elements in GeomWide bricks (one 8-B load, 5.7x the voxels).
 #ifndef VR_U8_PLAIN
 #define VR_U8_PLAIN 1

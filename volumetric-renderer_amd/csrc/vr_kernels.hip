@@ -218,9 +218,24 @@ struct Cell8 {
             v[6] = r1.y;
             v[3] = r1.z;
             v[7] = r1.w;
+        } else if constexpr (kPlainByte<VT> && GeomByte::EX == 4) {
+            // 4-byte rows (3-cell-wide bricks): the row of the cell starts at the 4-aligned
+            // address at or below e; one dwordx2 per slice holds rows y and y+1, the cell's
+            // voxels at bytes s, s+1 of each dword (s = x <= 2)
+            const size_t a = e & ~(size_t)3;
+            const uint32_t sh = 8u * ((uint32_t)e & 3u);
+            const u2a q0 = *reinterpret_cast<const u2a *>(base + a);
+            const u2a q1 = *reinterpret_cast<const u2a *>(base + a + GeomByte::Slice);
+            const uint32_t w[4] = {q0.x >> sh, q0.y >> sh, q1.x >> sh, q1.y >> sh};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {  // r = dy + 2 dz
+                v[2 * r] = byte_value<VT>(w[r], 0);
+                v[2 * r + 1] = byte_value<VT>(w[r], 1);
+            }
         } else if constexpr (kPlainByte<VT>) {
             // one dwordx4 per slice from the 4-aligned address at or below e (bricks and rows
             // are 4-aligned: s = e mod 4 = x mod 4): bytes s, s+1 = row y, s+8, s+9 = row y+1
+            static_assert(GeomByte::EX == 8, "plain 8-bit rows are 4 or 8 bytes");
             const size_t a = e & ~(size_t)3;
             const uint32_t sh = (uint32_t)e & 3u;
             const u4a q0 = *reinterpret_cast<const u4a *>(base + a);
@@ -754,6 +769,9 @@ __device__ __forceinline__ void phong(const MarchParams &P, float gx, float gy_,
     }
 }
 
+#ifndef VR_EXP_WAVE_STEPS
+#define VR_EXP_WAVE_STEPS 0
+#endif
 #ifndef VR_EXP_NO_GRAD_LOADS
 #define VR_EXP_NO_GRAD_LOADS 0  // experiment builds: time without the difference-field loads
 #endif
@@ -1023,7 +1041,17 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
         const unsigned long long rays = wave_sum(covered ? 1ull : 0ull);
         const unsigned long long sm = wave_sum(n_samples);
         const unsigned long long sh = wave_sum(n_shaded);
+#if VR_EXP_WAVE_STEPS  // experiment builds: steps = 64 x the wave's longest ray (lane occupancy)
+        unsigned long long mx = n_steps;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long t = __shfl_xor(mx, o, 64);
+            mx = t > mx ? t : mx;
+        }
+        const unsigned long long st = 64ull * mx;
+#else
         const unsigned long long st = wave_sum(n_steps);
+#endif
         const unsigned long long sk = wave_sum(n_skipped);
         if (lane == 0) {
             atomicAdd(&P.counters[0], rays);
