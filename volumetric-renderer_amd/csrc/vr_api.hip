@@ -33,6 +33,8 @@ struct vr_ctx {
     size_t lin_bytes = 0;
     int storage = ST_F32;
     int layout = ST_F32;  // brick layout code (storage | kQuadFlag for 8-bit yz-quads)
+    // the last frame's view (view_dense_rows): image x along the bricks' rows, dense sampling
+    bool dense_rows = false;
     uint32_t nx = 1, ny = 1, nz = 1;
     float vmin = 0.0f, vmax = 1.0f;
     // transfer function (decoded, linear float RGBA)
@@ -417,20 +419,59 @@ int check_params(vr_ctx *c, const vr_params *p)
     return VR_OK;
 }
 
+// View shape for the launch policy, from inverse(proj * view): at the depth where the centre
+// pixel's ray passes closest to the volume centre, the world step of one pixel along the image
+// x axis.  True when that step runs along the volume's x (|x component| >= 0.9 of it: a
+// wavefront's 16-pixel rows follow the bricks' contiguous rows) and spans at most 0.8 voxels
+// (neighbouring lanes share cache lines).
+bool view_dense_rows(const double *inv, uint32_t W, uint32_t nx, uint32_t ny, uint32_t nz)
+{
+    auto unproject = [&](double x, double z, double out[3]) {
+        double h[4];
+        for (int r = 0; r < 4; ++r) h[r] = inv[0 * 4 + r] * x + inv[2 * 4 + r] * z + inv[3 * 4 + r];
+        for (int a = 0; a < 3; ++a) out[a] = h[a] / h[3];
+    };
+    double o[3], f[3], o2[3], f2[3], d[3], s[3];
+    unproject(0.0, 0.0, o);
+    unproject(0.0, 1.0, f);
+    const double dx = 2.0 / (double)W;
+    unproject(dx, 0.0, o2);
+    unproject(dx, 1.0, f2);
+    double od = 0.0, dd = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        d[a] = f[a] - o[a];
+        od += o[a] * d[a];
+        dd += d[a] * d[a];
+    }
+    if (!(dd > 0.0)) return false;
+    const double t = -od / dd;
+    double n2 = 0.0, v2 = 0.0;
+    const double nv[3] = {(double)nx, (double)ny, (double)nz};
+    for (int a = 0; a < 3; ++a) {
+        s[a] = (o2[a] + t * (f2[a] - o2[a])) - (o[a] + t * d[a]);
+        n2 += s[a] * s[a];
+        v2 += (s[a] * nv[a]) * (s[a] * nv[a]);
+    }
+    if (!(n2 > 0.0)) return false;
+    return std::fabs(s[0]) >= 0.9 * std::sqrt(n2) && std::sqrt(v2) <= 0.8;
+}
+
 // Pipelined march (two samples of a ray in flight, vr_kernels.hip PIPE): always for shaded
 // frames (-6% over the view sweep); for unshaded launches of fewer than kPipelineMaxWaves
 // wavefronts -- one rank's share of a multi-GPU frame -- where per-ray latency, not the
-// chip's throughput, bounds the kernel (N = 8 rank share: 0.153 -> 0.094 ms); and for large
+// chip's throughput, bounds the kernel (N = 8 rank share: 0.153 -> 0.094 ms); for large
 // volumes, whose gathers miss the caches more: >= kPipelineMinBytes bricked bytes, or
 // >= kPipelineMinVoxels voxels (C4 1024^3 u8 in plain bricks, 1.6 GB: 421 -> 451 Gsamples/s,
-// every view 7-10% faster serially; C2 256^3 u8 loses 4%, a 512^3 f32 full frame loses on
-// oblique views).  VR_PIPELINE=0/1 overrides (A/B).
+// every view 7-10% faster serially; C2 256^3 u8 loses 4%); and for unshaded frames whose view
+// is view_dense_rows (3 frames in flight, C3 volume: fill -11%, oblique -12%, top -18% ms per
+// frame; the side, diagonal and r = 3 views, which lose 2-12% pipelined, are not dense-row
+// views; profiles/r02/kernel_choice/inflight3_pipeline_views.txt).  VR_PIPELINE=0/1 overrides.
 bool use_pipeline(bool shading, uint32_t tiles, const vr_ctx *c)
 {
     if (const char *e = std::getenv("VR_PIPELINE")) return e[0] == '1';
     const size_t voxels = (size_t)c->nx * c->ny * c->nz;
     return shading || tiles * (kThreadsPerTile / 64) < kPipelineMaxWaves ||
-           c->brick_bytes >= kPipelineMinBytes || voxels >= kPipelineMinVoxels;
+           c->brick_bytes >= kPipelineMinBytes || voxels >= kPipelineMinVoxels || c->dense_rows;
 }
 
 // Lane-pair march (two lanes per ray, each lane pipelined) for SHADED launches of fewer than
@@ -519,6 +560,7 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.out_format = out_format;
     P.slab_default = c->smin[0] == 0.0f && c->smin[1] == 0.0f && c->smin[2] == 0.0f &&
                      c->smax[0] == 1.0f && c->smax[1] == 1.0f && c->smax[2] == 1.0f;
+    c->dense_rows = view_dense_rows(P.inv, c->width, c->nx, c->ny, c->nz);
     P.pipelined = use_pipeline(p->shading != 0, P.tiles_x * P.tiles_y, c);
     P.lin = c->lin;
     P.lpx = lin_pitch_x(c->nx);
