@@ -14,6 +14,27 @@ import os
 import sys
 
 
+def template_args(name, head):
+    """Top-level template arguments of the first `head<...>` in a demangled kernel name
+    (nested <> kept whole: "march_kernel<vr::Quad8<unsigned char>, false, ...>")."""
+    s = name.split(head, 1)[1]
+    args, depth, cur = [], 0, ""
+    for ch in s:
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            if depth == 0:
+                break
+            depth -= 1
+        if ch == "," and depth == 0:
+            args.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    args.append(cur.strip())
+    return args
+
+
 def load(d, kname):
     agg = collections.defaultdict(list)
     durs = []
@@ -23,7 +44,7 @@ def load(d, kname):
             if kname not in k:
                 continue
             if "march_kernel<" in k:  # <VT, SHADE, COUNT, SKIP>: skip the counting variant
-                targs = [t.strip() for t in k.split("march_kernel<", 1)[1].split(">", 1)[0].split(",")]
+                targs = template_args(k, "march_kernel<")
                 if len(targs) > 2 and targs[2] == "true":
                     continue
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))

@@ -14,6 +14,27 @@ import json
 import os
 import sys
 
+def template_args(name, head):
+    """Top-level template arguments of the first `head<...>` in a demangled kernel name
+    (nested <> kept whole: "march_kernel<vr::Quad8<unsigned char>, false, ...>")."""
+    s = name.split(head, 1)[1]
+    args, depth, cur = [], 0, ""
+    for ch in s:
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            if depth == 0:
+                break
+            depth -= 1
+        if ch == "," and depth == 0:
+            args.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    args.append(cur.strip())
+    return args
+
+
 CONFIGS = ("c3", "c3_ref", "c3_default", "c2", "c4", "c5")
 
 
@@ -21,7 +42,7 @@ def frame_kernel(name):
     """True for a march launch that renders a frame (not the COUNT instantiation)."""
     for k in ("march_kernel<", "march_pair_kernel<", "march_lds_kernel<"):
         if k in name:
-            targs = [t.strip() for t in name.split(k, 1)[1].split(">", 1)[0].split(",")]
+            targs = template_args(name, k)
             return not (k == "march_kernel<" and targs[2] == "true")  # <VT, SHADE, COUNT, ...>
     return False
 
