@@ -456,21 +456,23 @@ bool view_dense_rows(const double *inv, uint32_t W, uint32_t nx, uint32_t ny, ui
     return std::fabs(s[0]) >= 0.9 * std::sqrt(n2) && std::sqrt(v2) <= 0.8;
 }
 
-// Pipelined march (two samples of a ray in flight, vr_kernels.hip PIPE): always for shaded
-// frames (-6% over the view sweep); for unshaded launches of fewer than kPipelineMaxWaves
+// Pipelined march (two samples of a ray in flight, vr_kernels.hip PIPE): for launches of
+// fewer than kPipelineMaxWaves
 // wavefronts -- one rank's share of a multi-GPU frame -- where per-ray latency, not the
 // chip's throughput, bounds the kernel (N = 8 rank share: 0.153 -> 0.094 ms); for large
 // volumes, whose gathers miss the caches more: >= kPipelineMinBytes bricked bytes, or
 // >= kPipelineMinVoxels voxels (C4 1024^3 u8 in plain bricks, 1.6 GB: 421 -> 451 Gsamples/s,
-// every view 7-10% faster serially; C2 256^3 u8 loses 4%); and for unshaded frames whose view
-// is view_dense_rows (3 frames in flight, C3 volume: fill -11%, oblique -12%, top -18% ms per
-// frame; the side, diagonal and r = 3 views, which lose 2-12% pipelined, are not dense-row
-// views; profiles/r02/kernel_choice/inflight3_pipeline_views.txt).  VR_PIPELINE=0/1 overrides.
+// every view 7-10% faster serially; C2 256^3 u8 loses 4%); and for frames whose view is
+// view_dense_rows (3 frames in flight, C3 volume, ms per frame: unshaded fill -11%, oblique
+// -12%, top -18%; shaded fill -7%, oblique -7%, top -11%; the side, diagonal and r = 3 views,
+// which lose 2-12% unshaded and 2-7% shaded pipelined, are not dense-row views;
+// profiles/r02/kernel_choice/inflight3_pipeline_views*.txt).  VR_PIPELINE=0/1 overrides.
 bool use_pipeline(bool shading, uint32_t tiles, const vr_ctx *c)
 {
+    (void)shading;
     if (const char *e = std::getenv("VR_PIPELINE")) return e[0] == '1';
     const size_t voxels = (size_t)c->nx * c->ny * c->nz;
-    return shading || tiles * (kThreadsPerTile / 64) < kPipelineMaxWaves ||
+    return tiles * (kThreadsPerTile / 64) < kPipelineMaxWaves ||
            c->brick_bytes >= kPipelineMinBytes || voxels >= kPipelineMinVoxels || c->dense_rows;
 }
 
