@@ -421,13 +421,16 @@ def main():
         # the reference's default camera (benchmarks at r=1.6 plus the default)
         dcfg = CONFIGS["c3_default"]
         V = run_variant(rp, dcfg, args.steps, min(args.warmup, 5), rank, world, inflight)
-        dtr, _ = load_traffic("c3_default", world, kernel)
+        # the launch policy picks the kernel per view (vr_api.hip use_pipeline): match the PMC
+        # bytes of the kernel this view ran
+        dkernel = rp.kernel_name(vr_amd.default_params(shading=dcfg["shading"]))
+        dtr, _ = load_traffic("c3_default", world, dkernel)
         variants["default_camera"] = dict(
             workload=dcfg["workload"], camera=synth.CAMERAS[dcfg["cam"]],
             value=round(V["frame"]["samples"] * args.steps / V["secs"] / 1e9, 3), unit="Gsamples/s",
             ms_per_step=round(V["secs"] / args.steps * 1e3, 4), fps=round(args.steps / V["secs"], 2),
             samples_per_frame=V["frame"]["samples"], rays_per_frame=V["frame"]["rays"],
-            hbm_bytes_per_frame=dtr,
+            kernel=dkernel, hbm_bytes_per_frame=dtr,
             hbm_frac=round(dtr / (V["secs"] / args.steps) / 1e9 / HBM_PEAK_GBS, 4) if dtr else None)
         vcfg = CONFIGS["c3_ref"]
         V = run_variant(rp, vcfg, args.steps, min(args.warmup, 5), rank, world, inflight)
