@@ -385,14 +385,8 @@ def main():
     inflight = 1 if args.serial_gather else max(1, min(16, args.frames_in_flight))
     if BACKEND != "nccl":
         inflight = 1
-    R = run_variant(rp, cfg, args.steps, args.warmup, rank, world, inflight)
-    secs, kms, fstats, r0stats, shard_px = R["secs"], R["kms"], R["frame"], R["mine"], R["shard_px"]
-    frame_s = secs / args.steps
-    value = fstats["samples"] * args.steps / secs / 1e9
-    fps = args.steps / secs
     kernel = rp.kernel_name(vr_amd.default_params(shading=cfg["shading"]))
     traffic, traffic_src = load_traffic(args.config, world, kernel)
-    gather_bytes = algorithmic_bytes(fstats, vbytes, cfg["W"] * cfg["H"])
 
     # also the reference-equivalent sample count (volume.frag as written: no
     # ERT, every in-slab step sampled) of the same frame, per second of this configuration
@@ -404,6 +398,19 @@ def main():
         dist.all_reduce(ref_samples, op=dist.ReduceOp.SUM)
     ref_samples = int(ref_samples.item())
 
+    cpu = None
+    small = int(np.prod(cfg["dims"])) <= 512 ** 3  # the oracle needs the volume as host floats
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and small:
+        cpu = cpu_baseline(rp, cfg, args.cpu_budget)
+        nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+        if nproc and nproc != cpu["cores"]:
+            # the same sample with one thread per nproc CPU, for the record (quota-throttled)
+            allc = cpu_baseline(rp, cfg, min(4.0, args.cpu_budget), nproc)
+            cpu["all_nproc_threads"] = dict(value=allc["value"], cores=nproc, sample=allc["sample"])
+        # SURVEY.md 8d: C1-C3 on the host cores, C1/C2 on smaller budgets
+        cpu["other_configs"] = {n: cpu_baseline_other(n, device, min(4.0, args.cpu_budget), cpu["cores"])
+                                for n in ("c1", "c2")}
+
     variants = {}
     serial_kms = None
     if not args.no_variants and inflight > 1:
@@ -414,7 +421,7 @@ def main():
         V = run_variant(rp, cfg, ns, min(args.warmup, 5), rank, world, 1)
         serial_kms = V["kms"]
         variants["serial_frames"] = dict(
-            value=round(fstats["samples"] * ns / V["secs"] / 1e9, 3), unit="Gsamples/s",
+            value=round(V["frame"]["samples"] * ns / V["secs"] / 1e9, 3), unit="Gsamples/s",
             ms_per_step=round(V["secs"] / ns * 1e3, 4), fps=round(ns / V["secs"], 2),
             kernel_ms=round(V["kms"], 4), frame_check=V["check"])
     if not args.no_variants and args.config == "c3":
@@ -453,6 +460,17 @@ def main():
             reference_equivalent_gsamples_per_s=round(
                 (f3["samples"] + f3["skipped_samples"]) * args.steps / V["secs"] / 1e9, 3),
             samples_per_frame=f3["samples"], skipped_samples_per_frame=f3["skipped_samples"])
+    # The headline runs after the CPU baseline and the variants, right after their frames: a
+    # device that sat idle for >= 100 ms renders the first ~50 pipelined frames 10-15% slower
+    # (a power-state ramp that a matmul, an HBM copy or serial frames do not remove;
+    # profiles/r02/warm_state/), so a K = 20 region timed cold measures that ramp, not the march.
+    R = run_variant(rp, cfg, args.steps, args.warmup, rank, world, inflight)
+    secs, kms, fstats, r0stats, shard_px = R["secs"], R["kms"], R["frame"], R["mine"], R["shard_px"]
+    frame_s = secs / args.steps
+    value = fstats["samples"] * args.steps / secs / 1e9
+    fps = args.steps / secs
+    gather_bytes = algorithmic_bytes(fstats, vbytes, cfg["W"] * cfg["H"])
+
     if not args.no_variants and world == 1:
         # PCIe-inclusive: vr_render into (pageable) host memory, the drop-in record() path.
         # The frame's RGBA8 bytes cross PCIe inside the timed region; row bands copy while
@@ -471,19 +489,6 @@ def main():
             gsamples_per_s=round(fstats["samples"] * args.steps / sh / 1e9, 3),
             frame_bytes=int(hbuf.nbytes),
             path="vr_render -> pageable host RGBA8 each frame (synchronous, as OffscreenPass::record + readback)")
-
-    cpu = None
-    small = int(np.prod(cfg["dims"])) <= 512 ** 3  # the oracle needs the volume as host floats
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and small:
-        cpu = cpu_baseline(rp, cfg, args.cpu_budget)
-        nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-        if nproc and nproc != cpu["cores"]:
-            # the same sample with one thread per nproc CPU, for the record (quota-throttled)
-            allc = cpu_baseline(rp, cfg, min(4.0, args.cpu_budget), nproc)
-            cpu["all_nproc_threads"] = dict(value=allc["value"], cores=nproc, sample=allc["sample"])
-        # SURVEY.md 8d: C1-C3 on the host cores, C1/C2 on smaller budgets
-        cpu["other_configs"] = {n: cpu_baseline_other(n, device, min(4.0, args.cpu_budget), cpu["cores"])
-                                for n in ("c1", "c2")}
 
     if rank == 0:
         # Roofline: the kernel is bound by HBM by the SURVEY's classification (a gather, no

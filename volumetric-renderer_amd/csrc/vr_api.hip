@@ -552,6 +552,8 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.tiles_x = (c->width + 15) / 16;
     P.tiles_y = (P.local_rows + kMarchRows - 1) / kMarchRows;
     P.tile_order = p->tile_order >= 1 && p->tile_order <= 4 ? (uint32_t)p->tile_order : 4u;
+    if (const char *e = std::getenv("VR_TILE_ORDER_DEFAULT"))  // experiment knob: default order
+        if (p->tile_order == 0 && e[0] >= '1' && e[0] <= '4') P.tile_order = (uint32_t)(e[0] - '0');
     // wavefront footprint: 1 8x8, 2 16x4, 3 4x16; auto = 16x4 (x-contiguous brick rows:
     // fewer cache lines per wave-level load; measured -11% on the r=3 view, even on others)
     P.wave_w_shift = p->wave_shape == 1 ? 3u : (p->wave_shape == 3 ? 2u : 4u);
@@ -740,8 +742,11 @@ hipEvent_t pooled_event(vr_ctx *c)
         c->ev_pool.pop_back();
         return e;
     }
+    // timing-only events: no system-scope fence when recorded.  The default event's fence
+    // writes back and invalidates the caches between this frame's kernel and the next one on
+    // the stream (C3 with 3 frames in flight: 5-10% per frame with timing on)
     hipEvent_t e = nullptr;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
     return e;
 }
 

@@ -153,8 +153,9 @@ int timed_begin(vr_dist *d, std::vector<TimedOp> &v, hipStream_t s)
 {
     if (!d->timing) return VR_OK;
     TimedOp t;
-    DTRY(hip_check(d, hipEventCreate(&t.t0), "hipEventCreate"));
-    if (hipEventCreate(&t.t1) != hipSuccess) {
+    // timing-only events: no system-scope cache writeback/invalidate when recorded
+    DTRY(hip_check(d, hipEventCreateWithFlags(&t.t0, hipEventDisableSystemFence), "hipEventCreate"));
+    if (hipEventCreateWithFlags(&t.t1, hipEventDisableSystemFence) != hipSuccess) {
         hipEventDestroy(t.t0);
         return dfail(d, VR_EIO, "hipEventCreate");
     }
