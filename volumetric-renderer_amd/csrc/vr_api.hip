@@ -35,6 +35,7 @@ struct vr_ctx {
     int layout = ST_F32;  // brick layout code (storage | kQuadFlag for 8-bit yz-quads)
     // the last frame's view (view_dense_rows): image x along the bricks' rows, dense sampling
     bool dense_rows = false;
+    double pixel_span = 0.0;  // voxels per pixel step at the volume centre (view_dense_rows)
     uint32_t nx = 1, ny = 1, nz = 1;
     float vmin = 0.0f, vmax = 1.0f;
     // transfer function (decoded, linear float RGBA)
@@ -423,9 +424,11 @@ int check_params(vr_ctx *c, const vr_params *p)
 // pixel's ray passes closest to the volume centre, the world step of one pixel along the image
 // x axis.  True when that step runs along the volume's x (|x component| >= 0.9 of it: a
 // wavefront's 16-pixel rows follow the bricks' contiguous rows) and spans at most 0.8 voxels
-// (neighbouring lanes share cache lines).
-bool view_dense_rows(const double *inv, uint32_t W, uint32_t nx, uint32_t ny, uint32_t nz)
+// (neighbouring lanes share cache lines).  *span = that step's length in voxels.
+bool view_dense_rows(const double *inv, uint32_t W, uint32_t nx, uint32_t ny, uint32_t nz,
+                     double *span)
 {
+    *span = 0.0;
     auto unproject = [&](double x, double z, double out[3]) {
         double h[4];
         for (int r = 0; r < 4; ++r) h[r] = inv[0 * 4 + r] * x + inv[2 * 4 + r] * z + inv[3 * 4 + r];
@@ -453,7 +456,8 @@ bool view_dense_rows(const double *inv, uint32_t W, uint32_t nx, uint32_t ny, ui
         v2 += (s[a] * nv[a]) * (s[a] * nv[a]);
     }
     if (!(n2 > 0.0)) return false;
-    return std::fabs(s[0]) >= 0.9 * std::sqrt(n2) && std::sqrt(v2) <= 0.8;
+    *span = std::sqrt(v2);
+    return std::fabs(s[0]) >= 0.9 * std::sqrt(n2) && *span <= 0.8;
 }
 
 // Pipelined march (two samples of a ray in flight, vr_kernels.hip PIPE): for launches of
@@ -564,7 +568,7 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.out_format = out_format;
     P.slab_default = c->smin[0] == 0.0f && c->smin[1] == 0.0f && c->smin[2] == 0.0f &&
                      c->smax[0] == 1.0f && c->smax[1] == 1.0f && c->smax[2] == 1.0f;
-    c->dense_rows = view_dense_rows(P.inv, c->width, c->nx, c->ny, c->nz);
+    c->dense_rows = view_dense_rows(P.inv, c->width, c->nx, c->ny, c->nz, &c->pixel_span);
     P.pipelined = use_pipeline(p->shading != 0, P.tiles_x * P.tiles_y, c);
     P.lin = c->lin;
     P.lpx = lin_pitch_x(c->nx);
@@ -610,13 +614,30 @@ int ensure_skip(vr_ctx *c, MarchParams &P, hipStream_t s)
     return VR_OK;
 }
 
+// Shaded f32 frames read the difference field unless the view samples sparsely: a pixel step
+// of >= kFieldMaxSpan voxels at the volume centre (the reference's default camera, r = 3: 1.4).
+// There rays sit too far apart to share the field's cache lines, the frame streams the whole
+// volume from HBM, and the field's 3x bytes cost more than the stencil's extra loads of
+// density lines the ray already holds: r = 3 with 3 frames in flight 0.350/0.363 -> 0.326 ms
+// per frame; fill (0.55 voxels) 0.500 -> 0.565, side 0.587 -> 0.579, diagonal +-1%
+// (profiles/r02/sparse_view_grad/).  VR_NO_GRAD_FIELD: the stencil path always (A/B, tests);
+// VR_FIELD_MAX_SPAN overrides the threshold.
+constexpr double kFieldMaxSpan = 1.0;
+bool use_grad_field(const vr_ctx *c)
+{
+    if (c->storage != ST_F32) return false;
+    if (std::getenv("VR_NO_GRAD_FIELD")) return false;
+    double lim = kFieldMaxSpan;
+    if (const char *e = std::getenv("VR_FIELD_MAX_SPAN")) lim = std::atof(e);
+    return c->pixel_span < lim;
+}
+
 // Shaded f32 frames: (re)build the gradient field when stale.  It needs 3 x the bricked
 // density; when that does not fit beside a 2 GiB reserve the kernel forms the differences
 // from the 4-wide stencil instead (same values, bit for bit).
 void ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s)
 {
-    if (c->storage != ST_F32) return;
-    if (std::getenv("VR_NO_GRAD_FIELD")) return;  // A/B and tests: the stencil path
+    if (!use_grad_field(c)) return;
     const size_t bytes = c->brick_bytes / element_size(ST_F32) * kGradElemBytes;
     if (!c->grad || c->grad_bytes != bytes) {
         if (c->grad) hipFree(c->grad);
@@ -1301,7 +1322,7 @@ const char *vr_kernel_name(const vr_ctx *c, const vr_params *p)
 {
     if (!c) return "";
     // the variant the next vr_render_device launches (after a shaded frame built the field)
-    const bool gf = p && p->shading && c->storage == ST_F32 && c->grad && c->grad_valid;
+    const bool gf = p && p->shading && use_grad_field(c) && c->grad && c->grad_valid;
     // the full frame (row_block 16, one rank), as vr_render launches it
     const uint32_t tiles = ((c->width + 15) / 16) * ((c->height + kMarchRows - 1) / kMarchRows);
     const bool pipe = use_pipeline(p && p->shading, tiles, c) &&
