@@ -37,6 +37,9 @@ import vr_dist  # noqa: E402
 
 BACKEND = "nccl"
 GATHER = "native"  # N > 1 over RCCL: "native" (vr_dist.h) or "torch" (torch.distributed.gather)
+# pipelined variants warm up for this many frames: they are measured in the device's steady
+# state (the headline keeps the driver's --warmup; see main())
+VARIANT_WARMUP = 120
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "Gsamples/sec + fps, 512³ NRRD @ 1080p; achieved HBM GB/s vs peak"
 
@@ -385,8 +388,6 @@ def main():
     inflight = 1 if args.serial_gather else max(1, min(16, args.frames_in_flight))
     if BACKEND != "nccl":
         inflight = 1
-    kernel = rp.kernel_name(vr_amd.default_params(shading=cfg["shading"]))
-    traffic, traffic_src = load_traffic(args.config, world, kernel)
 
     # also the reference-equivalent sample count (volume.frag as written: no
     # ERT, every in-slab step sampled) of the same frame, per second of this configuration
@@ -427,7 +428,7 @@ def main():
     if not args.no_variants and args.config == "c3":
         # the reference's default camera (benchmarks at r=1.6 plus the default)
         dcfg = CONFIGS["c3_default"]
-        V = run_variant(rp, dcfg, args.steps, min(args.warmup, 5), rank, world, inflight)
+        V = run_variant(rp, dcfg, args.steps, VARIANT_WARMUP, rank, world, inflight)
         # the launch policy picks the kernel per view (vr_api.hip use_pipeline): match the PMC
         # bytes of the kernel this view ran
         dkernel = rp.kernel_name(vr_amd.default_params(shading=dcfg["shading"]))
@@ -440,7 +441,7 @@ def main():
             kernel=dkernel, hbm_bytes_per_frame=dtr,
             hbm_frac=round(dtr / (V["secs"] / args.steps) / 1e9 / HBM_PEAK_GBS, 4) if dtr else None)
         vcfg = CONFIGS["c3_ref"]
-        V = run_variant(rp, vcfg, args.steps, min(args.warmup, 5), rank, world, inflight)
+        V = run_variant(rp, vcfg, args.steps, VARIANT_WARMUP, rank, world, inflight)
         rtr, _ = load_traffic("c3_ref", world, rp.kernel_name(vr_amd.default_params(shading=0)))
         variants["reference_semantics_no_shading_no_ert"] = dict(
             value=round(V["frame"]["samples"] * args.steps / V["secs"] / 1e9, 3), unit="Gsamples/s",
@@ -451,7 +452,7 @@ def main():
         # opt-in empty-space skipping (bit-identical frames): executed samples drop, so it is
         # reported as fps and as reference-equivalent samples/s, never as the headline value
         scfg = dict(CONFIGS["c3"], skip_empty=1)
-        V = run_variant(rp, scfg, args.steps, min(args.warmup, 5), rank, world, inflight)
+        V = run_variant(rp, scfg, args.steps, VARIANT_WARMUP, rank, world, inflight)
         f3 = V["frame"]
         variants["c3_skip_empty"] = dict(
             fps=round(args.steps / V["secs"], 2), ms_per_step=round(V["secs"] / args.steps * 1e3, 4),
@@ -470,6 +471,10 @@ def main():
     value = fstats["samples"] * args.steps / secs / 1e9
     fps = args.steps / secs
     gather_bytes = algorithmic_bytes(fstats, vbytes, cfg["W"] * cfg["H"])
+    # the kernel the launch policy picked for the headline's view (vr_kernel_name reads the
+    # last frame's view), and the PMC bytes measured for that kernel
+    kernel = rp.kernel_name(vr_amd.default_params(shading=cfg["shading"]))
+    traffic, traffic_src = load_traffic(args.config, world, kernel)
 
     if not args.no_variants and world == 1:
         # PCIe-inclusive: vr_render into (pageable) host memory, the drop-in record() path.

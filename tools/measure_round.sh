@@ -27,7 +27,7 @@ for cfg in $CFGS; do
 done &&
 python tools/traffic_json.py $O $O/pmc_traffic.json > /dev/null &&
 cp $O/pmc_traffic.json profiles/pmc_traffic.json &&
-timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err
+timeout -k 10 900 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err
 rc=$?
 echo "rc=$rc" > $O/rc.txt
 exit $rc
