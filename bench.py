@@ -27,6 +27,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 for sub in ("volumetric-renderer_amd", "tools", "oracle"):
     sys.path.insert(0, os.path.join(ROOT, sub))
 
+# 3 frames in flight on 3 streams, next to torch's own streams: with HIP's default of 4
+# hardware queues, two frame streams of a run can land on one queue and serialise (the
+# default-camera variant 0.38-0.39 against 0.33 ms per frame; profiles/r02/warm_state/
+# hw_queues.txt).  Set before the HIP runtime starts; an explicit setting wins.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402

@@ -66,6 +66,7 @@ struct vr_ctx {
         uint32_t tiles_x = 0, tiles_y = 0, supers_x = 0, per_xcd = 0;
         uint32_t row_block = 0, rank = 0, nranks = 0;
         int pair = 0;
+        uint32_t kernel = 0;  // march variant (tile_kernel_key): its tiles' durations differ
         void *stream = nullptr;
         uint32_t *cost = nullptr, *perm = nullptr, *lists = nullptr;
         bool have_perm = false;
@@ -686,14 +687,25 @@ int ensure_derived(vr_ctx *c, const vr_params *p, MarchParams &P, hipStream_t s)
     return VR_OK;
 }
 
+// The march variant a launch runs, as part of the schedule key: a shaded, unshaded or
+// skip-empty frame of the same geometry on the same stream has other tile durations, so one
+// variant's order is not learned from another's (speed only; no measured change on the bench,
+// whose runs use fresh streams).
+uint32_t tile_kernel_key(const MarchParams &P, bool shading)
+{
+    return (shading ? 1u : 0u) | (P.skip_empty ? 2u : 0u) | (P.grad ? 4u : 0u) |
+           (P.pipelined ? 8u : 0u);
+}
+
 // Adaptive tile order (tile_order 4): the schedule entry of this launch geometry (created on
-// first use, at most 16 kept, one per
-// geometry and stream); sets P.tile_cost, and P.tile_perm once a permutation exists.
-vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P, void *stream)
+// first use, at most kMaxTileScheds kept, one per geometry, stream and march variant); sets
+// P.tile_cost, and P.tile_perm once a permutation exists.
+vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P, void *stream, uint32_t kernel)
 {
     if (P.tile_order != 4) return nullptr;
     for (auto &t : c->sched)
         if (t.tiles_x == P.tiles_x && t.tiles_y == P.tiles_y && t.pair == P.pair &&
+            t.kernel == kernel &&
             t.stream == stream && t.row_block == P.row_block && t.rank == P.rank &&
             t.nranks == P.nranks) {
             P.tile_cost = t.cost;
@@ -703,7 +715,7 @@ vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P, void *stream)
             }
             return &t;
         }
-    if (c->sched.size() >= 16) {
+    if (c->sched.size() >= kMaxTileScheds) {
         hipFree(c->sched.front().cost);
         hipFree(c->sched.front().perm);
         hipFree(c->sched.front().lists);
@@ -714,6 +726,7 @@ vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P, void *stream)
     t.tiles_y = P.tiles_y;
     t.supers_x = P.supers_x;
     t.pair = P.pair;
+    t.kernel = kernel;
     t.stream = stream;
     t.row_block = P.row_block;
     t.rank = P.rank;
@@ -1148,7 +1161,7 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
         P.tiles_y = (P.local_rows + th - 1) / th;
         P.supers_total = P.supers_x * ((P.tiles_y + kSuper - 1) / kSuper);
     }
-    vr_ctx::TileSched *ts = tile_sched(c, P, stream);
+    vr_ctx::TileSched *ts = tile_sched(c, P, stream, tile_kernel_key(P, p->shading != 0));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing) {
         e0 = pooled_event(c);

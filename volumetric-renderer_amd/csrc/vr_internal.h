@@ -285,6 +285,8 @@ hipError_t launch_order_tiles(const uint32_t *cost, const uint32_t *lists, uint3
 #define VR_REORDER_EVERY 4
 #endif
 constexpr uint32_t kReorderEvery = VR_REORDER_EVERY;
+// schedules kept (one per geometry, stream and march variant; oldest dropped first)
+constexpr size_t kMaxTileScheds = 64;
 // Wavefront count (single-lane tiling) below which a launch uses the lane-pair kernel.
 constexpr uint32_t kPairMaxWaves = 24576;
 constexpr uint32_t kPairQuadMaxWaves = 6144;  // below: 4 lanes per ray
