@@ -468,7 +468,10 @@ def test_f32_gradient_field_equals_stencil_gradient(rp, monkeypatch):
         cam = synth.camera(camname).to_vr_camera()
         for skip in (0, 1):
             p = vr_amd.default_params(shading=1, skip_empty=skip)
+            # the field for every view (small frames of small volumes are sparse views)
+            monkeypatch.setenv("VR_FIELD_MAX_SPAN", "1e30")
             a = rp.render(cam, p, vr_amd.OUT_RGBA32F)
+            monkeypatch.delenv("VR_FIELD_MAX_SPAN")
             monkeypatch.setenv("VR_NO_GRAD_FIELD", "1")
             b = rp.render(cam, p, vr_amd.OUT_RGBA32F)
             monkeypatch.delenv("VR_NO_GRAD_FIELD")
@@ -476,6 +479,28 @@ def test_f32_gradient_field_equals_stencil_gradient(rp, monkeypatch):
     ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), synth.tf_band(0.2, 0.9), cam,
                            W, H, vr_amd.default_params(shading=1))
     check(a, ref)
+
+
+def test_sparse_views_take_the_stencil_gradient(rp):
+    """Launch policy (vr_api.hip use_grad_field): a shaded f32 frame whose pixel step at the
+    volume centre spans >= 1 voxel (the reference's default camera, r = 3) forms the gradient
+    from the density stencil; a frame-filling view (r = 1.6, 0.6 voxels per pixel here) reads
+    the difference field.  Both match the oracle."""
+    W, H = 192, 120
+    rp.framebuffer_size_changed(W, H)
+    vol = synth.gaussians_numpy((64, 64, 64), seed=21).astype(np.float32)
+    rp.volume_dataset_changed(synth.dataset(vol))
+    tf = synth.tf_band(0.15, 0.9)
+    rp.transfer_function_changed(tf)
+    p = vr_amd.default_params(shading=1)
+    for camname, field in (("fill", True), ("default", False), ("fill", True)):
+        cam = synth.camera(camname).to_vr_camera()
+        img = rp.render(cam, p, vr_amd.OUT_RGBA32F)
+        name = rp.kernel_name(p)
+        gf = "<float, true, false, false, true," in name
+        assert gf == field, (camname, name)
+        ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p)
+        check(img, ref)
 
 
 @pytest.mark.parametrize("shading", [0, 1])
