@@ -461,6 +461,28 @@ bool view_dense_rows(const double *inv, uint32_t W, uint32_t nx, uint32_t ny, ui
     return std::fabs(s[0]) >= 0.9 * std::sqrt(n2) && *span <= 0.8;
 }
 
+// Shaded f32 frames read the difference field unless the view samples sparsely: a pixel step
+// of >= kFieldMaxSpan voxels at the volume centre (the reference's default camera, r = 3: 1.4).
+// There rays sit too far apart to share the field's cache lines, the frame streams the whole
+// volume from HBM, and the field's 3x bytes cost more than the stencil's extra loads of
+// density lines the ray already holds: r = 3 with 3 frames in flight 0.350/0.363 -> 0.326 ms
+// per frame; fill (0.55 voxels) 0.500 -> 0.565, side 0.587 -> 0.579, diagonal +-1%
+// (profiles/r02/sparse_view_grad/).  VR_NO_GRAD_FIELD: the stencil path always (A/B, tests);
+// VR_FIELD_MAX_SPAN overrides the threshold.
+constexpr double kFieldMaxSpan = 1.0;
+bool sparse_view(const vr_ctx *c)
+{
+    double lim = kFieldMaxSpan;
+    if (const char *e = std::getenv("VR_FIELD_MAX_SPAN")) lim = std::atof(e);
+    return c->pixel_span >= lim;
+}
+bool use_grad_field(const vr_ctx *c)
+{
+    if (c->storage != ST_F32) return false;
+    if (std::getenv("VR_NO_GRAD_FIELD")) return false;
+    return !sparse_view(c);
+}
+
 // Pipelined march (two samples of a ray in flight, vr_kernels.hip PIPE): for launches of
 // fewer than kPipelineMaxWaves
 // wavefronts -- one rank's share of a multi-GPU frame -- where per-ray latency, not the
@@ -471,14 +493,17 @@ bool view_dense_rows(const double *inv, uint32_t W, uint32_t nx, uint32_t ny, ui
 // view_dense_rows (3 frames in flight, C3 volume, ms per frame: unshaded fill -11%, oblique
 // -12%, top -18%; shaded fill -7%, oblique -7%, top -11%; the side, diagonal and r = 3 views,
 // which lose 2-12% unshaded and 2-7% shaded pipelined, are not dense-row views;
-// profiles/r02/kernel_choice/inflight3_pipeline_views*.txt).  VR_PIPELINE=0/1 overrides.
+// profiles/r02/kernel_choice/inflight3_pipeline_views*.txt); and for shaded f32 frames of
+// sparse views, which form the gradient from the stencil (r = 3 with 3 frames in flight:
+// 0.329 -> 0.306 ms per frame; profiles/r02/sparse_view_grad/default_knobs.txt).
+// VR_PIPELINE=0/1 overrides.
 bool use_pipeline(bool shading, uint32_t tiles, const vr_ctx *c)
 {
-    (void)shading;
     if (const char *e = std::getenv("VR_PIPELINE")) return e[0] == '1';
     const size_t voxels = (size_t)c->nx * c->ny * c->nz;
     return tiles * (kThreadsPerTile / 64) < kPipelineMaxWaves ||
-           c->brick_bytes >= kPipelineMinBytes || voxels >= kPipelineMinVoxels || c->dense_rows;
+           c->brick_bytes >= kPipelineMinBytes || voxels >= kPipelineMinVoxels || c->dense_rows ||
+           (shading && c->storage == ST_F32 && sparse_view(c));
 }
 
 // Lane-pair march (two lanes per ray, each lane pipelined) for SHADED launches of fewer than
@@ -613,24 +638,6 @@ int ensure_skip(vr_ctx *c, MarchParams &P, hipStream_t s)
     P.skip_dist = c->skip_dist;
     P.skip_empty = 1;
     return VR_OK;
-}
-
-// Shaded f32 frames read the difference field unless the view samples sparsely: a pixel step
-// of >= kFieldMaxSpan voxels at the volume centre (the reference's default camera, r = 3: 1.4).
-// There rays sit too far apart to share the field's cache lines, the frame streams the whole
-// volume from HBM, and the field's 3x bytes cost more than the stencil's extra loads of
-// density lines the ray already holds: r = 3 with 3 frames in flight 0.350/0.363 -> 0.326 ms
-// per frame; fill (0.55 voxels) 0.500 -> 0.565, side 0.587 -> 0.579, diagonal +-1%
-// (profiles/r02/sparse_view_grad/).  VR_NO_GRAD_FIELD: the stencil path always (A/B, tests);
-// VR_FIELD_MAX_SPAN overrides the threshold.
-constexpr double kFieldMaxSpan = 1.0;
-bool use_grad_field(const vr_ctx *c)
-{
-    if (c->storage != ST_F32) return false;
-    if (std::getenv("VR_NO_GRAD_FIELD")) return false;
-    double lim = kFieldMaxSpan;
-    if (const char *e = std::getenv("VR_FIELD_MAX_SPAN")) lim = std::atof(e);
-    return c->pixel_span < lim;
 }
 
 // Shaded f32 frames: (re)build the gradient field when stale.  It needs 3 x the bricked
