@@ -468,10 +468,10 @@ def test_f32_gradient_field_equals_stencil_gradient(rp, monkeypatch):
         cam = synth.camera(camname).to_vr_camera()
         for skip in (0, 1):
             p = vr_amd.default_params(shading=1, skip_empty=skip)
-            # the field for every view (small frames of small volumes are sparse views)
-            monkeypatch.setenv("VR_FIELD_MAX_SPAN", "1e30")
+            # the field for every view (the launch policy reads it on dense-row views only)
+            monkeypatch.setenv("VR_GRAD_FIELD_ALWAYS", "1")
             a = rp.render(cam, p, vr_amd.OUT_RGBA32F)
-            monkeypatch.delenv("VR_FIELD_MAX_SPAN")
+            monkeypatch.delenv("VR_GRAD_FIELD_ALWAYS")
             monkeypatch.setenv("VR_NO_GRAD_FIELD", "1")
             b = rp.render(cam, p, vr_amd.OUT_RGBA32F)
             monkeypatch.delenv("VR_NO_GRAD_FIELD")
@@ -482,10 +482,10 @@ def test_f32_gradient_field_equals_stencil_gradient(rp, monkeypatch):
 
 
 def test_sparse_views_take_the_stencil_gradient(rp):
-    """Launch policy (vr_api.hip use_grad_field): a shaded f32 frame whose pixel step at the
-    volume centre spans >= 1 voxel (the reference's default camera, r = 3) forms the gradient
-    from the density stencil; a frame-filling view (r = 1.6, 0.6 voxels per pixel here) reads
-    the difference field.  Both match the oracle."""
+    """Launch policy (vr_api.hip use_grad_field): a shaded f32 frame reads the difference
+    field on dense-row views (the frame-filling r = 1.6 view, 0.6 voxels per pixel here) and
+    forms the gradient from the density stencil elsewhere (the reference's default camera,
+    r = 3, 1.2 voxels per pixel here).  Both match the oracle."""
     W, H = 192, 120
     rp.framebuffer_size_changed(W, H)
     vol = synth.gaussians_numpy((64, 64, 64), seed=21).astype(np.float32)

@@ -461,26 +461,21 @@ bool view_dense_rows(const double *inv, uint32_t W, uint32_t nx, uint32_t ny, ui
     return std::fabs(s[0]) >= 0.9 * std::sqrt(n2) && *span <= 0.8;
 }
 
-// Shaded f32 frames read the difference field unless the view samples sparsely: a pixel step
-// of >= kFieldMaxSpan voxels at the volume centre (the reference's default camera, r = 3: 1.4).
-// There rays sit too far apart to share the field's cache lines, the frame streams the whole
-// volume from HBM, and the field's 3x bytes cost more than the stencil's extra loads of
-// density lines the ray already holds: r = 3 with 3 frames in flight 0.350/0.363 -> 0.326 ms
-// per frame; fill (0.55 voxels) 0.500 -> 0.565, side 0.587 -> 0.579, diagonal +-1%
-// (profiles/r02/sparse_view_grad/).  VR_NO_GRAD_FIELD: the stencil path always (A/B, tests);
-// VR_FIELD_MAX_SPAN overrides the threshold.
-constexpr double kFieldMaxSpan = 1.0;
-bool sparse_view(const vr_ctx *c)
-{
-    double lim = kFieldMaxSpan;
-    if (const char *e = std::getenv("VR_FIELD_MAX_SPAN")) lim = std::atof(e);
-    return c->pixel_span >= lim;
-}
+// Shaded f32 frames read the difference field only on dense-row views (view_dense_rows:
+// image x along the bricks' rows, <= 0.8 voxels per pixel), where a wavefront's rays share
+// the field's cache lines.  Every other view forms the gradient from the density stencil,
+// pipelined (use_pipeline): the field is 3x the density's bytes, and off the bricks' rows its
+// 6 loads per shaded sample miss more than the stencil's extra loads of the density lines the
+// ray already holds.  C3, 3 frames in flight, ms per frame (field -> stencil + pipelined;
+// profiles/r02/sparse_view_grad/): default camera r = 3 0.363 -> 0.302, diagonal 0.812 ->
+// 0.770, side 0.600 -> 0.587; the fill view keeps the field (stencil: 0.500 -> 0.565).
+// VR_NO_GRAD_FIELD / VR_GRAD_FIELD_ALWAYS: the stencil / the field for every view (A/B, tests).
 bool use_grad_field(const vr_ctx *c)
 {
     if (c->storage != ST_F32) return false;
     if (std::getenv("VR_NO_GRAD_FIELD")) return false;
-    return !sparse_view(c);
+    if (std::getenv("VR_GRAD_FIELD_ALWAYS")) return true;
+    return c->dense_rows;
 }
 
 // Pipelined march (two samples of a ray in flight, vr_kernels.hip PIPE): for launches of
@@ -493,17 +488,17 @@ bool use_grad_field(const vr_ctx *c)
 // view_dense_rows (3 frames in flight, C3 volume, ms per frame: unshaded fill -11%, oblique
 // -12%, top -18%; shaded fill -7%, oblique -7%, top -11%; the side, diagonal and r = 3 views,
 // which lose 2-12% unshaded and 2-7% shaded pipelined, are not dense-row views;
-// profiles/r02/kernel_choice/inflight3_pipeline_views*.txt); and for shaded f32 frames of
-// sparse views, which form the gradient from the stencil (r = 3 with 3 frames in flight:
-// 0.329 -> 0.306 ms per frame; profiles/r02/sparse_view_grad/default_knobs.txt).
-// VR_PIPELINE=0/1 overrides.
+// profiles/r02/kernel_choice/inflight3_pipeline_views*.txt); and for every shaded f32 frame:
+// off the dense-row views they form the gradient from the stencil (use_grad_field), and
+// pipelined that runs 5-8% faster (3 frames in flight: r = 3 0.329 -> 0.306, diagonal
+// 0.812 -> 0.770 ms; profiles/r02/sparse_view_grad/).  VR_PIPELINE=0/1 overrides.
 bool use_pipeline(bool shading, uint32_t tiles, const vr_ctx *c)
 {
     if (const char *e = std::getenv("VR_PIPELINE")) return e[0] == '1';
     const size_t voxels = (size_t)c->nx * c->ny * c->nz;
     return tiles * (kThreadsPerTile / 64) < kPipelineMaxWaves ||
            c->brick_bytes >= kPipelineMinBytes || voxels >= kPipelineMinVoxels || c->dense_rows ||
-           (shading && c->storage == ST_F32 && sparse_view(c));
+           (shading && c->storage == ST_F32);
 }
 
 // Lane-pair march (two lanes per ray, each lane pipelined) for SHADED launches of fewer than
