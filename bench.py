@@ -30,8 +30,9 @@ for sub in ("volumetric-renderer_amd", "tools", "oracle"):
 # 3 frames in flight on 3 streams, next to torch's own streams: with HIP's default of 4
 # hardware queues, two frame streams of a run can land on one queue and serialise (the
 # default-camera variant 0.38-0.39 against 0.33 ms per frame; profiles/r02/warm_state/
-# hw_queues.txt).  Set before the HIP runtime starts; an explicit setting wins.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# hw_queues.txt).  Set before the HIP runtime starts (raised to 8; the GPU boxes export 4).
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -405,19 +406,6 @@ def main():
         dist.all_reduce(ref_samples, op=dist.ReduceOp.SUM)
     ref_samples = int(ref_samples.item())
 
-    cpu = None
-    small = int(np.prod(cfg["dims"])) <= 512 ** 3  # the oracle needs the volume as host floats
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and small:
-        cpu = cpu_baseline(rp, cfg, args.cpu_budget)
-        nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-        if nproc and nproc != cpu["cores"]:
-            # the same sample with one thread per nproc CPU, for the record (quota-throttled)
-            allc = cpu_baseline(rp, cfg, min(4.0, args.cpu_budget), nproc)
-            cpu["all_nproc_threads"] = dict(value=allc["value"], cores=nproc, sample=allc["sample"])
-        # SURVEY.md 8d: C1-C3 on the host cores, C1/C2 on smaller budgets
-        cpu["other_configs"] = {n: cpu_baseline_other(n, device, min(4.0, args.cpu_budget), cpu["cores"])
-                                for n in ("c1", "c2")}
-
     variants = {}
     serial_kms = None
     if not args.no_variants and inflight > 1:
@@ -467,7 +455,7 @@ def main():
             reference_equivalent_gsamples_per_s=round(
                 (f3["samples"] + f3["skipped_samples"]) * args.steps / V["secs"] / 1e9, 3),
             samples_per_frame=f3["samples"], skipped_samples_per_frame=f3["skipped_samples"])
-    # The headline runs after the CPU baseline and the variants, right after their frames: a
+    # The headline runs after the variants, right after their frames: a
     # device that sat idle for >= 100 ms renders the first ~50 pipelined frames 10-15% slower
     # (a power-state ramp that a matmul, an HBM copy or serial frames do not remove;
     # profiles/r02/warm_state/), so a K = 20 region timed cold measures that ramp, not the march.
@@ -500,6 +488,22 @@ def main():
             gsamples_per_s=round(fstats["samples"] * args.steps / sh / 1e9, 3),
             frame_bytes=int(hbuf.nbytes),
             path="vr_render -> pageable host RGBA8 each frame (synchronous, as OffscreenPass::record + readback)")
+
+    # the CPU baseline last: its OpenMP threads (in this process) would compete with the
+    # launching thread of the GPU runs
+    cpu = None
+    small = int(np.prod(cfg["dims"])) <= 512 ** 3  # the oracle needs the volume as host floats
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and small:
+        cpu = cpu_baseline(rp, cfg, args.cpu_budget)
+        nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+        if nproc and nproc != cpu["cores"]:
+            # the same sample with one thread per nproc CPU, for the record (quota-throttled)
+            allc = cpu_baseline(rp, cfg, min(4.0, args.cpu_budget), nproc)
+            cpu["all_nproc_threads"] = dict(value=allc["value"], cores=nproc, sample=allc["sample"])
+        # SURVEY.md 8d: C1-C3 on the host cores, C1/C2 on smaller budgets
+        cpu["other_configs"] = {n: cpu_baseline_other(n, device, min(4.0, args.cpu_budget), cpu["cores"])
+                                for n in ("c1", "c2")}
+
 
     if rank == 0:
         # Roofline: the kernel is bound by HBM by the SURVEY's classification (a gather, no
