@@ -27,7 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 for sub in ("volumetric-renderer_amd", "tools", "oracle"):
     sys.path.insert(0, os.path.join(ROOT, sub))
 
-# 3 frames in flight on 3 streams, next to torch's own streams: with HIP's default of 4
+# 4 frames in flight on 4 streams, next to torch's own streams: with HIP's default of 4
 # hardware queues, two frame streams of a run can land on one queue and serialise (the
 # default-camera variant 0.38-0.39 against 0.33 ms per frame; profiles/r02/warm_state/
 # hw_queues.txt).  Set before the HIP runtime starts (raised to 8; the GPU boxes export 4).
@@ -364,7 +364,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--frames-in-flight", type=int, default=3,
+    ap.add_argument("--frames-in-flight", type=int, default=4,
                     help="frames in flight on separate streams (1 = serial frame loop)")
     ap.add_argument("--serial-gather", action="store_true",
                     help="= --frames-in-flight 1: each frame's gather waited for before the next render")
