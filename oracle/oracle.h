@@ -16,6 +16,39 @@
  * plus the build's own extension (central-difference gradient Phong shading; the reference
  * has no shading).
  *
+ * Fixed-function semantics the shader runs under, and the Vulkan 1.3 specification text each
+ * rule restates (chapter "Image Operations" unless noted; section titles, not numbers, since
+ * numbering moves between spec revisions):
+ *   texel centres, u = s*N - 0.5       "Texel Coordinate Systems" + "Texel Filtering":
+ *                                      VK_FILTER_LINEAR takes i0 = floor(u - 0.5), i1 = i0 + 1,
+ *                                      weight alpha = frac(u - 0.5)   (texel_coord, tf_lookup)
+ *   trilinear order: x, then y, z      "Texel Filtering", the LINEAR formula for 3D images as a
+ *                                      weighted sum; the lerp nesting is this restatement's
+ *                                      choice (hardware precision is implementation-defined)
+ *   border = transparent black         "Wrapping Operations" (CLAMP_TO_BORDER keeps texels
+ *                                      outside the image as border texels) + "Texel
+ *                                      Replacement" (VK_BORDER_COLOR_FLOAT_TRANSPARENT_BLACK
+ *                                      = (0,0,0,0); R32_SFLOAT reads R = 0)      (voxel)
+ *   TF clamp-to-edge                   "Wrapping Operations": CLAMP_TO_EDGE i = clamp(i, 0, N-1)
+ *   sRGB decode BEFORE filtering       "Format Conversion" (each texel of an _SRGB format is
+ *                                      UNORM-converted, then R,G,B go through the sRGB EOTF of
+ *                                      the Khronos Data Format Specification; A unchanged),
+ *                                      which the sampling pipeline applies per texel ahead of
+ *                                      "Texel Filtering"                   (srgb_to_linear)
+ *   UNORM8 decode c / 255              "Fixed-Point Data Conversions": normalized fixed-point
+ *                                      to float, f = c / (2^b - 1)
+ *   RGBA8 UNORM store                  same section, float to normalized fixed-point:
+ *                                      convertFloatToUint(f * 255, 8) returns one of the two
+ *                                      nearest integers ("should" round to nearest) -- hence
+ *                                      the 1-LSB tolerance of the RGBA8 parity tests
+ *   blend                              chapter "The Framebuffer", "Blend Operations":
+ *                                      VK_BLEND_OP_ADD, RGB = src*Sf + dst*Df with the factors
+ *                                      of offscreen_pass.cpp:715-725
+ *   back-face cull, depth              chapter "Rasterization", "Basic Polygon Rasterization"
+ *                                      (facing from the signed area) / offscreen_pass.cpp:680-712
+ *
+ * These are cited to the published spec; no Vulkan implementation ran here to confirm them.
+ *
  * Parity status: the reference's hot path is a Vulkan fragment shader that cannot run in
  * this container (no Vulkan/ICD/glslc) and the reference ships no tests or
  * golden images, so pixel parity against the REAL reference is unpinned.  This restatement
