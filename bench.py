@@ -13,7 +13,12 @@ Workload (configs[2] of BASELINE.json, the configuration the metric is quoted on
   early-ray termination (eps 1e-5).  The reference-semantics variant (no shading, no ERT) is
   timed as well and reported under "variants".
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]; N > 1 under torch.distributed.run.
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W].
+  N > 1 under torch.distributed.run (WORLD_SIZE set): one process per GPU, the library's RCCL
+        frame path (vr_dist.h); WORLD_SIZE must equal N.
+  N > 1 without WORLD_SIZE: ONE process driving N devices through a multi-device context
+        (vr_create_mask, the drop-in boundary's own multi-GPU form).
+  Either way a run that cannot use exactly N GPUs fails (exit 2) naming what is missing.
 """
 from __future__ import annotations
 
@@ -27,12 +32,21 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 for sub in ("volumetric-renderer_amd", "tools", "oracle"):
     sys.path.insert(0, os.path.join(ROOT, sub))
 
-# 4 frames in flight on 4 streams, next to torch's own streams: with HIP's default of 4
-# hardware queues, two frame streams of a run can land on one queue and serialise (the
-# default-camera variant 0.38-0.39 against 0.33 ms per frame; profiles/r02/warm_state/
-# hw_queues.txt).  Set before the HIP runtime starts (raised to 8; the GPU boxes export 4).
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# Hardware queues: the process's environment is used as it is (HIP's default and the GPU
+# boxes' setting is 4) and recorded in the JSON line.  `--hw-queues Q` sets GPU_MAX_HW_QUEUES
+# for this process before the HIP runtime starts (an explicit experiment; never the default).
+def _early_flag(name):
+    for i, a in enumerate(sys.argv):
+        if a == name and i + 1 < len(sys.argv):
+            return sys.argv[i + 1]
+        if a.startswith(name + "="):
+            return a.split("=", 1)[1]
+    return None
+
+
+if _early_flag("--hw-queues") is not None:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(int(_early_flag("--hw-queues")))
+HW_QUEUES = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -44,9 +58,11 @@ import vr_dist  # noqa: E402
 
 BACKEND = "nccl"
 GATHER = "native"  # N > 1 over RCCL: "native" (vr_dist.h) or "torch" (torch.distributed.gather)
-# pipelined variants warm up for this many frames: they are measured in the device's steady
-# state (the headline keeps the driver's --warmup; see main())
-VARIANT_WARMUP = 120
+# Every timed run (the headline and each variant) warms up for max(--warmup, STEADY_WARMUP)
+# frames right before its timed region: a device idle for >= 100 ms renders its first ~50
+# pipelined frames 10-15% slower (profiles/r02/warm_state/), so a fixed warm-up makes each
+# number independent of what ran before it.  The frames actually run are recorded.
+STEADY_WARMUP = 120
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "Gsamples/sec + fps, 512³ NRRD @ 1080p; achieved HBM GB/s vs peak"
 
@@ -85,8 +101,8 @@ def algorithmic_bytes(stats, voxel_bytes, pixels, out_bytes=4):
             + pixels * out_bytes)
 
 
-def setup_pass(cfg, device):
-    rp = vr_amd.OffscreenPass(cfg["W"], cfg["H"], device=device)
+def setup_pass(cfg, device, device_mask=None):
+    rp = vr_amd.OffscreenPass(cfg["W"], cfg["H"], device=device, device_mask=device_mask)
     if cfg.get("source") == "ct_head":
         # host-generated u8 CT head through the Dataset path (volume_dataset_changed)
         rp.volume_dataset_changed(synth.dataset(synth.ct_head(cfg["dims"][0], cfg["seed"])))
@@ -159,14 +175,33 @@ class NativeFrames:
         self.stream.synchronize()
 
 
-def run_variant(rp, cfg, steps, warmup, rank, world, inflight, row_block=8):
+class GroupFrames:
+    """Frames of a multi-device context (vr_create_mask): each vr_render_device call renders
+    the whole frame across the context's devices into one frame buffer on the caller's stream
+    (the library keeps `frames_in_flight` frames in flight across the devices)."""
+
+    def __init__(self, rp, cam, p, H, W):
+        self.rp, self.cam, self.p = rp, cam, p
+        self.stream = torch.cuda.Stream()
+        self.last = vr_dist.Slot(None, frame=torch.empty((H, W), dtype=torch.int32, device="cuda"))
+
+    def step(self):
+        self.rp.render_device(self.cam, self.p, self.last.frame.data_ptr(), vr_amd.OUT_RGBA8, 8, 0, 1,
+                              self.stream.cuda_stream)
+
+    def drain(self):
+        self.stream.synchronize()
+
+
+def run_variant(rp, cfg, steps, warmup, rank, world, inflight, row_block=8, group=False):
     """Time `steps` frames; returns a dict: secs (max over ranks), kms (this rank's average
     kernel ms), frame (frame work counters), mine (this rank's), shard_px, check (N > 1:
     assembled frame == single-rank frame) and per_rank timings.  For N > 1 a frame is: render
     this rank's row blocks -> RCCL gather to rank 0 -> de-interleave on rank 0.  `inflight`
     frames are in flight (vr_dist.FramePipeline): frame i's work goes to stream i mod
     inflight, so consecutive frames overlap on the device and a frame's gather overlaps the
-    next frames' renders; inflight = 1 is the serial frame loop."""
+    next frames' renders; inflight = 1 is the serial frame loop.  group: rp is a multi-device
+    context (one process, vr_create_mask) that splits and gathers every frame itself."""
     W, H = cfg["W"], cfg["H"]
     cam = synth.camera(cfg["cam"]).to_vr_camera()
     p = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"],
@@ -175,7 +210,7 @@ def run_variant(rp, cfg, steps, warmup, rank, world, inflight, row_block=8):
     if BACKEND != "nccl":
         inflight = 1  # host-staged gloo rehearsal: serial
     slots = []
-    for _ in range(inflight):
+    for _ in range(0 if group else inflight):
         gbuf = frame = None
         if world > 1 and rank == 0:
             # RCCL gathers straight into the rank-major buffer the assembly kernel reads
@@ -193,7 +228,9 @@ def run_variant(rp, cfg, steps, warmup, rank, world, inflight, row_block=8):
     frame_stats = dict(zip(keys, [int(x) for x in tot.tolist()]))
 
     pipe = None
-    if world > 1 and BACKEND == "nccl" and GATHER == "native":
+    if group:
+        pipe = GroupFrames(rp, cam, p, H, W)
+    elif world > 1 and BACKEND == "nccl" and GATHER == "native":
         # the whole frame in the library: render -> ncclGather -> assemble, stream-ordered
         try:
             pipe = NativeFrames(dist_frames(rp, rank, world, row_block, inflight), cam, p, rank, H, W)
@@ -266,7 +303,8 @@ def run_variant(rp, cfg, steps, warmup, rank, world, inflight, row_block=8):
         torch.cuda.synchronize()
         check = bool(torch.equal(full[:H], pipe.last.frame))
     return dict(secs=float(el.item()), kms=kms / max(nl, 1), frame=frame_stats, mine=my_stats,
-                shard_px=sr * W, check=check, per_rank=per_rank)
+                shard_px=sr * W, check=check, per_rank=per_rank, warmup_frames=warmup,
+                last_frame=pipe.last.frame if group else None)
 
 
 def host_cores():
@@ -338,24 +376,46 @@ def cpu_baseline_other(name, device, budget_s, nthreads):
     return r
 
 
-def load_traffic(cfg_name, world, kernel):
+def load_traffic(cfg_name, world, kernel, layout):
     """Measured HBM bytes per frame (rocprofv3 PMC, profiles/pmc_traffic.json written by
-    tools/traffic_json.py from tools/measure_round.sh) for this config, if measured on the
-    kernel this run launches."""
+    tools/traffic_json.py from tools/measure_round.sh) for this config: (bytes, source, status).
+    The entry counts only if it was measured on the kernel this run launches, from the same
+    kernel sources (vr_amd.kernel_source_hash) and the same volume layout; otherwise bytes is
+    None and status says why ("stale: ...")."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
-        return None, None
+        return None, None, "missing: no profiles/pmc_traffic.json"
     try:
-        d = json.load(open(path))
-        e = d.get(cfg_name)
-        if e and int(e.get("n_gpus", 1)) == world and e.get("kernel", kernel) == kernel:
-            return float(e["hbm_bytes_per_launch"]), e.get("source")
-    except Exception:
-        return None, None
-    return None, None
+        e = json.load(open(path)).get(cfg_name)
+    except Exception as ex:
+        return None, None, f"unreadable: {ex}"
+    if not e:
+        return None, None, f"missing: no entry for {cfg_name}"
+    want = dict(n_gpus=world, kernel=kernel, source_hash=vr_amd.kernel_source_hash(), layout=layout)
+    for k, v in want.items():
+        if e.get(k) != v:
+            return None, e.get("source"), f"stale: {k} {e.get(k)!r} != this run's {v!r}"
+    return float(e["hbm_bytes_per_launch"]), e.get("source"), "ok"
+
+
+def fail_exit(msg):
+    print(f"bench: {msg}", file=sys.stderr, flush=True)
+    sys.exit(2)
+
+
+def volume_layout(rp):
+    """The resident layout a PMC traffic entry is keyed on: storage type + bricked bytes."""
+    _, _, st = rp.volume_info()
+    return f"st{st}:{rp.volume_bytes()}"
 
 
 def main():
+    # stdout carries exactly one line, the JSON result (rank 0).  Libraries print banners to
+    # fd 1 on their own (RCCL writes its version block when a communicator is created), so fd
+    # 1 points at stderr for the whole run and is restored only for the result line.
+    sys.stdout.flush()
+    result_fd = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -370,31 +430,63 @@ def main():
                     help="= --frames-in-flight 1: each frame's gather waited for before the next render")
     ap.add_argument("--gather", default="native", choices=("native", "torch"),
                     help="N > 1: the library's RCCL frame path (vr_dist.h) or torch.distributed.gather")
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="GPU_MAX_HW_QUEUES for this process (set before HIP starts; default: the "
+                         "environment's, HIP default 4)")
+    ap.add_argument("--multi-device-context", action="store_true",
+                    help="without WORLD_SIZE: drive the GPUs through vr_create_mask even for --gpus 1 "
+                         "(the default for --gpus > 1)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        fail_exit("--gpus must be >= 1")
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    # How the N GPUs are driven.  torch.distributed.run sets WORLD_SIZE: one process per GPU,
+    # and the launch must match --gpus.  Without it, --gpus N > 1 is ONE process over N devices
+    # (vr_create_mask).  Either way exactly N devices must be there.
+    world_env = os.environ.get("WORLD_SIZE")
+    world = int(world_env) if world_env is not None else 1
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_env is not None and world != args.gpus:
+        fail_exit(f"--gpus {args.gpus} but torch.distributed.run started WORLD_SIZE={world} "
+                  "ranks; they must agree")
+    group = world_env is None and (args.gpus > 1 or args.multi_device_context)
+    ndev = torch.cuda.device_count()
+    global BACKEND, GATHER
     # VR_DIST_BACKEND=gloo rehearses the N > 1 path with ranks sharing devices (host-staged
     # gathers); the real multi-GPU run uses "nccl" (RCCL over xGMI), one device per rank.
-    global BACKEND, GATHER
     BACKEND = os.environ.get("VR_DIST_BACKEND", "nccl")
     GATHER = args.gather
-    device = local_rank % max(1, torch.cuda.device_count())
+    if group:
+        if ndev < args.gpus:
+            fail_exit(f"--gpus {args.gpus} needs {args.gpus} HIP devices in this process; device "
+                      f"{ndev} is not present ({ndev} visible)")
+        device = 0
+    else:
+        if world == 1 and ndev < 1:
+            fail_exit(f"--gpus 1 needs a HIP device; device 0 is not present ({ndev} visible)")
+        if BACKEND == "nccl" and world > 1 and ndev <= local_rank:
+            fail_exit(f"rank {rank} (LOCAL_RANK {local_rank}) has no device: device {local_rank} is "
+                      f"not present ({ndev} visible)")
+        device = local_rank % max(1, ndev)
     torch.cuda.set_device(device)
     if world > 1:
         if BACKEND == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group(BACKEND)
+    n_gpus = args.gpus if group else world
 
     cfg = CONFIGS[args.config]
-    rp = setup_pass(cfg, device)
+    rp = setup_pass(cfg, device, device_mask=((1 << args.gpus) - 1) if group else None)
+    if group and rp.device_mask != (1 << args.gpus) - 1:
+        fail_exit(f"multi-device context spans mask {rp.device_mask:#x}, not {args.gpus} devices")
     vbytes = np.dtype(cfg["dtype"]).itemsize
 
-    inflight = 1 if args.serial_gather else max(1, min(16, args.frames_in_flight))
+    inflight = 1 if args.serial_gather else max(1, min(8 if group else 16, args.frames_in_flight))
     if BACKEND != "nccl":
         inflight = 1
+    warm = max(args.warmup, STEADY_WARMUP)
 
     # also the reference-equivalent sample count (volume.frag as written: no
     # ERT, every in-slab step sampled) of the same frame, per second of this configuration
@@ -406,61 +498,24 @@ def main():
         dist.all_reduce(ref_samples, op=dist.ReduceOp.SUM)
     ref_samples = int(ref_samples.item())
 
-    variants = {}
-    serial_kms = None
-    if not args.no_variants and inflight > 1:
-        # SURVEY.md 8e: the serial form too (one frame at a time; for N > 1 each frame's
-        # gather waited for before the next render).  Its kernels run alone on the device,
-        # so their HIP-event durations are the kernel's own.
-        ns = max(5, args.steps // 2)
-        V = run_variant(rp, cfg, ns, min(args.warmup, 5), rank, world, 1)
-        serial_kms = V["kms"]
-        variants["serial_frames"] = dict(
-            value=round(V["frame"]["samples"] * ns / V["secs"] / 1e9, 3), unit="Gsamples/s",
-            ms_per_step=round(V["secs"] / ns * 1e3, 4), fps=round(ns / V["secs"], 2),
-            kernel_ms=round(V["kms"], 4), frame_check=V["check"])
-    if not args.no_variants and args.config == "c3":
-        # the reference's default camera (SURVEY.md 8d: benchmarks at r=1.6 plus the default)
-        dcfg = CONFIGS["c3_default"]
-        V = run_variant(rp, dcfg, args.steps, VARIANT_WARMUP, rank, world, inflight)
-        # the launch policy picks the kernel per view (vr_api.hip use_pipeline): match the PMC
-        # bytes of the kernel this view ran
-        dkernel = rp.kernel_name(vr_amd.default_params(shading=dcfg["shading"]))
-        dtr, _ = load_traffic("c3_default", world, dkernel)
-        variants["default_camera"] = dict(
-            workload=dcfg["workload"], camera=synth.CAMERAS[dcfg["cam"]],
-            value=round(V["frame"]["samples"] * args.steps / V["secs"] / 1e9, 3), unit="Gsamples/s",
-            ms_per_step=round(V["secs"] / args.steps * 1e3, 4), fps=round(args.steps / V["secs"], 2),
-            samples_per_frame=V["frame"]["samples"], rays_per_frame=V["frame"]["rays"],
-            kernel=dkernel, hbm_bytes_per_frame=dtr,
-            hbm_frac=round(dtr / (V["secs"] / args.steps) / 1e9 / HBM_PEAK_GBS, 4) if dtr else None)
-        vcfg = CONFIGS["c3_ref"]
-        V = run_variant(rp, vcfg, args.steps, VARIANT_WARMUP, rank, world, inflight)
-        rtr, _ = load_traffic("c3_ref", world, rp.kernel_name(vr_amd.default_params(shading=0)))
-        variants["reference_semantics_no_shading_no_ert"] = dict(
-            value=round(V["frame"]["samples"] * args.steps / V["secs"] / 1e9, 3), unit="Gsamples/s",
-            ms_per_step=round(V["secs"] / args.steps * 1e3, 4),
-            fps=round(args.steps / V["secs"], 2), samples_per_frame=V["frame"]["samples"],
-            kernel_ms=round(V["kms"], 4), hbm_bytes_per_frame=rtr,
-            hbm_frac=round(rtr / (V["secs"] / args.steps) / 1e9 / HBM_PEAK_GBS, 4) if rtr else None)
-        # opt-in empty-space skipping (bit-identical frames): executed samples drop, so it is
-        # reported as fps and as reference-equivalent samples/s, never as the headline value
-        scfg = dict(CONFIGS["c3"], skip_empty=1)
-        V = run_variant(rp, scfg, args.steps, VARIANT_WARMUP, rank, world, inflight)
-        f3 = V["frame"]
-        variants["c3_skip_empty"] = dict(
-            fps=round(args.steps / V["secs"], 2), ms_per_step=round(V["secs"] / args.steps * 1e3, 4),
-            kernel_ms=round(V["kms"], 4),
-            executed_gsamples_per_s=round(f3["samples"] * args.steps / V["secs"] / 1e9, 3),
-            reference_equivalent_gsamples_per_s=round(
-                (f3["samples"] + f3["skipped_samples"]) * args.steps / V["secs"] / 1e9, 3),
-            samples_per_frame=f3["samples"], skipped_samples_per_frame=f3["skipped_samples"])
-    # The headline runs after the variants, right after their frames: a
-    # device that sat idle for >= 100 ms renders the first ~50 pipelined frames 10-15% slower
-    # (a power-state ramp that a matmul, an HBM copy or serial frames do not remove;
-    # profiles/r02/warm_state/), so a K = 20 region timed cold measures that ramp, not the march.
-    R = run_variant(rp, cfg, args.steps, args.warmup, rank, world, inflight)
-    secs, kms, fstats, r0stats, shard_px = R["secs"], R["kms"], R["frame"], R["mine"], R["shard_px"]
+    def frame_check(last_frame, vcfg, p):
+        """Multi-device context: the assembled frame == a one-device context's frame, bytes."""
+        one = setup_pass(vcfg, device)
+        try:
+            full = torch.empty((vcfg["H"], vcfg["W"]), dtype=torch.int32, device="cuda")
+            one.render_device(synth.camera(vcfg["cam"]).to_vr_camera(), p, full.data_ptr(),
+                              vr_amd.OUT_RGBA8, 16, 0, 1, torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            return bool(torch.equal(full, last_frame))
+        finally:
+            one.close()
+
+    # The headline first: W (at least STEADY_WARMUP) untimed frames, then exactly K timed ones.
+    R = run_variant(rp, cfg, args.steps, warm, rank, world, inflight, group=group)
+    if group and rank == 0:
+        R["check"] = frame_check(R["last_frame"], cfg, vr_amd.default_params(
+            shading=cfg["shading"], ert_eps=cfg["ert"], frames_in_flight=inflight))
+    secs, kms, fstats = R["secs"], R["kms"], R["frame"]
     frame_s = secs / args.steps
     value = fstats["samples"] * args.steps / secs / 1e9
     fps = args.steps / secs
@@ -468,16 +523,76 @@ def main():
     # the kernel the launch policy picked for the headline's view (vr_kernel_name reads the
     # last frame's view), and the PMC bytes measured for that kernel
     kernel = rp.kernel_name(vr_amd.default_params(shading=cfg["shading"]))
-    traffic, traffic_src = load_traffic(args.config, world, kernel)
+    layout = volume_layout(rp)
+    traffic, traffic_src, traffic_status = load_traffic(args.config, n_gpus, kernel, layout)
+    # compulsory traffic of a frame: every voxel once at the source dtype + the framebuffer
+    compulsory = int(np.prod(cfg["dims"])) * vbytes + cfg["W"] * cfg["H"] * 4
 
-    if not args.no_variants and world == 1:
+    variants = {}
+    serial_kms = None
+    if not args.no_variants and inflight > 1:
+        # SURVEY.md 8e: the serial form too (one frame at a time; for N > 1 each frame's
+        # gather waited for before the next render).  Its kernels run alone on the device,
+        # so their HIP-event durations are the kernel's own.
+        ns = max(5, args.steps // 2)
+        V = run_variant(rp, cfg, ns, warm, rank, world, 1, group=group)
+        serial_kms = V["kms"]
+        variants["serial_frames"] = dict(
+            value=round(V["frame"]["samples"] * ns / V["secs"] / 1e9, 3), unit="Gsamples/s",
+            ms_per_step=round(V["secs"] / ns * 1e3, 4), fps=round(ns / V["secs"], 2),
+            kernel_ms=round(V["kms"], 4), frame_check=V["check"], warmup_frames=V["warmup_frames"])
+    if not args.no_variants and args.config == "c3":
+        # the reference's default camera (SURVEY.md 8d: benchmarks at r=1.6 plus the default)
+        dcfg = CONFIGS["c3_default"]
+        V = run_variant(rp, dcfg, args.steps, warm, rank, world, inflight, group=group)
+        # the launch policy picks the kernel per view (vr_api.hip use_pipeline): match the PMC
+        # bytes of the kernel this view ran
+        dkernel = rp.kernel_name(vr_amd.default_params(shading=dcfg["shading"]))
+        dtr, _, dstatus = load_traffic("c3_default", n_gpus, dkernel, layout)
+        dms = V["secs"] / args.steps
+        variants["default_camera"] = dict(
+            workload=dcfg["workload"], camera=synth.CAMERAS[dcfg["cam"]],
+            value=round(V["frame"]["samples"] * args.steps / V["secs"] / 1e9, 3), unit="Gsamples/s",
+            ms_per_step=round(dms * 1e3, 4), fps=round(args.steps / V["secs"], 2),
+            samples_per_frame=V["frame"]["samples"], rays_per_frame=V["frame"]["rays"],
+            kernel=dkernel, hbm_bytes_per_frame=dtr, traffic_status=dstatus,
+            hbm_frac=round(dtr / dms / 1e9 / HBM_PEAK_GBS, 4) if dtr else None,
+            traffic_over_compulsory=round(dtr / compulsory, 3) if dtr else None,
+            warmup_frames=V["warmup_frames"])
+        vcfg = CONFIGS["c3_ref"]
+        V = run_variant(rp, vcfg, args.steps, warm, rank, world, inflight, group=group)
+        rkernel = rp.kernel_name(vr_amd.default_params(shading=0))
+        rtr, _, rstatus = load_traffic("c3_ref", n_gpus, rkernel, layout)
+        rms = V["secs"] / args.steps
+        variants["reference_semantics_no_shading_no_ert"] = dict(
+            value=round(V["frame"]["samples"] * args.steps / V["secs"] / 1e9, 3), unit="Gsamples/s",
+            ms_per_step=round(rms * 1e3, 4),
+            fps=round(args.steps / V["secs"], 2), samples_per_frame=V["frame"]["samples"],
+            kernel_ms=round(V["kms"], 4), hbm_bytes_per_frame=rtr, traffic_status=rstatus,
+            hbm_frac=round(rtr / rms / 1e9 / HBM_PEAK_GBS, 4) if rtr else None,
+            warmup_frames=V["warmup_frames"])
+        # opt-in empty-space skipping (bit-identical frames): executed samples drop, so it is
+        # reported as fps and as reference-equivalent samples/s, never as the headline value
+        scfg = dict(CONFIGS["c3"], skip_empty=1)
+        V = run_variant(rp, scfg, args.steps, warm, rank, world, inflight, group=group)
+        f3 = V["frame"]
+        variants["c3_skip_empty"] = dict(
+            fps=round(args.steps / V["secs"], 2), ms_per_step=round(V["secs"] / args.steps * 1e3, 4),
+            kernel_ms=round(V["kms"], 4),
+            executed_gsamples_per_s=round(f3["samples"] * args.steps / V["secs"] / 1e9, 3),
+            reference_equivalent_gsamples_per_s=round(
+                (f3["samples"] + f3["skipped_samples"]) * args.steps / V["secs"] / 1e9, 3),
+            samples_per_frame=f3["samples"], skipped_samples_per_frame=f3["skipped_samples"],
+            warmup_frames=V["warmup_frames"])
+
+    if not args.no_variants and world == 1 and not group:
         # PCIe-inclusive: vr_render into (pageable) host memory, the drop-in record() path.
         # The frame's RGBA8 bytes cross PCIe inside the timed region; row bands copy while
         # the later bands render (vr_api.hip vr_render).  Never the headline value.
         hcam = synth.camera(cfg["cam"]).to_vr_camera()
         hp = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"])
         hbuf = np.empty((cfg["H"], cfg["W"], 4), dtype=np.uint8)
-        for _ in range(min(args.warmup, 5)):
+        for _ in range(min(warm, 30)):
             rp.render(hcam, hp, vr_amd.OUT_RGBA8, out=hbuf)
         t0 = time.perf_counter()
         for _ in range(args.steps):
@@ -493,7 +608,7 @@ def main():
     # launching thread of the GPU runs
     cpu = None
     small = int(np.prod(cfg["dims"])) <= 512 ** 3  # the oracle needs the volume as host floats
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and small:
+    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline and small:
         cpu = cpu_baseline(rp, cfg, args.cpu_budget)
         nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
         if nproc and nproc != cpu["cores"]:
@@ -504,20 +619,29 @@ def main():
         cpu["other_configs"] = {n: cpu_baseline_other(n, device, min(4.0, args.cpu_budget), cpu["cores"])
                                 for n in ("c1", "c2")}
 
-
     if rank == 0:
+        if group:
+            parallelism = (f"image 8-row blocks cyclic x{n_gpus} devices in one process "
+                           "(vr_create_mask) + RCCL ncclGather (ncclCommInitAll), stream-ordered")
+        elif world > 1:
+            parallelism = f"image 8-row blocks cyclic x{world} processes" + (
+                " + gloo host-staged gather (rehearsal, ranks share devices)" if BACKEND != "nccl"
+                else " + RCCL ncclGather (vr_dist.h, stream-ordered)" if GATHER == "native"
+                else " + RCCL gather (torch.distributed)")
+        else:
+            parallelism = "one device"
         # Roofline: the kernel is bound by HBM by the SURVEY's classification (a gather, no
         # MFMA).  `achieved` is the MEASURED DRAM traffic of one frame (rocprofv3 PMC
-        # FETCH_SIZE x2 + WRITE_SIZE, same build/config/camera, profiles/pmc_traffic.json) over
-        # this run's frame period, so frac = traffic / ms_per_step / 8 TB/s.  The SURVEY 8d
-        # gather model (8 x sizeof(voxel) per sample + 48 x sizeof(voxel) per shaded sample +
-        # 4 B/pixel) counts L1/L2 hits as well and is reported apart as gather_bytes_frac,
-        # which can exceed 1.
+        # FETCH_SIZE x2 + WRITE_SIZE, same kernel sources/config/camera/layout,
+        # profiles/pmc_traffic.json) over this run's frame period, so frac = traffic /
+        # ms_per_step / 8 TB/s.  The SURVEY 8d gather model (8 x sizeof(voxel) per sample + 48 x
+        # sizeof(voxel) per shaded sample + 4 B/pixel) counts L1/L2 hits as well and is reported
+        # apart as gather_bytes_frac, which can exceed 1.
         out = {
             "metric": METRIC,
             "value": round(value, 3),
             "unit": "Gsamples/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(frame_s * 1e3, 4),
@@ -534,12 +658,10 @@ def main():
                 "viewport": f"{cfg['W']}x{cfg['H']}",
                 "camera": synth.CAMERAS[cfg["cam"]],
                 "tf": cfg["tf"], "shading": cfg["shading"], "ert_eps": cfg["ert"],
-                "parallelism": f"image 8-row blocks cyclic x{world}" + (
-                    (" + gloo host-staged gather (rehearsal, ranks share devices)" if BACKEND != "nccl"
-                     else " + RCCL ncclGather (vr_dist.h, stream-ordered)" if GATHER == "native"
-                     else " + RCCL gather (torch.distributed)")
-                    if world > 1 else "") + f", {inflight} frames in flight",
+                "parallelism": parallelism + f", {inflight} frames in flight",
                 "frames_in_flight": inflight,
+                "hw_queues": HW_QUEUES,
+                "warmup_frames_run": R["warmup_frames"],
                 "samples_per_frame": fstats["samples"],
                 "reference_equivalent_samples_per_frame": ref_samples,
                 "shaded_samples_per_frame": fstats["shaded_samples"],
@@ -554,9 +676,15 @@ def main():
                 "unit": "GB/s",
                 "frac": round(traffic / frame_s / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
                 "traffic": traffic,
+                "traffic_status": traffic_status,
+                "kernel_source_hash": vr_amd.kernel_source_hash(),
+                "volume_layout": layout,
                 "traffic_source": (f"profiles/pmc_traffic.json ({traffic_src}): rocprofv3 --pmc "
                                    "FETCH_SIZE x2 + WRITE_SIZE per frame launch") if traffic else None,
                 "basis": "measured HBM bytes per frame / this run's ms_per_step / 8000 GB/s",
+                "compulsory_bytes": compulsory,
+                "compulsory_basis": "every voxel once at the source dtype + the RGBA8 framebuffer",
+                "traffic_over_compulsory": round(traffic / compulsory, 3) if traffic else None,
                 "kernel_ms": round(kms, 4),
                 "serial_kernel_ms": round(serial_kms, 4) if serial_kms else None,
                 "gather_bytes_per_frame": int(gather_bytes),
@@ -571,7 +699,10 @@ def main():
             "per_rank": R["per_rank"],
             "variants": variants,
         }
+        sys.stdout.flush()
+        os.dup2(result_fd, 1)
         print(json.dumps(out), flush=True)
+        os.dup2(2, 1)
     for d in _DIST.values():
         d.close()
     rp.close()

@@ -32,6 +32,9 @@
 //                                               // (offscreen_pass.cpp:1379-1406)
 //       Sampler get_sampler() const;  ImageView get_image_view() const;
 //     };
+//     static uint32_t device_mask();            // OPTIONAL: the GPUs every frame is split
+//                                               // over (bit d = device d; vr_create_mask);
+//                                               // absent or 0: device 0 alone
 //   };
 //
 // and `using OffscreenPass = Vol::Rendering::Hip::BasicOffscreenPass<Traits>;`.  The HIP
@@ -47,6 +50,7 @@
 
 #include <cstdint>
 #include <functional>
+#include <type_traits>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -102,6 +106,33 @@ struct HeadlessTraits {
     };
 };
 
+// The GPUs a pass renders on: an explicit DeviceMask argument, else Traits::device_mask() when
+// the host's Traits declares it, else device 0.  The reference's construction call
+// (vulkan_context.cpp:51, `new OffscreenPass(this, 100, 100)`) thus stays unchanged while a
+// Traits with device_mask() = 0xFF renders every frame across a node's 8 GPUs.
+struct DeviceMask {
+    uint32_t bits;
+};
+
+namespace detail {
+template <class T, class = void>
+struct has_device_mask : std::false_type {};
+template <class T>
+struct has_device_mask<T, std::void_t<decltype(T::device_mask())>> : std::true_type {};
+template <class T>
+uint32_t traits_device_mask()
+{
+    if constexpr (has_device_mask<T>::value)
+        return (uint32_t)T::device_mask();
+    else
+        return 0u;
+}
+inline vr_ctx *create_ctx(uint32_t mask, int device, uint32_t w, uint32_t h)
+{
+    return mask ? vr_create_mask(mask, w, h) : vr_create(device, w, h);
+}
+}  // namespace detail
+
 template <class Traits>
 class BasicOffscreenPass {
   public:
@@ -110,13 +141,27 @@ class BasicOffscreenPass {
     using Sampler = typename Traits::Sampler;
     using ImageView = typename Traits::ImageView;
 
-    // offscreen_pass.cpp:112-134 (the device is the ctx's: `device`, default 0)
+    // offscreen_pass.cpp:112-134 (the GPUs: Traits::device_mask() if declared, else `device`)
     explicit BasicOffscreenPass(Context *context, uint32_t width, uint32_t height, int device = 0)
-        : ctx_(vr_create(device, width, height)), presenter_(context, width, height),
-          width_(width), height_(height)
+        : ctx_(detail::create_ctx(detail::traits_device_mask<Traits>(), device, width, height)),
+          presenter_(context, width, height), width_(width), height_(height)
     {
         if (!ctx_) throw std::runtime_error(std::string("vr_create: ") + vr_last_error(nullptr));
         vr_params_default(&params_);
+    }
+    // every frame split over the devices of `mask` (vr_create_mask)
+    BasicOffscreenPass(Context *context, uint32_t width, uint32_t height, DeviceMask mask)
+        : ctx_(vr_create_mask(mask.bits, width, height)), presenter_(context, width, height),
+          width_(width), height_(height)
+    {
+        if (!ctx_) throw std::runtime_error(std::string("vr_create_mask: ") + vr_last_error(nullptr));
+        vr_params_default(&params_);
+    }
+    uint32_t device_mask() const
+    {
+        uint32_t m = 0;
+        vr_get_device_mask(ctx_, &m);
+        return m;
     }
     ~BasicOffscreenPass() { vr_destroy(ctx_); }
     BasicOffscreenPass(const BasicOffscreenPass &) = delete;

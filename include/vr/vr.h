@@ -8,15 +8,21 @@
  *
  * Every entry point is `extern "C"`, takes plain pointers and sizes, never throws, and
  * returns 0 on success or a negative errno-style code (VR_E*) on failure; the message of
- * the last failure is available from vr_last_error().  A context is bound to ONE HIP
- * device and is not thread-safe (one host thread per context, as the reference's single
- * render thread).  Multi-GPU runs use one process (and one context) per GPU; see
- * vr_render_device() row-block sharding and vr_assemble_rows().  Volume and TF changes wait
- * for the device first (the reference's vkDeviceWaitIdle before a resource swap), so frames
- * still in flight on any stream finish on the old data.
+ * the last failure is available from vr_last_error().  A context is not thread-safe (one
+ * host thread calls it, as the reference's single render thread).  vr_create binds one HIP
+ * device; vr_create_mask (SURVEY.md §8b `vr_create(int device_mask, ...)`) binds every device
+ * of a mask and renders each frame across them inside the context: the volume, TF and slicing
+ * are replicated on every device, each device ray-marches its 8-row blocks of the frame
+ * (block b -> device b mod N), one RCCL ncclGather per frame collects them on the mask's
+ * lowest device over xGMI, and the frame is assembled there.  The unchanged single-threaded
+ * host thus drives a node of GPUs through the same calls.  (One process per GPU is the other
+ * multi-GPU form: vr_render_device() row-block sharding + vr_dist.h.)  Volume and TF changes
+ * wait for the device(s) first (the reference's vkDeviceWaitIdle before a resource swap), so
+ * frames still in flight on any stream finish on the old data.
  *
  * Mapping to the reference (each function lists the interface it replaces):
- *   vr_create                 OffscreenPass::OffscreenPass(VulkanContext*, w, h)   offscreen_pass.cpp:112-134
+ *   vr_create / vr_create_mask
+ *                             OffscreenPass::OffscreenPass(VulkanContext*, w, h)   offscreen_pass.cpp:112-134
  *   vr_destroy                OffscreenPass::~OffscreenPass()                      offscreen_pass.cpp:136-161
  *   vr_resize                 OffscreenPass::framebuffer_size_changed(w, h)        offscreen_pass.cpp:232-255
  *   vr_set_volume             OffscreenPass::volume_dataset_changed(Dataset&)      offscreen_pass.cpp:257-269
@@ -38,7 +44,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 3
+#define VR_ABI_VERSION 4
 
 /* ---- status codes (negative errno style) ---- */
 #define VR_OK 0
@@ -144,14 +150,24 @@ void vr_params_default(vr_params *p);
  * vr_last_error(NULL)). */
 typedef struct vr_ctx vr_ctx;
 vr_ctx *vr_create(int device, uint32_t width, uint32_t height);
+/* A context over every HIP device of device_mask (bit d = device d), e.g. 0xFF for the 8 GPUs
+ * of a node: same entry points, same results (every frame byte-identical to a one-device
+ * context's), each frame's rows split over the devices (8-row blocks, block-cyclic) and
+ * gathered with RCCL on the lowest device of the mask, which holds vr_render_device's output.
+ * Every device's memory holds a replica of the volume.  NULL with VR_ENODEV (message naming the
+ * missing device) when a device of the mask is not present. */
+vr_ctx *vr_create_mask(uint32_t device_mask, uint32_t width, uint32_t height);
 void vr_destroy(vr_ctx *ctx);
 const char *vr_last_error(const vr_ctx *ctx);
 
 /* framebuffer_size_changed: 0 sizes are ignored (offscreen_pass.cpp:237-239). */
 int vr_resize(vr_ctx *ctx, uint32_t width, uint32_t height);
 int vr_get_size(const vr_ctx *ctx, uint32_t *width, uint32_t *height);
-/* The HIP device index the context renders on (vr_create's `device`). */
+/* The HIP device index the context renders on (vr_create's `device`; for vr_create_mask the
+ * lowest device of the mask, where frames are assembled). */
 int vr_get_device(const vr_ctx *ctx, int *device);
+/* The devices the context renders on (bit d = device d; one bit for vr_create). */
+int vr_get_device_mask(const vr_ctx *ctx, uint32_t *device_mask);
 
 /* ---- inputs (the callee copies; the caller keeps ownership) ---- */
 
@@ -203,7 +219,10 @@ int vr_render(vr_ctx *ctx, const vr_camera *cam, const vr_params *p, void *out,
  * asynchronously.  Image-space sharding for multi-GPU: the frame's rows are cut into
  * blocks of `row_block` rows and block b is rendered by rank (b % nranks); this rank's
  * blocks are written densely, in order, to `out_dev` (vr_shard_rows() rows x W pixels).
- * nranks = 1, rank = 0 renders the whole frame. */
+ * nranks = 1, rank = 0 renders the whole frame.  A vr_create_mask context renders whole frames
+ * only (rank 0 of 1; row_block is ignored), into memory of its lowest device, complete once
+ * `stream` (a stream of that device) passes this point; p->frames_in_flight (1..8) frames may
+ * be in flight across its devices. */
 int vr_render_device(vr_ctx *ctx, const vr_camera *cam, const vr_params *p, void *out_dev,
                      int out_format, uint32_t row_block, uint32_t rank, uint32_t nranks,
                      void *stream);

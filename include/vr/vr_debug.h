@@ -1,0 +1,45 @@
+/*
+ * vr_debug.h — launch-policy overrides for tests and A/B experiments.
+ *
+ * Not part of the drop-in boundary (the reference has no equivalent): the library picks the
+ * march kernel variant, the 8-bit brick layout and the tile order from the volume, the view
+ * and vr_params alone (DESIGN.md §5 "Which kernel a launch runs").  Every variant renders the
+ * same bytes, so these knobs change speed, never results; the GPU tests use them to render
+ * each variant and compare.  The library never reads the process environment, except in
+ * experiment builds (`make EXTRA=-DVR_EXPERIMENTS`), where vr_create() seeds the knobs from
+ * VR_PIPELINE, VR_PAIR, VR_PAIR_LANES, VR_NO_GRAD_FIELD / VR_GRAD_FIELD_ALWAYS, VR_LDS,
+ * VR_U8_LAYOUT and VR_TILE_ORDER_DEFAULT (the names the round-1/2 A/B scripts under tools/
+ * set).
+ */
+#ifndef VR_VR_DEBUG_H
+#define VR_VR_DEBUG_H
+
+#include "vr.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum vr_knob {
+    VR_KNOB_PIPELINE = 1,   /* -1 auto, 0 one sample in flight per ray, 1 pipelined (two)   */
+    VR_KNOB_PAIR = 2,       /* -1 auto, 0 never, 1 lane groups (march_pair_kernel) if legal */
+    VR_KNOB_PAIR_LANES = 3, /* 0 auto, 2 or 4 lanes per ray                                 */
+    VR_KNOB_GRAD_FIELD = 4, /* -1 auto (dense-row views), 0 stencil gradient, 1 the f32
+                               difference field on every view                               */
+    VR_KNOB_LDS = 5,        /* 0 (default) off; 1 keep a linear copy at the next volume
+                               upload and launch the LDS-staged march (march_lds_kernel)   */
+    VR_KNOB_U8_LAYOUT = 6,  /* -1 auto, 0 plain 7x8x8 bricks, 1 yz-quads (next upload)      */
+    VR_KNOB_TILE_ORDER = 7  /* tile order used when vr_params.tile_order == 0: 0 auto (4),
+                               1..4 as vr_params.tile_order                                */
+};
+
+/* Set / read one knob of `ctx` (a multi-device context sets it on every device).
+ * VR_EINVAL for an unknown knob or an out-of-range value. */
+int vr_debug_set_knob(vr_ctx *ctx, int knob, int value);
+int vr_debug_get_knob(const vr_ctx *ctx, int knob, int *value);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VR_VR_DEBUG_H */

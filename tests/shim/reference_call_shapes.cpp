@@ -108,6 +108,14 @@ struct VkTraits {
     using Sampler = VkSampler;
     using ImageView = VkImageView;
     static Vol::Rendering::Hip::Camera camera();  // below: Application::main()...get_camera()
+    // the GPUs every frame is split over (offscreen_pass_hip.hpp): set from argv here, as a
+    // host would from its configuration; 0 = device 0 alone
+    static uint32_t &mask()
+    {
+        static uint32_t m = 0;
+        return m;
+    }
+    static uint32_t device_mask() { return mask(); }
     struct Presenter {
         ImageStandIn color;  // create_color_attachment (offscreen_pass.cpp:290-382)
         std::vector<uint32_t> staging;
@@ -258,8 +266,10 @@ static Vol::Data::Dataset parse_blob()
     return d;
 }
 
-int main()
+int main(int argc, char **argv)
 {
+    if (argc > 2 && std::string(argv[1]) == "--device-mask")
+        VkTraits::mask() = (uint32_t)std::stoul(argv[2], nullptr, 0);
     try {
         Application &app = Application::main();
         app.vulkan_context.reset(new Vol::Rendering::VulkanContext());
@@ -284,8 +294,8 @@ int main()
                           pass->presenter().presents == 2 && pass->get_image().frame == 3;
         uint32_t covered = 0;
         for (uint32_t px : shown.pixels) covered += (px & 0xFFFFFFu) != 0x1C1C1Cu;
-        std::printf("presented %ux%u frames=%u covered=%u match=%d\n", shown.width, shown.height,
-                    pass->presenter().presents, covered, (int)same);
+        std::printf("presented %ux%u frames=%u covered=%u device_mask=0x%x match=%d\n", shown.width,
+                    shown.height, pass->presenter().presents, covered, pass->device_mask(), (int)same);
         return same && covered > 0 ? 0 : 1;
     } catch (std::exception &e) {
         std::fprintf(stderr, "error: %s\n", e.what());

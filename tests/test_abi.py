@@ -25,10 +25,10 @@ def exported():
     return {l.split()[-1] for l in out.splitlines() if " T " in l}
 
 
-@pytest.mark.parametrize("header", ["vr.h", "vr_host.h", "vr_dist.h"])
+@pytest.mark.parametrize("header", ["vr.h", "vr_host.h", "vr_dist.h", "vr_debug.h"])
 def test_every_declared_symbol_is_exported(header):
     names = declared(header)
-    assert len(names) >= 6
+    assert len(names) >= 2
     missing = names - exported()
     assert not missing, missing
 
@@ -37,11 +37,28 @@ def test_binding_lists_cover_headers():
     assert declared("vr.h") == set(vr_amd.ABI_SYMBOLS)
     assert declared("vr_host.h") == set(vr_amd.HOST_SYMBOLS)
     assert declared("vr_dist.h") == set(vr_amd.DIST_SYMBOLS)
+    assert declared("vr_debug.h") == set(vr_amd.DEBUG_SYMBOLS)
+
+
+def test_product_never_reads_the_environment():
+    """Launch-policy overrides go through vr_debug.h knobs; the library reads the process
+    environment only in experiment builds (#ifdef VR_EXPERIMENTS)."""
+    csrc = os.path.join(ROOT, "volumetric-renderer_amd", "csrc")
+    for name in sorted(os.listdir(csrc)):
+        depth, guarded = 0, []
+        for line in open(os.path.join(csrc, name)):
+            s = line.strip()
+            if s.startswith("#if"):
+                guarded.append("VR_EXPERIMENTS" in s)
+            elif s.startswith("#endif") and guarded:
+                guarded.pop()
+            elif "getenv" in s and not any(guarded):
+                raise AssertionError(f"{name}: getenv outside #ifdef VR_EXPERIMENTS: {s}")
 
 
 def test_library_loads_and_pure_entry_points():
     L = vr_amd.lib()
-    assert L.vr_abi_version() == 3
+    assert L.vr_abi_version() == 4
     p = vr_amd.default_params()
     assert p.step == pytest.approx(0.005) and p.ray_dist == pytest.approx(1.8)
     assert list(p.clear_color) == pytest.approx([0.11, 0.11, 0.11, 1.0])
@@ -75,7 +92,7 @@ int main(void) { printf("%zu %zu %zu %zu %zu %zu\n", sizeof(vr_camera), sizeof(v
                                      C.sizeof(vr_amd.vr_stats), vr_amd.vr_params.spec_power.offset,
                                      vr_amd.vr_params.skip_empty.offset,
                                      vr_amd.vr_params.frames_in_flight.offset]
-    assert "VR_ABI_VERSION 3" in src
+    assert "VR_ABI_VERSION 4" in src
 
 
 def test_create_without_device_fails_cleanly():

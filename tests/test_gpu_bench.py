@@ -36,7 +36,26 @@ def test_bench_prints_one_contract_line(gpu):
         # frac is measured bytes over this run's frame period: never above the HBM peak
         assert abs(rf["achieved"] - rf["traffic"] / (d["ms_per_step"] * 1e-3) / 1e9) < 0.01 * rf["achieved"]
         assert rf["frac"] <= 1.0
+    assert rf["traffic_status"] == "ok" or rf["traffic"] is None
+    assert rf["compulsory_bytes"] == 512 ** 3 * 4 + 1920 * 1080 * 4
+    assert d["config"]["hw_queues"] >= 1 and d["config"]["warmup_frames_run"] >= d["warmup"]
     assert d["per_rank"][0]["rank"] == 0
     # the value is executed samples of the whole frame per second
     spf = d["config"]["samples_per_frame"]
     assert abs(d["value"] - spf * d["steps"] / (d["ms_per_step"] * 1e-3 * d["steps"]) / 1e9) < 0.01 * d["value"]
+
+
+def test_bench_multi_device_context_path(gpu):
+    """The single-process multi-GPU path (vr_create_mask) of bench.py, forced at N = 1 on the
+    one-GPU box: one contract line, n_gpus 1, and the assembled frame equals a one-device
+    context's frame (frame_check)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "2",
+                        "--no-cpu-baseline", "--no-variants", "--multi-device-context"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["frame_check"] is True
+    assert "vr_create_mask" in d["config"]["parallelism"]
+    assert d["value"] > 0

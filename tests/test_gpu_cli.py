@@ -30,13 +30,13 @@ def run_cli(*args):
     return r.stdout
 
 
-@pytest.mark.parametrize("skip", [False, True])
-def test_cli_synthetic_matches_ctypes(gpu, tmp_path, skip):
+@pytest.mark.parametrize("skip,mask", [(False, None), (True, None), (False, "0x1")])
+def test_cli_synthetic_matches_ctypes(gpu, tmp_path, skip, mask):
     W, H = 96, 64
     out = str(tmp_path / "f.ppm")
     args = ["synthetic:40", out, "--size", f"{W}x{H}", "--radius", "2", "--rotate", "100,60",
             "--tf", "demo", "--shading"]
-    run_cli(*args, *(["--skip-empty"] if skip else []))
+    run_cli(*args, *(["--skip-empty"] if skip else []), *(["--device-mask", mask] if mask else []))
     img = read_ppm(out)
     rp = vr_amd.OffscreenPass(W, H)
     rp.generate_volume((40, 40, 40), np.float32, seed=2024)

@@ -127,9 +127,9 @@ def test_native_dtypes(rp, np_dtype):
 
 
 @pytest.mark.parametrize("np_dtype", [np.uint8, np.int8])
-def test_byte_layouts_plain_and_quad_identical(rp, monkeypatch, np_dtype):
+def test_byte_layouts_plain_and_quad_identical(rp, np_dtype):
     """8-bit volumes are bricked as yz-quads up to kQuadMaxVoxels voxels and as plain 7x8x8-cell
-    bricks above (vr_internal.h); both layouts, forced through VR_U8_LAYOUT at upload, read
+    bricks above (vr_internal.h); both layouts, forced through the u8_layout knob at upload, read
     back the volume exactly and render the same bytes -- single lane, pipelined, lane pairs,
     shaded (stencil gradient across brick boundaries and the border), skip-empty -- and match
     the oracle."""
@@ -142,13 +142,11 @@ def test_byte_layouts_plain_and_quad_identical(rp, monkeypatch, np_dtype):
     tf = synth.tf_band(0.2, 0.95)
     combos = [dict(shading=0, skip_empty=0), dict(shading=1, skip_empty=0),
               dict(shading=0, skip_empty=1), dict(shading=1, skip_empty=1)]
-    envs = [dict(VR_PIPELINE="0", VR_PAIR="0"), dict(VR_PIPELINE="1", VR_PAIR="0"),
-            dict(VR_PAIR="1", VR_PAIR_LANES="2")]
+    envs = [dict(pipeline=0, pair=0), dict(pipeline=1, pair=0), dict(pair=1, pair_lanes=2)]
     out = {}
     for layout in ("quad", "plain"):
-        monkeypatch.setenv("VR_U8_LAYOUT", layout)
-        rp.volume_dataset_changed(synth.dataset(vol))
-        monkeypatch.delenv("VR_U8_LAYOUT")
+        with rp.knobs(u8_layout=1 if layout == "quad" else 0):
+            rp.volume_dataset_changed(synth.dataset(vol))
         assert ("Quad8" in rp.kernel_name(vr_amd.default_params())) == (layout == "quad")
         rp.transfer_function_changed(tf)
         assert np.array_equal(rp.read_volume(), vol.astype(np.float32)), layout
@@ -156,11 +154,8 @@ def test_byte_layouts_plain_and_quad_identical(rp, monkeypatch, np_dtype):
             cam = synth.camera(camname).to_vr_camera()
             for c in combos:
                 for env in envs if not c["skip_empty"] else envs[:1]:
-                    for k, v in env.items():
-                        monkeypatch.setenv(k, v)
-                    img = rp.render(cam, vr_amd.default_params(ert_eps=1e-4, **c), vr_amd.OUT_RGBA32F)
-                    for k in env:
-                        monkeypatch.delenv(k)
+                    with rp.knobs(**env):
+                        img = rp.render(cam, vr_amd.default_params(ert_eps=1e-4, **c), vr_amd.OUT_RGBA32F)
                     key = (camname, tuple(c.items()), tuple(env.items()))
                     out.setdefault(key, []).append(img)
     for key, (a, b) in out.items():
@@ -171,7 +166,7 @@ def test_byte_layouts_plain_and_quad_identical(rp, monkeypatch, np_dtype):
         p = vr_amd.default_params(shading=shading, ert_eps=1e-4)
         ref, _ = oracle_render(vol.astype(np.float32), ds.vmin, ds.vmax, tf, cam, W, H, p)
         check(out[("rotA", (("shading", shading), ("skip_empty", 0)),
-                   (("VR_PIPELINE", "0"), ("VR_PAIR", "0")))][1], ref)
+                   (("pipeline", 0), ("pair", 0)))][1], ref)
 
 
 def test_row_block_sharding_assembles_exactly(rp):
@@ -454,9 +449,9 @@ def test_work_placement_never_changes_results(rp):
             assert rp.count_work(cam, p) == cw, (order, shape)
 
 
-def test_f32_gradient_field_equals_stencil_gradient(rp, monkeypatch):
+def test_f32_gradient_field_equals_stencil_gradient(rp):
     """Shaded f32 frames read the precomputed difference field; with it disabled
-    (VR_NO_GRAD_FIELD) the kernel forms the same differences from the 4-wide stencil: the
+    (knob grad_field = 0) the kernel forms the same differences from the 4-wide stencil: the
     frames are identical, dense and with empty-space skipping, across brick boundaries and
     the volume border."""
     W, H = 80, 64
@@ -469,12 +464,10 @@ def test_f32_gradient_field_equals_stencil_gradient(rp, monkeypatch):
         for skip in (0, 1):
             p = vr_amd.default_params(shading=1, skip_empty=skip)
             # the field for every view (the launch policy reads it on dense-row views only)
-            monkeypatch.setenv("VR_GRAD_FIELD_ALWAYS", "1")
-            a = rp.render(cam, p, vr_amd.OUT_RGBA32F)
-            monkeypatch.delenv("VR_GRAD_FIELD_ALWAYS")
-            monkeypatch.setenv("VR_NO_GRAD_FIELD", "1")
-            b = rp.render(cam, p, vr_amd.OUT_RGBA32F)
-            monkeypatch.delenv("VR_NO_GRAD_FIELD")
+            with rp.knobs(grad_field=1):
+                a = rp.render(cam, p, vr_amd.OUT_RGBA32F)
+            with rp.knobs(grad_field=0):
+                b = rp.render(cam, p, vr_amd.OUT_RGBA32F)
             assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (camname, skip)
     ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), synth.tf_band(0.2, 0.9), cam,
                            W, H, vr_amd.default_params(shading=1))
@@ -504,10 +497,10 @@ def test_sparse_views_take_the_stencil_gradient(rp):
 
 
 @pytest.mark.parametrize("shading", [0, 1])
-def test_kernel_variants_bit_identical(rp, monkeypatch, shading):
+def test_kernel_variants_bit_identical(rp, shading):
     """Every march kernel a launch can select -- single lane, pipelined (PIPE), lane groups of
     2 and 4 (march_pair_kernel), with and without the f32 difference field -- renders the
-    same bytes and matches the oracle (forced through the A/B environment overrides)."""
+    same bytes and matches the oracle (forced through the vr_debug.h knobs)."""
     W, H = 96, 72
     rp.framebuffer_size_changed(W, H)
     vol = synth.gaussians_numpy((33, 27, 40), seed=17).astype(np.float32)
@@ -516,17 +509,14 @@ def test_kernel_variants_bit_identical(rp, monkeypatch, shading):
     rp.transfer_function_changed(tf)
     cam = synth.camera("fill_oblique").to_vr_camera()
     p = vr_amd.default_params(shading=shading, ert_eps=1e-4)
-    combos = [dict(VR_PIPELINE="0", VR_PAIR="0"), dict(VR_PIPELINE="1", VR_PAIR="0"),
-              dict(VR_PAIR="1", VR_PAIR_LANES="2"), dict(VR_PAIR="1", VR_PAIR_LANES="4"),
-              dict(VR_PAIR="1", VR_PAIR_LANES="4", VR_NO_GRAD_FIELD="1"),
-              dict(VR_PIPELINE="1", VR_PAIR="0", VR_NO_GRAD_FIELD="1")]
+    combos = [dict(pipeline=0, pair=0), dict(pipeline=1, pair=0),
+              dict(pair=1, pair_lanes=2), dict(pair=1, pair_lanes=4),
+              dict(pair=1, pair_lanes=4, grad_field=0),
+              dict(pipeline=1, pair=0, grad_field=0)]
     imgs = []
     for env in combos:
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        imgs.append(rp.render(cam, p, vr_amd.OUT_RGBA32F))
-        for k in env:
-            monkeypatch.delenv(k)
+        with rp.knobs(**env):
+            imgs.append(rp.render(cam, p, vr_amd.OUT_RGBA32F))
     for env, img in zip(combos[1:], imgs[1:]):
         assert np.array_equal(img.view(np.uint32), imgs[0].view(np.uint32)), env
     ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p)
@@ -534,10 +524,10 @@ def test_kernel_variants_bit_identical(rp, monkeypatch, shading):
 
 
 @pytest.mark.parametrize("np_dtype", [np.float32, np.uint8, np.int16])
-def test_lds_staged_kernel_bit_identical(rp, monkeypatch, np_dtype):
-    """The opt-in LDS-staged march (VR_LDS=1 at upload and render: per-stage voxel boxes
+def test_lds_staged_kernel_bit_identical(rp, np_dtype):
+    """The opt-in LDS-staged march (knob lds = 1 at upload and render: per-stage voxel boxes
     DMA'd into LDS from a zero-padded linear copy) renders the bricked gather's bytes, shaded
-    and unshaded; without VR_LDS no linear copy is kept."""
+    and unshaded; without the knob no linear copy is kept."""
     W, H = 88, 70
     rp.framebuffer_size_changed(W, H)
     vol = synth.gaussians_numpy((37, 30, 43), seed=23)
@@ -548,8 +538,8 @@ def test_lds_staged_kernel_bit_identical(rp, monkeypatch, np_dtype):
         vol = vol.astype(np.float32)
     tf = synth.tf_band(0.1, 0.9)
     base_bytes = None
-    for lds in ("0", "1"):
-        monkeypatch.setenv("VR_LDS", lds)
+    for lds in (0, 1):
+        rp.set_knob("lds", lds)
         rp.volume_dataset_changed(synth.dataset(vol))
         rp.transfer_function_changed(tf)
         imgs = []
@@ -560,12 +550,12 @@ def test_lds_staged_kernel_bit_identical(rp, monkeypatch, np_dtype):
                                       vr_amd.OUT_RGBA32F))
         if base_bytes is None:
             base_bytes = imgs
-            assert "lds" not in rp.kernel_name(vr_amd.default_params()), "no linear copy without VR_LDS"
+            assert "lds" not in rp.kernel_name(vr_amd.default_params()), "no linear copy without the knob"
         else:
             assert "lds" in rp.kernel_name(vr_amd.default_params())
             for a, b in zip(base_bytes, imgs):
                 assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), np_dtype
-    monkeypatch.delenv("VR_LDS")
+    rp.set_knob("lds", 0)
     rp.volume_dataset_changed(synth.dataset(vol))  # later tests: no linear copy
 
 

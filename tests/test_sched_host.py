@@ -118,7 +118,7 @@ def _worker(rank, world, port, W, H, rb, inflight, nframes, q):
         dist.destroy_process_group()
 
 
-def _check_order(rank, log, inflight, nframes):
+def _check_order(rank, log, inflight, nframes, consume=True):
     ev = {(OPS[op], fr): (t0, t1) for op, _, fr, t0, t1 in log}
     for i in range(nframes):
         assert ev[("gather", i)][0] >= ev[("render", i)][1], ("gather before render", i)
@@ -131,7 +131,10 @@ def _check_order(rank, log, inflight, nframes):
                 assert ev[("assemble", i)][0] >= ev[("consume", i - 1)][1], ("frame overwritten", i)
         else:
             assert ("assemble", i) not in ev
-            assert ev[("consume", i)][0] >= ev[("gather", i)][1], ("consume before frame done", i)
+            if consume:
+                assert ev[("consume", i)][0] >= ev[("gather", i)][1], ("consume before frame done", i)
+            else:  # a multi-device context's other members: nothing consumes their frames
+                assert ("consume", i) not in ev
         if i >= inflight:  # slot reuse: frame i renders only after frame i-F freed the slot
             freed = ev[("assemble" if rank == 0 else "gather", i - inflight)][1]
             assert ev[("render", i)][0] >= freed, ("slot reused early", i)
@@ -179,3 +182,105 @@ def test_host_schedule_propagates_callback_errors():
     assert lib.vr_sched_host_synchronize(h) == -5
     lib.vr_sched_host_destroy(h)
     assert not lib.vr_sched_host_create(0, 0, cb, None)
+
+
+GCB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_uint64)
+
+
+def _glib():
+    lib = C.CDLL(LIB)
+    lib.vr_group_host_create.restype = C.c_void_p
+    lib.vr_group_host_create.argtypes = [C.c_int, C.c_int, GCB, C.c_void_p]
+    lib.vr_group_host_frame.argtypes = [C.c_void_p]
+    lib.vr_group_host_synchronize.argtypes = [C.c_void_p]
+    lib.vr_group_host_destroy.argtypes = [C.c_void_p]
+    return lib
+
+
+@pytest.mark.parametrize("members,inflight,nframes", [(2, 3, 7), (3, 2, 5), (3, 1, 3), (1, 2, 3)])
+def test_group_schedule_one_process(members, inflight, nframes):
+    """A multi-device context (vr_create_mask) in ONE process: vr_frame_workers.h issues every
+    frame on N members -- member 0 on the calling thread, the others on worker threads -- each
+    member running the same FrameSchedule as vr_dist (vr_dist.cpp group_render).  Here the
+    members' streams are host threads, the render is the CPU oracle on the member's 8-row blocks,
+    the gather a host rendezvous standing in for ncclGather.  Every frame the caller consumes
+    equals the oracle's single-device frame bit for bit, and each member's op log honours the
+    schedule (slot reuse, gather order, assembly after the caller consumed the previous frame)."""
+    import sys
+    for sub in ("volumetric-renderer_amd", "oracle", "tools"):
+        sys.path.insert(0, os.path.join(ROOT, sub))
+    import vr_dist
+    W, H, rb = 36, 41, 8
+    rows = [vr_dist.shard_global_rows(H, rb, m, members) for m in range(members)]
+    sr = len(rows[0])
+    shards = [[np.zeros((sr, W, 4), np.float32) for _ in range(inflight)] for _ in range(members)]
+    gbufs = [np.zeros((members, sr, W, 4), np.float32) for _ in range(inflight)]
+    frame_buf = np.full((H, W, 4), np.nan, np.float32)
+    consumed, errors = [], []
+    logs = [[] for _ in range(members)]
+    cond = threading.Condition()
+    deposits = {}
+    rng = np.random.default_rng(7)
+    delays = rng.uniform(0.0, 0.01, size=(members, nframes, 4))
+
+    def op_fn(_user, m, op, slot, frame):
+        t0 = time.monotonic_ns()
+        try:
+            time.sleep(delays[m, frame, op])
+            if op == 0:
+                r = rows[m]
+                img, _ = _scene(W, H, frame).render_rows(r[r >= 0], nthreads=1)
+                sh = np.zeros((sr, W, 4), np.float32)
+                sh[r >= 0] = img[r[r >= 0]]
+                shards[m][slot][:] = sh
+            elif op == 1:  # the collective: every member's shard to member 0
+                with cond:
+                    deposits[(frame, m)] = shards[m][slot].copy()
+                    cond.notify_all()
+                    if m == 0:
+                        cond.wait_for(lambda: all((frame, k) in deposits for k in range(members)),
+                                      timeout=60)
+                        for k in range(members):
+                            gbufs[slot][k] = deposits.pop((frame, k))
+            elif op == 2:
+                frame_buf[:] = vr_dist.assemble_numpy(gbufs[slot], H, rb, members)
+            elif op == 3:
+                consumed.append((frame, frame_buf.copy()))
+        except Exception as e:  # reported by the test, never across the C boundary
+            errors.append(repr(e))
+            return -5
+        logs[m].append((op, slot, frame, t0, time.monotonic_ns()))
+        return 0
+
+    cb = GCB(op_fn)
+    lib = _glib()
+    g = lib.vr_group_host_create(members, inflight, cb, None)
+    assert g
+    for _ in range(nframes):
+        assert lib.vr_group_host_frame(g) == 0
+    rc = lib.vr_group_host_synchronize(g)
+    lib.vr_group_host_destroy(g)
+    assert rc == 0 and not errors, (rc, errors)
+    for m in range(members):
+        _check_order(m, logs[m], inflight, nframes, consume=(m == 0))
+    assert [f for f, _ in consumed] == list(range(nframes))
+    for k, img in consumed:
+        full, _ = _scene(W, H, k).render()
+        assert np.array_equal(img, full), k
+
+
+def test_group_schedule_reports_member_errors():
+    """A member's failing op surfaces from synchronize (the worker's sticky error), and every
+    member's streams still drain."""
+    lib = _glib()
+
+    def op_fn(_u, m, op, _slot, frame):
+        return -5 if (m == 2 and op == 0 and frame == 1) else 0
+
+    cb = GCB(op_fn)
+    g = lib.vr_group_host_create(3, 2, cb, None)
+    for _ in range(4):
+        assert lib.vr_group_host_frame(g) == 0
+    assert lib.vr_group_host_synchronize(g) == -5
+    lib.vr_group_host_destroy(g)
+    assert not lib.vr_group_host_create(0, 2, cb, None)

@@ -28,8 +28,12 @@ def test_reference_call_shapes_compile_and_link():
 
 
 @pytest.mark.gpu
-def test_reference_call_shapes_present_the_hip_frame(gpu):
+@pytest.mark.parametrize("mask", [None, "0x1"])
+def test_reference_call_shapes_present_the_hip_frame(gpu, mask):
+    """Unchanged call sites; with Traits::device_mask() set the same construction call
+    (vulkan_context.cpp:51) yields a multi-device context (vr_create_mask)."""
     exe = EXE if os.path.exists(EXE) else build()
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    r = subprocess.run([exe] + (["--device-mask", mask] if mask else []), capture_output=True,
+                       text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "match=1" in r.stdout
+    assert "match=1" in r.stdout and "device_mask=0x1" in r.stdout

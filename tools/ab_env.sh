@@ -1,4 +1,7 @@
 #!/bin/bash
+# NOTE (round 3): the VR_* launch-policy variables only act on an experiment build
+# (make -C volumetric-renderer_amd EXTRA=-DVR_EXPERIMENTS LIBDIR=lib_exp BUILDDIR=build_exp, then
+# VR_AMD_LIB=.../lib_exp/libvr_amd.so); the product library reads no environment (vr_debug.h).
 # Per-view A/B of one build under environment settings (e.g. VR_PIPELINE=0 / 1).
 # Usage (GPU box): bash tools/ab_env.sh <tag> "<cfg args>" "ENV=a" "ENV=b" ...
 set -o pipefail

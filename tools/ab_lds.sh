@@ -1,4 +1,7 @@
 #!/bin/bash
+# NOTE (round 3): the VR_* launch-policy variables only act on an experiment build
+# (make -C volumetric-renderer_amd EXTRA=-DVR_EXPERIMENTS LIBDIR=lib_exp BUILDDIR=build_exp, then
+# VR_AMD_LIB=.../lib_exp/libvr_amd.so); the product library reads no environment (vr_debug.h).
 # A/B of the LDS-staged march against the bricked gather kernels on the GPU box: parity suites
 # under VR_LDS=1 first (every frame checked against the oracle), then per-view kernel times of
 # each arm (f32 shaded + ERT, f32 reference semantics, u8 1024^3 @ 2048^2).  Each GPU step has

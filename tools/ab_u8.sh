@@ -1,4 +1,7 @@
 #!/bin/bash
+# NOTE (round 3): the VR_* launch-policy variables only act on an experiment build
+# (make -C volumetric-renderer_amd EXTRA=-DVR_EXPERIMENTS LIBDIR=lib_exp BUILDDIR=build_exp, then
+# VR_AMD_LIB=.../lib_exp/libvr_amd.so); the product library reads no environment (vr_debug.h).
 # 8-bit layout A/B (plain 7x8x8-cell bricks vs yz-quads): GPU tests on the default build, view
 # sweeps of C4 and C2 per library, the pipelined override on C4, C4/C5 bench lines and PMC
 # HBM bytes of a C4 frame.  Usage (GPU box): bash tools/ab_u8.sh <tag> <lib_a> <lib_b>

@@ -1,4 +1,7 @@
 #!/bin/bash
+# NOTE (round 3): the VR_* launch-policy variables only act on an experiment build
+# (make -C volumetric-renderer_amd EXTRA=-DVR_EXPERIMENTS LIBDIR=lib_exp BUILDDIR=build_exp, then
+# VR_AMD_LIB=.../lib_exp/libvr_amd.so); the product library reads no environment (vr_debug.h).
 # Per-view kernel-choice sweep (serial frames, tools/view_sweep.py) over the launch-policy
 # overrides: pipelined / lane-pair (2, 4 lanes per ray) kernels and wavefront shapes.
 # Usage (GPU box): bash tools/knob_sweep.sh <tag> "<view_sweep args>"

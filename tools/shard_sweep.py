@@ -1,4 +1,6 @@
 """Kernel time of ONE rank's share of a frame for N = 1, 2, 4, 8 (GPU; exploration tool).
+# NOTE (round 3): VR_PIPELINE / VR_PAIR only act on an experiment build (make EXTRA=-DVR_EXPERIMENTS,
+# VR_AMD_LIB pointing at it); the product library reads no environment (include/vr/vr_debug.h).
 
 Renders rank 0's row-block shard (vr_render_device with rank 0 of N) of the C3 frame on one
 device and reports the HIP-event kernel time: the per-rank GPU cost under strong scaling,

@@ -60,6 +60,16 @@ def counter(d, name):
     return sum(vals) / len(vals), kernels.most_common(1)[0][0], len(vals)
 
 
+def bench_line(log):
+    """The bench.py JSON line in a pass's log (stdout of the profiled bench.py run)."""
+    if not os.path.exists(log):
+        return None
+    for line in open(log, errors="replace"):
+        if line.startswith('{"metric"'):
+            return json.loads(line)
+    return None
+
+
 def main():
     src = sys.argv[1]
     out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
@@ -69,7 +79,14 @@ def main():
         w, _, _ = counter(os.path.join(src, f"pmc_{cfg}_WRITE_SIZE"), "WRITE_SIZE")
         if f is None:
             continue
-        res[cfg] = dict(n_gpus=1, kernel=kern, dispatches=n, fetch_size_kb=f, write_size_kb=w,
+        # the key bench.py checks before using the entry: the kernel sources and volume layout
+        # the profiled run reported (its own JSON line)
+        b = bench_line(os.path.join(src, f"pmc_{cfg}_FETCH_SIZE.log")) or {}
+        rf = b.get("roofline", {})
+        if rf.get("kernel") and rf["kernel"] != kern:
+            print(f"{cfg}: profiled kernel {kern} != bench's {rf['kernel']}", file=sys.stderr)
+        res[cfg] = dict(n_gpus=1, kernel=kern, source_hash=rf.get("kernel_source_hash"),
+                        layout=rf.get("volume_layout"), dispatches=n, fetch_size_kb=f, write_size_kb=w,
                         hbm_bytes_per_launch=2 * f * 1024 + (w or 0) * 1024,
                         method="rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate runs of "
                                f"bench.py --config {cfg} --no-variants, mean over the frame "

@@ -7,7 +7,9 @@
 // unprojection matrix the kernel's ray setup uses).  No exceptions cross the ABI; HIP errors
 // become negative status codes with a message in vr_last_error().
 #include "../../include/vr/vr.h"
+#include "../../include/vr/vr_debug.h"
 #include "vr_internal.h"
+#include "vr_group.h"
 
 #include <algorithm>
 #include <cmath>
@@ -92,6 +94,18 @@ struct vr_ctx {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
     double timed_ms = 0.0;
     uint64_t timed_launches = 0;
+    // launch-policy overrides for tests and A/B experiments (include/vr/vr_debug.h); the
+    // product path never reads the process environment
+    struct Knobs {
+        int pipeline = -1, pair = -1, pair_lanes = 0, grad_field = -1, lds = 0, u8_layout = -1,
+            tile_order = 0;
+    } knobs;
+    // multi-device context (vr_create_mask): one member context per device of the mask, the
+    // volume/TF/slicing replicated on each, frames rendered across them by `group`
+    std::vector<vr_ctx *> members;
+    vr::Group *group = nullptr;
+    uint32_t device_mask = 0;
+    hipStream_t group_stream = nullptr;  // vr_render's frame stream (device 0)
     std::string err;
 };
 
@@ -298,11 +312,11 @@ struct SplitMix {
 // Brick layout of an nx x ny x nz volume of storage type st (vr_internal.h kQuadFlag): 8-bit
 // volumes of at most kQuadMaxVoxels voxels in yz-quads, larger ones in plain bricks.
 // VR_U8_LAYOUT=quad|plain overrides (A/B, tests).
-int brick_layout(int st, uint32_t nx, uint32_t ny, uint32_t nz)
+int brick_layout(const vr_ctx *c, int st, uint32_t nx, uint32_t ny, uint32_t nz)
 {
     if (!VR_U8_PLAIN || (st != ST_U8 && st != ST_I8)) return st;
     bool quad = (size_t)nx * ny * nz <= kQuadMaxVoxels;
-    if (const char *e = std::getenv("VR_U8_LAYOUT")) quad = e[0] == 'q';
+    if (c->knobs.u8_layout >= 0) quad = c->knobs.u8_layout == 1;
     return quad ? (st | kQuadFlag) : st;
 }
 
@@ -335,10 +349,10 @@ int set_bricks(vr_ctx *c, int storage, uint32_t nx, uint32_t ny, uint32_t nz, vo
 int set_lin(vr_ctx *c, int storage, int src_dtype, const void *src, uint32_t nx, uint32_t ny,
             uint32_t nz, hipStream_t s)
 {
-    // only for the opt-in LDS-staged kernel (VR_LDS=1 at upload): it measured slower than the
-    // bricked gather (profiles/r02/lds_staging), and the copy costs memory and an upload pass
-    const char *want = std::getenv("VR_LDS");
-    if (!want || want[0] != '1') {
+    // only for the opt-in LDS-staged kernel (knob VR_KNOB_LDS = 1 at upload): it measured slower
+    // than the bricked gather (profiles/r02/lds_staging), and the copy costs memory and an
+    // upload pass
+    if (c->knobs.lds != 1) {
         if (c->lin) hipFree(c->lin);
         c->lin = nullptr;
         c->lin_bytes = 0;
@@ -356,13 +370,12 @@ int set_lin(vr_ctx *c, int storage, int src_dtype, const void *src, uint32_t nx,
     return VR_OK;
 }
 
-// LDS-staged march (march_lds_kernel): VR_LDS=1/0 overrides; needs the linear copy, the TF in
-// LDS and no empty-space skipping (that variant keeps the bricked kernels).
+// LDS-staged march (march_lds_kernel): only with knob VR_KNOB_LDS = 1; needs the linear copy,
+// the TF in LDS and no empty-space skipping (that variant keeps the bricked kernels).
 bool use_lds(const vr_ctx *c, const vr_params *p)
 {
     if (!c->lin || p->skip_empty || c->tf_n > 256) return false;
-    if (const char *e = std::getenv("VR_LDS")) return e[0] == '1';
-    return false;
+    return c->knobs.lds == 1;
 }
 
 int upload_tf(vr_ctx *c, const uint32_t *tf, uint32_t n)
@@ -469,12 +482,11 @@ bool view_dense_rows(const double *inv, uint32_t W, uint32_t nx, uint32_t ny, ui
 // ray already holds.  C3, 3 frames in flight, ms per frame (field -> stencil + pipelined;
 // profiles/r02/sparse_view_grad/): default camera r = 3 0.363 -> 0.302, diagonal 0.812 ->
 // 0.770, side 0.600 -> 0.587; the fill view keeps the field (stencil: 0.500 -> 0.565).
-// VR_NO_GRAD_FIELD / VR_GRAD_FIELD_ALWAYS: the stencil / the field for every view (A/B, tests).
+// Knob VR_KNOB_GRAD_FIELD 0 / 1: the stencil / the field for every view (A/B, tests).
 bool use_grad_field(const vr_ctx *c)
 {
     if (c->storage != ST_F32) return false;
-    if (std::getenv("VR_NO_GRAD_FIELD")) return false;
-    if (std::getenv("VR_GRAD_FIELD_ALWAYS")) return true;
+    if (c->knobs.grad_field >= 0) return c->knobs.grad_field == 1;
     return c->dense_rows;
 }
 
@@ -491,10 +503,10 @@ bool use_grad_field(const vr_ctx *c)
 // profiles/r02/kernel_choice/inflight3_pipeline_views*.txt); and for every shaded f32 frame:
 // off the dense-row views they form the gradient from the stencil (use_grad_field), and
 // pipelined that runs 5-8% faster (3 frames in flight: r = 3 0.329 -> 0.306, diagonal
-// 0.812 -> 0.770 ms; profiles/r02/sparse_view_grad/).  VR_PIPELINE=0/1 overrides.
+// 0.812 -> 0.770 ms; profiles/r02/sparse_view_grad/).  Knob VR_KNOB_PIPELINE 0/1 overrides.
 bool use_pipeline(bool shading, uint32_t tiles, const vr_ctx *c)
 {
-    if (const char *e = std::getenv("VR_PIPELINE")) return e[0] == '1';
+    if (c->knobs.pipeline >= 0) return c->knobs.pipeline == 1;
     const size_t voxels = (size_t)c->nx * c->ny * c->nz;
     return tiles * (kThreadsPerTile / 64) < kPipelineMaxWaves ||
            c->brick_bytes >= kPipelineMinBytes || voxels >= kPipelineMinVoxels || c->dense_rows ||
@@ -507,11 +519,11 @@ bool use_pipeline(bool shading, uint32_t tiles, const vr_ctx *c)
 // share: N = 8 0.190 -> 0.153 ms, N = 4 0.270 -> 0.227 ms; the full frame and unshaded shares
 // stay faster single-lane (tools/shard_sweep.py, profiles/r01/multi_gpu/).  Serial frames
 // only (vr_params.frames_in_flight <= 1).  Not for
-// skip-empty frames or TFs beyond the LDS copy.  VR_PAIR=0/1 overrides (A/B).
-bool use_pair(const MarchParams &P, const vr_params *p)
+// skip-empty frames or TFs beyond the LDS copy.  Knob VR_KNOB_PAIR 0/1 overrides (A/B).
+bool use_pair(const vr_ctx *c, const MarchParams &P, const vr_params *p)
 {
     if (p->skip_empty || P.tf_n > 256) return false;
-    if (const char *e = std::getenv("VR_PAIR")) return e[0] == '1';
+    if (c->knobs.pair >= 0) return c->knobs.pair == 1;
     // frames overlapping on the device: the next frame hides this one's tail, so throughput
     // per sample decides and the single-lane kernel wins (N = 8 C3 share with 3 frames in
     // flight: 0.070 against 0.107 ms per frame, tools/inflight_sweep.py)
@@ -577,8 +589,8 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.tiles_x = (c->width + 15) / 16;
     P.tiles_y = (P.local_rows + kMarchRows - 1) / kMarchRows;
     P.tile_order = p->tile_order >= 1 && p->tile_order <= 4 ? (uint32_t)p->tile_order : 4u;
-    if (const char *e = std::getenv("VR_TILE_ORDER_DEFAULT"))  // experiment knob: default order
-        if (p->tile_order == 0 && e[0] >= '1' && e[0] <= '4') P.tile_order = (uint32_t)(e[0] - '0');
+    if (p->tile_order == 0 && c->knobs.tile_order >= 1)  // experiment knob: the default order
+        P.tile_order = (uint32_t)c->knobs.tile_order;
     // wavefront footprint: 1 8x8, 2 16x4, 3 4x16; auto = 16x4 (x-contiguous brick rows:
     // fewer cache lines per wave-level load; measured -11% on the r=3 view, even on others)
     P.wave_w_shift = p->wave_shape == 1 ? 3u : (p->wave_shape == 3 ? 2u : 4u);
@@ -771,6 +783,122 @@ vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P, void *stream, uint32_t 
     return &c->sched.back();
 }
 
+// ---- multi-device contexts (vr_create_mask) ----
+bool is_group(const vr_ctx *c) { return c && c->group; }
+
+// Resource swaps on a multi-device context: every issued frame done on every device first.
+int group_idle(vr_ctx *c)
+{
+    std::string m;
+    if (vr::group_synchronize(c->group, &m) != VR_OK) return fail(c, VR_EIO, m);
+    return VR_OK;
+}
+
+// Member 0 holds the new volume: copy its bricks to every other member over xGMI (device to
+// device, one stream per destination, all in flight together), so each device renders from
+// its own replica (the volume replicated per GPU).
+int replicate_volume(vr_ctx *c)
+{
+    vr_ctx *src = c->members[0];
+    const size_t n = c->members.size();
+    std::vector<hipStream_t> st(n, nullptr);
+    int rc = VR_OK;
+    for (size_t k = 1; k < n && rc == VR_OK; ++k) {
+        vr_ctx *d = c->members[k];
+        if ((rc = wait_idle(d)) != VR_OK) break;
+        void *dst = nullptr;
+        if ((rc = set_bricks(d, src->layout, src->nx, src->ny, src->nz, &dst)) != VR_OK) break;
+        hipError_t e = hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking);
+        if (e == hipSuccess)
+            e = hipMemcpyPeerAsync(dst, d->device, src->bricks, src->device, src->brick_bytes, st[k]);
+        if (e == hipSuccess && src->lin) {  // the LDS-staged kernel's linear copy (knob lds)
+            if (d->lin && d->lin_bytes != src->lin_bytes) {
+                hipFree(d->lin);
+                d->lin = nullptr;
+            }
+            if (!d->lin) e = hipMalloc(&d->lin, src->lin_bytes);
+            d->lin_bytes = src->lin_bytes;
+            if (e == hipSuccess)
+                e = hipMemcpyPeerAsync(d->lin, d->device, src->lin, src->device, src->lin_bytes, st[k]);
+        } else if (e == hipSuccess && d->lin) {
+            hipFree(d->lin);
+            d->lin = nullptr;
+            d->lin_bytes = 0;
+        }
+        if (e != hipSuccess) rc = hip_fail(c, e, "replicate volume (peer copy)");
+        if (rc == VR_OK) {
+            d->storage = src->storage;
+            d->layout = src->layout;
+            d->nx = src->nx;
+            d->ny = src->ny;
+            d->nz = src->nz;
+            d->vmin = src->vmin;
+            d->vmax = src->vmax;
+            d->range_valid = d->dist_valid = d->grad_valid = false;
+        }
+    }
+    for (size_t k = 1; k < n; ++k)
+        if (st[k]) {
+            hipSetDevice(c->members[k]->device);
+            const hipError_t e = hipStreamSynchronize(st[k]);
+            if (e != hipSuccess && rc == VR_OK) rc = hip_fail(c, e, "replicate volume (sync)");
+            hipStreamDestroy(st[k]);
+        }
+    hipSetDevice(c->device);
+    return rc;
+}
+
+// A member's failure reported on the multi-device context.
+int member_rc(vr_ctx *c, vr_ctx *m, int rc)
+{
+    if (rc != VR_OK) c->err = m->err;
+    return rc;
+}
+
+// include/vr/vr_debug.h knobs
+int *knob_slot(vr_ctx *c, int knob)
+{
+    switch (knob) {
+        case VR_KNOB_PIPELINE: return &c->knobs.pipeline;
+        case VR_KNOB_PAIR: return &c->knobs.pair;
+        case VR_KNOB_PAIR_LANES: return &c->knobs.pair_lanes;
+        case VR_KNOB_GRAD_FIELD: return &c->knobs.grad_field;
+        case VR_KNOB_LDS: return &c->knobs.lds;
+        case VR_KNOB_U8_LAYOUT: return &c->knobs.u8_layout;
+        case VR_KNOB_TILE_ORDER: return &c->knobs.tile_order;
+        default: return nullptr;
+    }
+}
+
+bool knob_value_ok(int knob, int v)
+{
+    switch (knob) {
+        case VR_KNOB_PAIR_LANES: return v == 0 || v == 2 || v == 4;
+        case VR_KNOB_LDS: return v == 0 || v == 1;
+        case VR_KNOB_TILE_ORDER: return v >= 0 && v <= 4;
+        default: return v >= -1 && v <= 1;
+    }
+}
+
+#ifdef VR_EXPERIMENTS
+// Experiment builds only: seed the knobs from the A/B scripts' environment variables.
+void knobs_from_env(vr_ctx *c)
+{
+    auto flag = [](const char *name, int &dst) {
+        if (const char *e = std::getenv(name)) dst = e[0] == '1' ? 1 : 0;
+    };
+    flag("VR_PIPELINE", c->knobs.pipeline);
+    flag("VR_PAIR", c->knobs.pair);
+    flag("VR_LDS", c->knobs.lds);
+    if (const char *e = std::getenv("VR_PAIR_LANES")) c->knobs.pair_lanes = e[0] == '4' ? 4 : 2;
+    if (std::getenv("VR_NO_GRAD_FIELD")) c->knobs.grad_field = 0;
+    if (std::getenv("VR_GRAD_FIELD_ALWAYS")) c->knobs.grad_field = 1;
+    if (const char *e = std::getenv("VR_U8_LAYOUT")) c->knobs.u8_layout = e[0] == 'q' ? 1 : 0;
+    if (const char *e = std::getenv("VR_TILE_ORDER_DEFAULT"))
+        if (e[0] >= '1' && e[0] <= '4') c->knobs.tile_order = e[0] - '0';
+}
+#endif
+
 hipEvent_t pooled_event(vr_ctx *c)
 {
     if (!c->ev_pool.empty()) {
@@ -787,6 +915,8 @@ hipEvent_t pooled_event(vr_ctx *c)
 }
 
 }  // namespace
+
+bool vr::is_multi_device(const vr_ctx *c) { return is_group(c); }
 
 extern "C" {
 
@@ -839,6 +969,9 @@ vr_ctx *vr_create(int device, uint32_t width, uint32_t height)
     c->device = device;
     c->width = width;
     c->height = height;
+#ifdef VR_EXPERIMENTS
+    knobs_from_env(c);
+#endif
     if (hipMalloc(&c->counters, 8 * sizeof(unsigned long long)) != hipSuccess) {
         fail(nullptr, VR_ENOMEM, "hipMalloc(counters)");
         delete c;
@@ -856,9 +989,75 @@ vr_ctx *vr_create(int device, uint32_t width, uint32_t height)
     return c;
 }
 
+vr_ctx *vr_create_mask(uint32_t device_mask, uint32_t width, uint32_t height)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        fail(nullptr, VR_ENODEV, "no HIP device available");
+        return nullptr;
+    }
+    if (device_mask == 0) {
+        fail(nullptr, VR_EINVAL, "device_mask is empty");
+        return nullptr;
+    }
+    for (int d = 0; d < 32; ++d)
+        if ((device_mask >> d) & 1u && d >= ndev) {
+            fail(nullptr, VR_ENODEV, "device " + std::to_string(d) + " of device_mask 0x" +
+                                         [&] { char b[16]; std::snprintf(b, sizeof b, "%x", device_mask); return std::string(b); }() +
+                                         " is not present (" + std::to_string(ndev) +
+                                         " HIP device(s) visible)");
+            return nullptr;
+        }
+    if (width == 0 || height == 0) {
+        fail(nullptr, VR_EINVAL, "framebuffer size must be non-zero");
+        return nullptr;
+    }
+    vr_ctx *c = new (std::nothrow) vr_ctx();
+    if (!c) {
+        fail(nullptr, VR_ENOMEM, "out of host memory");
+        return nullptr;
+    }
+    c->device = __builtin_ctz(device_mask);
+    c->device_mask = device_mask;
+    c->width = width;
+    c->height = height;
+#ifdef VR_EXPERIMENTS
+    knobs_from_env(c);
+#endif
+    for (int d = 0; d < 32; ++d) {
+        if (!((device_mask >> d) & 1u)) continue;
+        vr_ctx *m = vr_create(d, width, height);  // the reference constructor's placeholders
+        if (!m) {
+            const std::string e = g_err;
+            vr_destroy(c);
+            fail(nullptr, VR_ENODEV, "device " + std::to_string(d) + ": " + e);
+            return nullptr;
+        }
+        m->knobs = c->knobs;
+        c->members.push_back(m);
+    }
+    std::string err;
+    c->group = vr::group_create(c->members, &err);
+    if (!c->group) {
+        vr_destroy(c);
+        fail(nullptr, VR_ENODEV, "multi-device context: " + err);
+        return nullptr;
+    }
+    hipSetDevice(c->device);
+    return c;
+}
+
 void vr_destroy(vr_ctx *c)
 {
     if (!c) return;
+    if (c->group) vr::group_destroy(c->group);
+    for (vr_ctx *m : c->members) vr_destroy(m);
+    c->members.clear();
+    c->group = nullptr;
+    if (c->group_stream) {
+        hipSetDevice(c->device);
+        hipStreamDestroy(c->group_stream);
+    }
     hipSetDevice(c->device);
     hipDeviceSynchronize();
     for (auto &pr : c->ev_pending) {
@@ -893,6 +1092,11 @@ int vr_resize(vr_ctx *c, uint32_t width, uint32_t height)
 {
     if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
     if (width == 0 || height == 0) return VR_OK;  // offscreen_pass.cpp:237-239
+    if (is_group(c)) {
+        if (int rc = group_idle(c)) return rc;
+        for (vr_ctx *m : c->members)
+            if (int rc = vr_resize(m, width, height)) return member_rc(c, m, rc);
+    }
     c->width = width;
     c->height = height;
     return VR_OK;
@@ -913,6 +1117,13 @@ int vr_get_device(const vr_ctx *c, int *device)
     return VR_OK;
 }
 
+int vr_get_device_mask(const vr_ctx *c, uint32_t *device_mask)
+{
+    if (!c || !device_mask) return fail(nullptr, VR_EINVAL, "NULL argument");
+    *device_mask = is_group(c) ? c->device_mask : (1u << c->device);
+    return VR_OK;
+}
+
 int vr_set_volume_device(vr_ctx *c, const void *data_dev, int dtype, uint32_t nx, uint32_t ny,
                          uint32_t nz, float vmin, float vmax, void *stream)
 {
@@ -922,10 +1133,17 @@ int vr_set_volume_device(vr_ctx *c, const void *data_dev, int dtype, uint32_t nx
     if (st < 0) return fail(c, VR_EINVAL, "unsupported volume dtype");
     if (nx == 0 || ny == 0 || nz == 0) return fail(c, VR_EINVAL, "volume dims must be non-zero");
     if (nx > 65536 || ny > 65536 || nz > 65536) return fail(c, VR_EINVAL, "volume dim > 65536");
+    if (is_group(c)) {  // upload and brick on member 0 (the data's device), then replicate
+        if (int rc = group_idle(c)) return rc;
+        vr_ctx *m0 = c->members[0];
+        if (int rc = vr_set_volume_device(m0, data_dev, dtype, nx, ny, nz, vmin, vmax, stream))
+            return member_rc(c, m0, rc);
+        return replicate_volume(c);
+    }
     int rc = wait_idle(c);
     if (rc) return rc;
     void *dst = nullptr;
-    const int lay = brick_layout(st, nx, ny, nz);
+    const int lay = brick_layout(c, st, nx, ny, nz);
     rc = set_bricks(c, lay, nx, ny, nz, &dst);
     if (rc) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -952,6 +1170,12 @@ int vr_set_volume(vr_ctx *c, const void *data, int dtype, uint32_t nx, uint32_t 
     if (storage_for(dtype) < 0) return fail(c, VR_EINVAL, "unsupported volume dtype");
     if (nx == 0 || ny == 0 || nz == 0) return fail(c, VR_EINVAL, "volume dims must be non-zero");
     if (nx > 65536 || ny > 65536 || nz > 65536) return fail(c, VR_EINVAL, "volume dim > 65536");
+    if (is_group(c)) {
+        if (int rc = group_idle(c)) return rc;
+        vr_ctx *m0 = c->members[0];
+        if (int rc = vr_set_volume(m0, data, dtype, nx, ny, nz, vmin, vmax)) return member_rc(c, m0, rc);
+        return replicate_volume(c);
+    }
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     const size_t bytes = (size_t)nx * ny * nz * dtype_size(dtype);
     void *tmp = nullptr;
@@ -972,6 +1196,13 @@ int vr_generate_volume(vr_ctx *c, int kind, int dtype, uint32_t nx, uint32_t ny,
                        uint32_t seed, float *vmin_out, float *vmax_out)
 {
     if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (is_group(c)) {
+        if (int rc = group_idle(c)) return rc;
+        vr_ctx *m0 = c->members[0];
+        if (int rc = vr_generate_volume(m0, kind, dtype, nx, ny, nz, seed, vmin_out, vmax_out))
+            return member_rc(c, m0, rc);
+        return replicate_volume(c);
+    }
     if (kind != 0) return fail(c, VR_EINVAL, "unknown synthetic volume kind");
     int st;
     float scale;
@@ -1027,7 +1258,7 @@ int vr_generate_volume(vr_ctx *c, int kind, int dtype, uint32_t nx, uint32_t ny,
     }
     const int src_dtype = st == ST_U8 ? VR_DTYPE_U8 : (st == ST_U16 ? VR_DTYPE_U16 : VR_DTYPE_F32);
     void *dst = nullptr;
-    const int lay = brick_layout(st, nx, ny, nz);
+    const int lay = brick_layout(c, st, nx, ny, nz);
     int rc = set_bricks(c, lay, nx, ny, nz, &dst);
     if (rc == VR_OK) {
         e = launch_brick_from_linear(src_dtype, lin, dst, nx, ny, nz, lay, nullptr);
@@ -1057,11 +1288,16 @@ int vr_generate_volume(vr_ctx *c, int kind, int dtype, uint32_t nx, uint32_t ny,
     return VR_OK;
 }
 
-uint64_t vr_volume_bytes(const vr_ctx *c) { return c ? (uint64_t)c->brick_bytes : 0; }
+uint64_t vr_volume_bytes(const vr_ctx *c)
+{
+    if (is_group(c)) return vr_volume_bytes(c->members[0]);  // per device (replicated)
+    return c ? (uint64_t)c->brick_bytes : 0;
+}
 
 int vr_debug_read_volume_native(vr_ctx *c, void *out)
 {
     if (!c || !out) return fail(c, VR_EINVAL, "NULL argument");
+    if (is_group(c)) return member_rc(c, c->members[0], vr_debug_read_volume_native(c->members[0], out));
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     // unbricked on the device in slabs of z-slices (<= 256 MiB of scratch), then copied out
     const size_t vb = storage_size(c->storage), slice = (size_t)c->nx * c->ny * vb;
@@ -1083,6 +1319,7 @@ int vr_debug_read_volume_native(vr_ctx *c, void *out)
 int vr_debug_read_volume(vr_ctx *c, float *out)
 {
     if (!c || !out) return fail(c, VR_EINVAL, "NULL argument");
+    if (is_group(c)) return member_rc(c, c->members[0], vr_debug_read_volume(c->members[0], out));
     const size_t n = (size_t)c->nx * c->ny * c->nz;
     if (c->storage == ST_F32) return vr_debug_read_volume_native(c, out);
     std::vector<unsigned char> host(n * storage_size(c->storage));
@@ -1102,6 +1339,7 @@ int vr_debug_read_volume(vr_ctx *c, float *out)
 int vr_debug_volume_info(const vr_ctx *c, uint32_t dims[3], float minmax[2], int *storage)
 {
     if (!c) return VR_EINVAL;
+    if (is_group(c)) return vr_debug_volume_info(c->members[0], dims, minmax, storage);
     if (dims) {
         dims[0] = c->nx;
         dims[1] = c->ny;
@@ -1120,6 +1358,12 @@ int vr_set_transfer_function(vr_ctx *c, const uint32_t *rgba8_srgb, uint32_t n)
     if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
     if (!rgba8_srgb || n == 0) return fail(c, VR_EINVAL, "transfer function is empty");
     if (n > (1u << 20)) return fail(c, VR_EINVAL, "transfer function too large");
+    if (is_group(c)) {
+        if (int rc = group_idle(c)) return rc;
+        for (vr_ctx *m : c->members)
+            if (int rc = vr_set_transfer_function(m, rgba8_srgb, n)) return member_rc(c, m, rc);
+        return VR_OK;
+    }
     if (int rc = wait_idle(c)) return rc;
     return upload_tf(c, rgba8_srgb, n);
 }
@@ -1128,6 +1372,11 @@ int vr_set_slicing(vr_ctx *c, const float min_slice[3], const float max_slice[3]
 {
     if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
     if (!min_slice || !max_slice) return fail(c, VR_EINVAL, "slice bounds are NULL");
+    if (is_group(c)) {  // frames already issued keep the old box (as the reference's UBO ring)
+        if (int rc = group_idle(c)) return rc;
+        for (vr_ctx *m : c->members)
+            if (int rc = vr_set_slicing(m, min_slice, max_slice)) return member_rc(c, m, rc);
+    }
     for (int a = 0; a < 3; ++a) {
         c->smin[a] = min_slice[a];
         c->smax[a] = max_slice[a];
@@ -1148,6 +1397,20 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
 {
     if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
     if (!out_dev) return fail(c, VR_EINVAL, "output buffer is NULL");
+    if (is_group(c)) {
+        // the whole frame, split over the devices internally (8-row blocks, block-cyclic)
+        if (rank != 0 || nranks != 1)
+            return fail(c, VR_EINVAL, "a multi-device context renders whole frames (rank 0 of 1)");
+        if (!cam) return fail(c, VR_EINVAL, "camera is NULL");
+        if (int rc = check_params(c, p)) return rc;
+        if (out_format != VR_OUT_RGBA8 && out_format != VR_OUT_RGBA32F)
+            return fail(c, VR_EINVAL, "unknown out_format");
+        std::string m;
+        if (int rc = vr::group_render(c->group, cam, p, out_dev, out_format,
+                                      static_cast<hipStream_t>(stream), &m))
+            return fail(c, rc, m);
+        return VR_OK;
+    }
     MarchParams P;
     int rc = build_params(c, cam, p, out_dev, out_format, row_block, rank, nranks, P);
     if (rc) return rc;
@@ -1155,10 +1418,10 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
     hipStream_t s = static_cast<hipStream_t>(stream);
     rc = ensure_derived(c, p, P, s);
     if (rc) return rc;
-    if (!P.lds && use_pair(P, p)) {  // L lanes per ray on 16 x (16 / L) tiles (march_pair_kernel)
+    if (!P.lds && use_pair(c, P, p)) {  // L lanes per ray on 16 x (16 / L) tiles (march_pair_kernel)
         // 4 lanes below kPairQuadMaxWaves (N = 8 C3 share: 0.151 -> 0.144 ms), else 2
         P.pair = P.tiles_x * P.tiles_y * (kThreadsPerTile / 64) < kPairQuadMaxWaves ? 4 : 2;
-        if (const char *e = std::getenv("VR_PAIR_LANES")) P.pair = e[0] == '4' ? 4 : 2;
+        if (c->knobs.pair_lanes == 2 || c->knobs.pair_lanes == 4) P.pair = c->knobs.pair_lanes;
         const uint32_t th = 16 / P.pair;
         P.tiles_y = (P.local_rows + th - 1) / th;
         P.supers_total = P.supers_x * ((P.tiles_y + kSuper - 1) / kSuper);
@@ -1194,6 +1457,26 @@ int vr_render(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out, in
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     const size_t bpp = out_format == VR_OUT_RGBA32F ? 16 : 4;
     const uint32_t W = c->width, H = c->height;
+    if (is_group(c)) {  // the frame across the devices into device 0, then one copy out
+        const size_t fb = (size_t)W * H * bpp;
+        if (c->frame_bytes < fb) {
+            if (c->frame_dev) hipFree(c->frame_dev);
+            c->frame_dev = nullptr;
+            c->frame_bytes = 0;
+            HIP_TRY(c, hipMalloc(&c->frame_dev, fb), "hipMalloc(frame)");
+            c->frame_bytes = fb;
+        }
+        if (!c->group_stream)
+            HIP_TRY(c, hipStreamCreateWithFlags(&c->group_stream, hipStreamNonBlocking),
+                    "hipStreamCreate");
+        int rc = vr_render_device(c, cam, p, c->frame_dev, out_format, vr::kGroupRowBlock, 0, 1,
+                                  c->group_stream);
+        if (rc) return rc;
+        HIP_TRY(c, hipMemcpyAsync(out, c->frame_dev, fb, hipMemcpyDeviceToHost, c->group_stream),
+                "hipMemcpyAsync(frame)");
+        HIP_TRY(c, hipStreamSynchronize(c->group_stream), "hipStreamSynchronize(frame)");
+        return VR_OK;
+    }
     // kHostBands row bands of R rows (a multiple of the 16-row tile): band b is the row shard
     // (row_block R, rank b, nranks kHostBands), rendered densely at rows [b R, b R + R)
     const int nb = H >= kHostBandMinRows ? kHostBands : 1;
@@ -1256,6 +1539,9 @@ int vr_assemble_rows(vr_ctx *c, const void *gathered_dev, void *out_dev, int out
     if (row_block == 0 || nranks == 0) return fail(c, VR_EINVAL, "bad shard");
     if (out_format != VR_OUT_RGBA8 && out_format != VR_OUT_RGBA32F)
         return fail(c, VR_EINVAL, "unknown out_format");
+    if (is_group(c))
+        return member_rc(c, c->members[0], vr_assemble_rows(c->members[0], gathered_dev, out_dev,
+                                                            out_format, row_block, nranks, stream));
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     HIP_TRY(c, launch_assemble(gathered_dev, out_dev, out_format, c->width, c->height, row_block,
                                nranks, vr_shard_rows(c->height, row_block, nranks),
@@ -1269,6 +1555,11 @@ int vr_count_work(vr_ctx *c, const vr_camera *cam, const vr_params *p, uint32_t 
 {
     if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
     if (!out) return fail(c, VR_EINVAL, "stats is NULL");
+    if (is_group(c)) {  // every device holds the same scene: count on member 0
+        if (int rc = group_idle(c)) return rc;
+        return member_rc(c, c->members[0],
+                         vr_count_work(c->members[0], cam, p, row_block, rank, nranks, out));
+    }
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     const size_t bytes = (size_t)c->width * vr_shard_rows(c->height, row_block ? row_block : 1,
                                                           nranks ? nranks : 1) * 4;
@@ -1299,6 +1590,7 @@ int vr_count_work(vr_ctx *c, const vr_camera *cam, const vr_params *p, uint32_t 
 int vr_timing_enable(vr_ctx *c, int enable)
 {
     if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    for (vr_ctx *m : c->members) vr_timing_enable(m, enable);
     c->timing = enable != 0;
     return VR_OK;
 }
@@ -1306,6 +1598,22 @@ int vr_timing_enable(vr_ctx *c, int enable)
 int vr_timing_read(vr_ctx *c, double *total_ms, uint64_t *launches)
 {
     if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (is_group(c)) {  // summed over the devices' launches
+        if (int rc = group_idle(c)) return rc;
+        double ms = 0.0;
+        uint64_t n = 0;
+        for (vr_ctx *m : c->members) {
+            double a = 0.0;
+            uint64_t b = 0;
+            if (int rc = vr_timing_read(m, &a, &b)) return member_rc(c, m, rc);
+            ms += a;
+            n += b;
+        }
+        hipSetDevice(c->device);
+        if (total_ms) *total_ms = ms;
+        if (launches) *launches = n;
+        return VR_OK;
+    }
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     for (auto &pr : c->ev_pending) {
         HIP_TRY(c, hipEventSynchronize(pr.second), "hipEventSynchronize");
@@ -1324,6 +1632,12 @@ int vr_timing_read(vr_ctx *c, double *total_ms, uint64_t *launches)
 
 int vr_timing_reset(vr_ctx *c)
 {
+    if (is_group(c)) {
+        if (int rc = group_idle(c)) return rc;
+        for (vr_ctx *m : c->members)
+            if (int rc = vr_timing_reset(m)) return member_rc(c, m, rc);
+        return VR_OK;
+    }
     double ms;
     uint64_t n;
     int rc = vr_timing_read(c, &ms, &n);
@@ -1336,6 +1650,7 @@ int vr_timing_reset(vr_ctx *c)
 const char *vr_kernel_name(const vr_ctx *c, const vr_params *p)
 {
     if (!c) return "";
+    if (is_group(c)) return vr_kernel_name(c->members[0], p);
     // the variant the next vr_render_device launches (after a shaded frame built the field)
     const bool gf = p && p->shading && use_grad_field(c) && c->grad && c->grad_valid;
     // the full frame (row_block 16, one rank), as vr_render launches it
@@ -1345,6 +1660,26 @@ const char *vr_kernel_name(const vr_ctx *c, const vr_params *p)
     if (p && use_lds(c, p)) return march_lds_kernel_name(c->storage, p->shading != 0);
     return march_kernel_name(c->layout, p && p->shading != 0, false, p && p->skip_empty != 0, gf,
                              pipe);
+}
+
+int vr_debug_set_knob(vr_ctx *c, int knob, int value)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    int *k = knob_slot(c, knob);
+    if (!k) return fail(c, VR_EINVAL, "unknown knob");
+    if (!knob_value_ok(knob, value)) return fail(c, VR_EINVAL, "knob value out of range");
+    *k = value;
+    for (vr_ctx *m : c->members) vr_debug_set_knob(m, knob, value);
+    return VR_OK;
+}
+
+int vr_debug_get_knob(const vr_ctx *c, int knob, int *value)
+{
+    if (!c || !value) return fail(nullptr, VR_EINVAL, "NULL argument");
+    int *k = knob_slot(const_cast<vr_ctx *>(c), knob);
+    if (!k) return fail(nullptr, VR_EINVAL, "unknown knob");
+    *value = *k;
+    return VR_OK;
 }
 
 #ifdef VR_WG_TIMES

@@ -22,6 +22,8 @@
 #include <rccl/rccl.h>
 
 #include "vr_frame_schedule.h"
+#include "vr_frame_workers.h"
+#include "vr_group.h"
 
 #include <cstring>
 #include <new>
@@ -37,6 +39,7 @@ struct Rccl {
     std::string err;
     ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
     ncclResult_t (*comm_init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_init_all)(ncclComm_t *, int, const int *) = nullptr;
     ncclResult_t (*gather)(const void *, void *, size_t, ncclDataType_t, int, ncclComm_t,
                            hipStream_t) = nullptr;
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
@@ -63,9 +66,10 @@ Rccl load_rccl()
     }
     if (!bind(h, "ncclGetUniqueId", r.get_unique_id) ||
         !bind(h, "ncclCommInitRank", r.comm_init_rank) || !bind(h, "ncclGather", r.gather) ||
+        !bind(h, "ncclCommInitAll", r.comm_init_all) ||
         !bind(h, "ncclCommDestroy", r.comm_destroy) ||
         !bind(h, "ncclGetErrorString", r.error_string)) {
-        r.err = "librccl.so.1 lacks ncclGather/ncclCommInitRank/...";
+        r.err = "librccl.so.1 lacks ncclGather/ncclCommInitRank/ncclCommInitAll/...";
         return r;
     }
     r.ok = true;
@@ -79,7 +83,7 @@ Rccl &rccl()
 }
 
 struct Buffers {
-    void *shard = nullptr;  // shard_rows x W RGBA8
+    void *shard = nullptr;  // shard_rows x W pixels (RGBA8, or RGBA32F in multi-device contexts)
     void *gbuf = nullptr;   // rank 0: nranks shards, rank-major
 };
 
@@ -87,6 +91,7 @@ struct Buffers {
 // by vr_dist_timing_read.
 struct TimedOp {
     hipEvent_t t0 = nullptr, t1 = nullptr;
+    bool closed = false;  // t1 recorded
 };
 
 // HIP + RCCL executor of vr::sched::FrameSchedule (members defined below vr_dist).
@@ -109,6 +114,9 @@ struct vr_dist {
     int nranks = 1, rank = 0;
     uint32_t row_block = 8, width = 0, height = 0, shard_rows = 0;
     ncclComm_t comm = nullptr;
+    bool owns_comm = true;  // false: a multi-device context's communicator (vr_group.h)
+    int out_format = VR_OUT_RGBA8;
+    uint32_t words_per_pixel = 1;  // 32-bit words a pixel of out_format takes (gather count)
     std::vector<Buffers> bufs;  // per slot
     vr::sched::FrameSchedule<HipExec> sched;
     const vr_camera *cam = nullptr;  // the frame being issued
@@ -148,10 +156,23 @@ int nccl_check(vr_dist *d, ncclResult_t r, const char *what)
         if (_rc != VR_OK) return _rc; \
     } while (0)
 
-// With timing on, a pair of timing events brackets the op on its stream.
+// With timing on, a pair of timing events brackets the op on its stream.  At most
+// kMaxTimedFrames pairs per op are kept between reads: later frames go untimed (the count
+// vr_dist_timing_read returns is the number actually timed), so timing left on without reads
+// holds a bounded number of events.
+constexpr size_t kMaxTimedFrames = 1u << 16;
+// The op failed after timed_begin: drop its unfinished pair (a later read must not wait on an
+// event that was never recorded).
+void timed_abort(vr_dist *d, std::vector<TimedOp> &v)
+{
+    if (!d->timing || v.empty() || v.back().closed) return;
+    hipEventDestroy(v.back().t0);
+    hipEventDestroy(v.back().t1);
+    v.pop_back();
+}
 int timed_begin(vr_dist *d, std::vector<TimedOp> &v, hipStream_t s)
 {
-    if (!d->timing) return VR_OK;
+    if (!d->timing || v.size() >= kMaxTimedFrames) return VR_OK;
     TimedOp t;
     // timing-only events: no system-scope cache writeback/invalidate when recorded
     DTRY(hip_check(d, hipEventCreateWithFlags(&t.t0, hipEventDisableSystemFence), "hipEventCreate"));
@@ -160,12 +181,21 @@ int timed_begin(vr_dist *d, std::vector<TimedOp> &v, hipStream_t s)
         return dfail(d, VR_EIO, "hipEventCreate");
     }
     v.push_back(t);
-    return hip_check(d, hipEventRecord(t.t0, s), "hipEventRecord");
+    if (hipEventRecord(t.t0, s) != hipSuccess) {
+        timed_abort(d, v);
+        return dfail(d, VR_EIO, "hipEventRecord");
+    }
+    return VR_OK;
 }
 int timed_end(vr_dist *d, std::vector<TimedOp> &v, hipStream_t s)
 {
-    if (!d->timing) return VR_OK;
-    return hip_check(d, hipEventRecord(v.back().t1, s), "hipEventRecord");
+    if (!d->timing || v.empty() || v.back().closed) return VR_OK;
+    v.back().closed = true;
+    if (hipEventRecord(v.back().t1, s) != hipSuccess) {
+        timed_abort(d, v);
+        return dfail(d, VR_EIO, "hipEventRecord");
+    }
+    return VR_OK;
 }
 
 int HipExec::record(Event e, Stream s) { return hip_check(d, hipEventRecord(e, s), "hipEventRecord"); }
@@ -178,23 +208,31 @@ int HipExec::render(int slot, uint64_t, Stream s)
     vr_params q = *d->params;
     q.frames_in_flight = (int32_t)d->sched.slots.size();
     DTRY(timed_begin(d, d->t_render, s));
-    if (vr_render_device(d->ctx, d->cam, &q, d->bufs[slot].shard, VR_OUT_RGBA8, d->row_block,
-                         (uint32_t)d->rank, (uint32_t)d->nranks, s) != VR_OK)
+    if (vr_render_device(d->ctx, d->cam, &q, d->bufs[slot].shard, d->out_format, d->row_block,
+                         (uint32_t)d->rank, (uint32_t)d->nranks, s) != VR_OK) {
+        timed_abort(d, d->t_render);
         return dfail(d, VR_EIO, std::string("render: ") + vr_last_error(d->ctx));
+    }
     return timed_end(d, d->t_render, s);
 }
 int HipExec::gather(int slot, uint64_t, Stream s)
 {
     const Buffers &b = d->bufs[slot];
     DTRY(timed_begin(d, d->t_gather, s));
-    DTRY(nccl_check(d, rccl().gather(b.shard, d->rank == 0 ? b.gbuf : nullptr,
-                                     (size_t)d->shard_rows * d->width, ncclUint32, 0, d->comm, s),
-                    "ncclGather"));
+    const int rc = nccl_check(d, rccl().gather(b.shard, d->rank == 0 ? b.gbuf : nullptr,
+                                               (size_t)d->shard_rows * d->width * d->words_per_pixel,
+                                               ncclUint32, 0,
+                                               d->comm, s),
+                              "ncclGather");
+    if (rc != VR_OK) {
+        timed_abort(d, d->t_gather);
+        return rc;
+    }
     return timed_end(d, d->t_gather, s);
 }
 int HipExec::assemble(int slot, uint64_t, void *frame_dev, Stream s)
 {
-    if (vr_assemble_rows(d->ctx, d->bufs[slot].gbuf, frame_dev, VR_OUT_RGBA8, d->row_block,
+    if (vr_assemble_rows(d->ctx, d->bufs[slot].gbuf, frame_dev, d->out_format, d->row_block,
                          (uint32_t)d->nranks, s) != VR_OK)
         return dfail(d, VR_EIO, std::string("assemble: ") + vr_last_error(d->ctx));
     return VR_OK;
@@ -218,7 +256,7 @@ void release(vr_dist *d)
     for (auto &s : S.slots)
         if (s.stream) hipStreamSynchronize(s.stream);
     if (S.comm) hipStreamSynchronize(S.comm);
-    if (d->comm) rccl().comm_destroy(d->comm);
+    if (d->comm && d->owns_comm) rccl().comm_destroy(d->comm);
     free_timing(d);
     for (auto &b : d->bufs) {
         if (b.shard) hipFree(b.shard);
@@ -235,19 +273,27 @@ void release(vr_dist *d)
     d->bufs.clear();
 }
 
-int setup(vr_dist *d, const void *id, int frames)
+// Join the communicator of `id` (vr_dist_create) or adopt `comm` (multi-device contexts), then
+// allocate the slots.
+int setup(vr_dist *d, const void *id, ncclComm_t comm, int frames)
 {
     DTRY(hip_check(d, hipSetDevice(d->device), "hipSetDevice"));
-    ncclUniqueId uid;
-    static_assert(sizeof(uid) == VR_DIST_ID_BYTES, "ncclUniqueId size");
-    std::memcpy(&uid, id, sizeof(uid));
-    DTRY(nccl_check(d, rccl().comm_init_rank(&d->comm, d->nranks, uid, d->rank), "ncclCommInitRank"));
+    if (comm) {
+        d->comm = comm;
+        d->owns_comm = false;
+    } else {
+        ncclUniqueId uid;
+        static_assert(sizeof(uid) == VR_DIST_ID_BYTES, "ncclUniqueId size");
+        std::memcpy(&uid, id, sizeof(uid));
+        DTRY(nccl_check(d, rccl().comm_init_rank(&d->comm, d->nranks, uid, d->rank),
+                        "ncclCommInitRank"));
+    }
     auto &S = d->sched;
     S.rank = d->rank;
     DTRY(hip_check(d, hipStreamCreateWithFlags(&S.comm, hipStreamNonBlocking),
                    "hipStreamCreate(comm)"));
     DTRY(hip_check(d, hipEventCreateWithFlags(&S.called, hipEventDisableTiming), "hipEventCreate"));
-    const size_t shard_bytes = (size_t)d->shard_rows * d->width * 4;
+    const size_t shard_bytes = (size_t)d->shard_rows * d->width * 4 * d->words_per_pixel;
     S.slots.resize(frames);
     d->bufs.resize(frames);
     for (int k = 0; k < frames; ++k) {
@@ -279,13 +325,13 @@ int vr_dist_unique_id(void *id_out)
     return VR_OK;
 }
 
-vr_dist *vr_dist_create(vr_ctx *ctx, const void *id, int nranks, int rank, uint32_t row_block,
-                        int frames_in_flight)
+}  // extern "C"
+
+namespace {
+
+vr_dist *dist_create(vr_ctx *ctx, const void *id, ncclComm_t comm, int nranks, int rank,
+                     uint32_t row_block, int frames_in_flight, int out_format)
 {
-    if (!ctx || !id) {
-        dfail(nullptr, VR_EINVAL, "ctx or id is NULL");
-        return nullptr;
-    }
     if (nranks < 1 || rank < 0 || rank >= nranks || row_block == 0 || frames_in_flight < 1 ||
         frames_in_flight > 8) {
         dfail(nullptr, VR_EINVAL, "bad nranks/rank/row_block/frames_in_flight");
@@ -304,19 +350,40 @@ vr_dist *vr_dist_create(vr_ctx *ctx, const void *id, int nranks, int rank, uint3
     d->nranks = nranks;
     d->rank = rank;
     d->row_block = row_block;
+    d->out_format = out_format;
+    d->words_per_pixel = out_format == VR_OUT_RGBA32F ? 4 : 1;
     if (vr_get_device(ctx, &d->device) != VR_OK || vr_get_size(ctx, &d->width, &d->height) != VR_OK) {
         dfail(nullptr, VR_EINVAL, "bad ctx");
         delete d;
         return nullptr;
     }
     d->shard_rows = vr_shard_rows(d->height, row_block, (uint32_t)nranks);
-    if (setup(d, id, frames_in_flight) != VR_OK) {
+    if (setup(d, id, comm, frames_in_flight) != VR_OK) {
         g_dist_err = d->err;
         release(d);
         delete d;
         return nullptr;
     }
     return d;
+}
+
+}  // namespace
+
+extern "C" {
+
+vr_dist *vr_dist_create(vr_ctx *ctx, const void *id, int nranks, int rank, uint32_t row_block,
+                        int frames_in_flight)
+{
+    if (!ctx || !id) {
+        dfail(nullptr, VR_EINVAL, "ctx or id is NULL");
+        return nullptr;
+    }
+    if (vr::is_multi_device(ctx)) {
+        dfail(nullptr, VR_EINVAL,
+              "a multi-device context (vr_create_mask) distributes its own frames");
+        return nullptr;
+    }
+    return dist_create(ctx, id, nullptr, nranks, rank, row_block, frames_in_flight, VR_OUT_RGBA8);
 }
 
 int vr_dist_render(vr_dist *d, const vr_camera *cam, const vr_params *p, void *frame_dev,
@@ -360,10 +427,12 @@ int vr_dist_timing_read(vr_dist *d, double *render_ms, double *gather_ms, uint64
     DTRY(vr_dist_synchronize(d));
     double acc[2] = {0.0, 0.0};
     int i = 0;
+    int rc = VR_OK;
     for (auto *v : {&d->t_render, &d->t_gather}) {
         for (auto &t : *v) {
             float ms = 0.0f;
-            DTRY(hip_check(d, hipEventElapsedTime(&ms, t.t0, t.t1), "hipEventElapsedTime"));
+            if (rc == VR_OK)
+                rc = hip_check(d, hipEventElapsedTime(&ms, t.t0, t.t1), "hipEventElapsedTime");
             acc[i] += ms;
         }
         ++i;
@@ -371,8 +440,8 @@ int vr_dist_timing_read(vr_dist *d, double *render_ms, double *gather_ms, uint64
     if (render_ms) *render_ms = acc[0];
     if (gather_ms) *gather_ms = acc[1];
     if (frames) *frames = d->t_render.size();
-    free_timing(d);
-    return VR_OK;
+    free_timing(d);  // on failure too: the record is cleared either way, nothing leaks
+    return rc;
 }
 
 const char *vr_dist_last_error(const vr_dist *d) { return d ? d->err.c_str() : g_dist_err.c_str(); }
@@ -385,3 +454,195 @@ void vr_dist_destroy(vr_dist *d)
 }
 
 }  // extern "C"
+
+// ---- multi-device contexts (vr_create_mask; vr_group.h) ---------------------------------------
+// One process drives every device of the mask.  Member m renders its 8-row blocks of the frame
+// with the slot pipeline above (rank m of N, communicator from ncclCommInitAll), member 0's
+// pipeline gathers and assembles into the caller's frame.  The members' enqueues run on
+// FrameWorkers threads (member 0 on the caller's), each issuing on its own communicator in
+// frame order: NCCL's one-thread-per-device pattern, no ncclGroupStart needed.
+namespace vr {
+
+struct GroupJob {
+    vr_camera cam;
+    vr_params p;
+    void *out = nullptr;            // member 0: the caller's frame
+    hipStream_t stream = nullptr;   // member 0: the caller's stream
+};
+
+struct Group {
+    std::vector<vr_ctx *> members;
+    std::vector<int> devices;
+    std::vector<ncclComm_t> comms;
+    std::vector<vr_dist *> dists;      // per member; rebuilt when the frame shape changes
+    std::vector<hipStream_t> own;      // members 1..: the stream standing in for the caller's
+    uint32_t width = 0, height = 0;
+    int frames = 0, out_format = -1;
+    std::unique_ptr<sched::FrameWorkers<GroupJob>> workers;
+};
+
+namespace {
+
+int member_issue(Group *g, int m, const GroupJob &j, std::string *msg)
+{
+    vr_dist *d = g->dists[m];
+    const int rc = vr_dist_render(d, &j.cam, &j.p, m == 0 ? j.out : nullptr,
+                                  m == 0 ? j.stream : g->own[m]);
+    if (rc && msg) *msg = d->err;
+    return rc;
+}
+
+void free_pipelines(Group *g)
+{
+    g->workers.reset();  // drains the queues and joins the threads
+    for (vr_dist *d : g->dists) {
+        if (!d) continue;
+        release(d);
+        delete d;
+    }
+    g->dists.clear();
+    g->frames = 0;
+    g->out_format = -1;
+}
+
+// The slot pipelines for this frame shape (size, frames in flight, pixel format).
+int ensure_pipelines(Group *g, int frames, int out_format, std::string *err)
+{
+    uint32_t w = 0, h = 0;
+    vr_get_size(g->members[0], &w, &h);
+    if (!g->dists.empty() && g->frames == frames && g->out_format == out_format && g->width == w &&
+        g->height == h)
+        return VR_OK;
+    std::string m;
+    if (g->workers && g->workers->drain(&m) != VR_OK) {
+        *err = m;
+        return VR_EIO;
+    }
+    if (int rc = group_synchronize(g, err)) return rc;
+    free_pipelines(g);
+    const int n = (int)g->members.size();
+    for (int k = 0; k < n; ++k) {
+        vr_dist *d = dist_create(g->members[k], nullptr, g->comms[k], n, k, kGroupRowBlock, frames,
+                                 out_format);
+        if (!d) {
+            *err = g_dist_err;
+            free_pipelines(g);
+            return VR_EIO;
+        }
+        g->dists.push_back(d);
+    }
+    g->width = w;
+    g->height = h;
+    g->frames = frames;
+    g->out_format = out_format;
+    g->workers.reset(new sched::FrameWorkers<GroupJob>(
+        n, [g](int m, const GroupJob &j, std::string *msg) { return member_issue(g, m, j, msg); },
+        [g](int m) { hipSetDevice(g->devices[m]); }));
+    return VR_OK;
+}
+
+}  // namespace
+
+Group *group_create(const std::vector<vr_ctx *> &members, std::string *err)
+{
+    if (members.empty()) {
+        *err = "no devices";
+        return nullptr;
+    }
+    if (!rccl().ok) {
+        *err = rccl().err;
+        return nullptr;
+    }
+    std::unique_ptr<Group> g(new (std::nothrow) Group());
+    if (!g) {
+        *err = "out of host memory";
+        return nullptr;
+    }
+    g->members = members;
+    for (vr_ctx *c : members) {
+        int dev = -1;
+        vr_get_device(c, &dev);
+        g->devices.push_back(dev);
+    }
+    g->comms.assign(members.size(), nullptr);
+    const ncclResult_t r =
+        rccl().comm_init_all(g->comms.data(), (int)members.size(), g->devices.data());
+    if (r != ncclSuccess) {
+        *err = std::string("ncclCommInitAll: ") + rccl().error_string(r);
+        return nullptr;
+    }
+    g->own.assign(members.size(), nullptr);
+    for (size_t m = 1; m < members.size(); ++m) {
+        hipSetDevice(g->devices[m]);
+        if (hipStreamCreateWithFlags(&g->own[m], hipStreamNonBlocking) != hipSuccess) {
+            *err = "hipStreamCreate";
+            Group *raw = g.release();
+            group_destroy(raw);
+            return nullptr;
+        }
+    }
+    hipSetDevice(g->devices[0]);
+    return g.release();
+}
+
+int group_drain(Group *g, std::string *err)
+{
+    if (!g->workers) return VR_OK;
+    return g->workers->drain(err) == 0 ? VR_OK : VR_EIO;
+}
+
+int group_synchronize(Group *g, std::string *err)
+{
+    if (int rc = group_drain(g, err)) return rc;
+    for (vr_dist *d : g->dists)
+        if (vr_dist_synchronize(d) != VR_OK) {
+            *err = d->err;
+            return VR_EIO;
+        }
+    for (size_t m = 1; m < g->own.size(); ++m)
+        if (g->own[m]) {
+            hipSetDevice(g->devices[m]);
+            if (hipStreamSynchronize(g->own[m]) != hipSuccess) {
+                *err = "hipStreamSynchronize";
+                return VR_EIO;
+            }
+        }
+    hipSetDevice(g->devices[0]);
+    return VR_OK;
+}
+
+void group_destroy(Group *g)
+{
+    if (!g) return;
+    std::string ignored;
+    group_synchronize(g, &ignored);
+    free_pipelines(g);
+    for (size_t m = 0; m < g->comms.size(); ++m)
+        if (g->comms[m]) {
+            hipSetDevice(g->devices[m]);
+            rccl().comm_destroy(g->comms[m]);
+        }
+    for (size_t m = 1; m < g->own.size(); ++m)
+        if (g->own[m]) {
+            hipSetDevice(g->devices[m]);
+            hipStreamDestroy(g->own[m]);
+        }
+    if (!g->devices.empty()) hipSetDevice(g->devices[0]);
+    delete g;
+}
+
+int group_render(Group *g, const vr_camera *cam, const vr_params *p, void *out_dev,
+                 int out_format, hipStream_t stream, std::string *err)
+{
+    const int frames = p->frames_in_flight < 1 ? 1 : (p->frames_in_flight > 8 ? 8 : p->frames_in_flight);
+    if (int rc = ensure_pipelines(g, frames, out_format, err)) return rc;
+    GroupJob j;
+    j.cam = *cam;
+    j.p = *p;
+    j.out = out_dev;
+    j.stream = stream;
+    const int rc = g->workers->issue(j, err);
+    return rc == 0 ? VR_OK : (rc < 0 ? rc : VR_EIO);
+}
+
+}  // namespace vr

@@ -1,0 +1,42 @@
+// vr_group.h — internal: the frame path of a multi-device context (vr_create_mask, vr.h).
+//
+// vr_api.hip owns the member contexts (one vr_ctx per device, the volume/TF/slicing replicated
+// on each); this part (vr_dist.cpp) owns what a frame needs across them: one RCCL communicator
+// per member from ncclCommInitAll, the per-member slot pipelines of vr_dist (render this
+// member's 8-row blocks -> ncclGather to member 0 -> assemble there, stream-ordered), and the
+// frame workers (vr_frame_workers.h) that enqueue every member's part in parallel.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/vr/vr.h"
+
+namespace vr {
+
+struct Group;
+
+// Rows per block of the block-cyclic split (block b -> member b mod N), as SURVEY.md §8e.
+constexpr uint32_t kGroupRowBlock = 8;
+
+// True for a vr_create_mask context (vr_api.hip).
+bool is_multi_device(const vr_ctx *c);
+
+// The communicators over the members' devices (one member per device, member 0 = the frame's
+// device).  nullptr on failure (*err says why).
+Group *group_create(const std::vector<vr_ctx *> &members, std::string *err);
+// Waits for every frame issued so far (enqueue and device work), then frees the pipelines and
+// communicators; the member contexts stay.
+void group_destroy(Group *g);
+// Waits until every member has enqueued every frame issued so far (not for the device).
+int group_drain(Group *g, std::string *err);
+// Waits for every frame issued so far on the devices as well.
+int group_synchronize(Group *g, std::string *err);
+// One frame across the members into out_dev (member 0's device, W*H pixels of out_format),
+// complete once `stream` passes this point (the vr_dist_render contract).
+int group_render(Group *g, const vr_camera *cam, const vr_params *p, void *out_dev,
+                 int out_format, hipStream_t stream, std::string *err);
+
+}  // namespace vr

@@ -8,6 +8,11 @@
 // shards, torch.distributed.gather over gloo, numpy assembly, a frame check).  It lets the
 // world-size-2 CPU test (tests/test_sched_host.py) drive the exact slot/stream/event order a
 // multi-GPU frame uses, without a GPU.  Built by g++ into lib/libvr_sched_host.so.
+//
+// vr_group_host_* does the same for a multi-device context (vr_create_mask): N members in one
+// process, each with its own FrameSchedule, issued by the same vr::sched::FrameWorkers
+// (vr_frame_workers.h: member 0 on the calling thread, the others on worker threads) that
+// vr_dist.cpp's group_render uses.
 #include <stdint.h>
 
 #include <condition_variable>
@@ -20,6 +25,7 @@
 #include <vector>
 
 #include "vr_frame_schedule.h"
+#include "vr_frame_workers.h"
 
 namespace {
 
@@ -221,5 +227,90 @@ int vr_sched_host_frame(vr_sched_host *h)
 int vr_sched_host_synchronize(vr_sched_host *h) { return h ? h->sync() : -22; }
 
 void vr_sched_host_destroy(vr_sched_host *h) { delete h; }
+
+// ---- multi-device context on host threads ----
+typedef int (*vr_group_op_fn)(void *user, int member, int op, int slot, uint64_t frame);
+
+struct vr_group_host;
+struct GroupMember {
+    vr_group_host *g = nullptr;
+    int member = 0;
+};
+
+struct vr_group_host {
+    vr_group_op_fn fn = nullptr;
+    void *user = nullptr;
+    std::vector<std::unique_ptr<GroupMember>> tags;
+    std::vector<vr_sched_host *> members;
+    std::unique_ptr<vr::sched::FrameWorkers<uint64_t>> workers;
+    ~vr_group_host()
+    {
+        workers.reset();
+        for (auto *m : members) delete m;
+    }
+};
+
+static int group_member_op(void *user, int op, int slot, uint64_t frame)
+{
+    GroupMember *t = static_cast<GroupMember *>(user);
+    return t->g->fn(t->g->user, t->member, op, slot, frame);
+}
+
+// One frame on member m (rank m of the members): the schedule, plus (member 0) the caller's
+// consume of the assembled frame.
+static int group_member_frame(vr_group_host *g, int m)
+{
+    vr_sched_host *h = g->members[m];
+    const uint64_t frame = h->sched.frame;
+    int rc = h->sched.issue(h->x, h->caller, nullptr);
+    if (rc || m != 0) return rc;
+    return h->x.call(h->caller, OP_CONSUME, (int)(frame % h->sched.slots.size()), frame);
+}
+
+// fn(user, member, op, slot, frame) as vr_sched_host's, with the member index (= its rank).
+vr_group_host *vr_group_host_create(int members, int frames_in_flight, vr_group_op_fn fn, void *user)
+{
+    if (members < 1 || members > 32 || frames_in_flight < 1 || frames_in_flight > 8 || !fn)
+        return nullptr;
+    vr_group_host *g = new (std::nothrow) vr_group_host();
+    if (!g) return nullptr;
+    g->fn = fn;
+    g->user = user;
+    for (int m = 0; m < members; ++m) {
+        g->tags.emplace_back(new GroupMember{g, m});
+        vr_sched_host *h = vr_sched_host_create(m, frames_in_flight, group_member_op, g->tags.back().get());
+        if (!h) {
+            delete g;
+            return nullptr;
+        }
+        g->members.push_back(h);
+    }
+    g->workers.reset(new vr::sched::FrameWorkers<uint64_t>(
+        members, [g](int m, const uint64_t &, std::string *) { return group_member_frame(g, m); },
+        nullptr));
+    return g;
+}
+
+int vr_group_host_frame(vr_group_host *g)
+{
+    if (!g) return -22;
+    std::string msg;
+    return g->workers->issue(0, &msg);
+}
+
+// Waits until every member has issued and run every op so far; the first failure, else 0.
+int vr_group_host_synchronize(vr_group_host *g)
+{
+    if (!g) return -22;
+    std::string msg;
+    int rc = g->workers->drain(&msg);
+    for (auto *m : g->members) {
+        const int r = m->sync();
+        if (r && !rc) rc = r;
+    }
+    return rc;
+}
+
+void vr_group_host_destroy(vr_group_host *g) { delete g; }
 
 }  // extern "C"

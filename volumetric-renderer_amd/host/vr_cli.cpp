@@ -8,7 +8,7 @@
 //
 //   vr_cli <file.nhdr|file.nrrd|synthetic:N> <out.ppm> [--size WxH] [--radius R]
 //          [--rotate DX,DY] [--tf default|demo] [--shading] [--ert EPS] [--skip-empty]
-//          [--frames K]
+//          [--frames K] [--device-mask M]   (M: render every frame across these GPUs)
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -24,7 +24,7 @@ int main(int argc, char **argv)
     if (argc < 3) {
         std::fprintf(stderr, "usage: %s <file.nhdr|synthetic:N> <out.ppm> [--size WxH] [--radius R] "
                              "[--rotate DX,DY] [--tf default|demo] [--shading] [--ert EPS] [--skip-empty] "
-                             "[--frames K]\n",
+                             "[--frames K] [--device-mask M]\n",
                      argv[0]);
         return 2;
     }
@@ -32,6 +32,7 @@ int main(int argc, char **argv)
     uint32_t W = 800, H = 600;
     float radius = 3.0f, rx = 0.0f, ry = 0.0f, ert = 0.0f;
     int shading = 0, skip_empty = 0, frames = 1;
+    uint32_t mask = 0;
     std::string tfname = "default";
     for (int i = 3; i < argc; ++i) {
         std::string a = argv[i];
@@ -43,13 +44,16 @@ int main(int argc, char **argv)
         else if (a == "--skip-empty") skip_empty = 1;
         else if (a == "--ert" && i + 1 < argc) ert = std::strtof(argv[++i], nullptr);
         else if (a == "--frames" && i + 1 < argc) frames = std::atoi(argv[++i]);
+        else if (a == "--device-mask" && i + 1 < argc) mask = (uint32_t)std::strtoul(argv[++i], nullptr, 0);
         else {
             std::fprintf(stderr, "unknown argument %s\n", a.c_str());
             return 2;
         }
     }
     try {
-        Vol::Rendering::Hip::OffscreenPass pass(W, H);
+        Vol::Rendering::Hip::OffscreenPass pass = mask ? Vol::Rendering::Hip::OffscreenPass(
+                                                             nullptr, W, H, Vol::Rendering::Hip::DeviceMask{mask})
+                                                       : Vol::Rendering::Hip::OffscreenPass(W, H);
         if (src.rfind("synthetic:", 0) == 0) {
             const uint32_t n = (uint32_t)std::atoi(src.c_str() + 10);
             float lo, hi;

@@ -9,6 +9,7 @@ raises at import-time use, and every render goes through the HIP kernels.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 from dataclasses import dataclass
@@ -69,6 +70,7 @@ class vr_dataset(C.Structure):
 # Every entry point include/vr/vr.h and include/vr/vr_host.h declare (checked by the CPU tests).
 ABI_SYMBOLS = [
     "vr_abi_version", "vr_params_default", "vr_create", "vr_destroy", "vr_last_error",
+    "vr_create_mask", "vr_get_device_mask",
     "vr_resize", "vr_get_size", "vr_get_device", "vr_set_volume", "vr_set_volume_device", "vr_generate_volume",
     "vr_volume_bytes", "vr_debug_read_volume", "vr_debug_read_volume_native", "vr_debug_volume_info",
     "vr_set_transfer_function", "vr_set_slicing", "vr_render", "vr_render_device",
@@ -90,8 +92,14 @@ DIST_SYMBOLS = [
     "vr_dist_last_error", "vr_dist_destroy", "vr_dist_timing_enable", "vr_dist_timing_read",
 ]
 DIST_ID_BYTES = 128  # include/vr/vr_dist.h VR_DIST_ID_BYTES
+DEBUG_SYMBOLS = ["vr_debug_set_knob", "vr_debug_get_knob"]
+# include/vr/vr_debug.h enum vr_knob (launch-policy overrides: speed only, never results)
+KNOBS = {"pipeline": 1, "pair": 2, "pair_lanes": 3, "grad_field": 4, "lds": 5, "u8_layout": 6,
+         "tile_order": 7}
+KNOB_AUTO = {"pipeline": -1, "pair": -1, "pair_lanes": 0, "grad_field": -1, "lds": 0,
+             "u8_layout": -1, "tile_order": 0}
 
-ABI_VERSION = 3  # include/vr/vr.h VR_ABI_VERSION
+ABI_VERSION = 4  # include/vr/vr.h VR_ABI_VERSION
 _LIB = None
 
 
@@ -123,6 +131,8 @@ def lib() -> C.CDLL:
         "vr_resize": (i32, [vp, u32, u32]),
         "vr_get_size": (i32, [vp, C.POINTER(u32), C.POINTER(u32)]),
         "vr_get_device": (i32, [vp, C.POINTER(i32)]),
+        "vr_create_mask": (vp, [u32, u32, u32]),
+        "vr_get_device_mask": (i32, [vp, C.POINTER(u32)]),
         "vr_dist_unique_id": (i32, [vp]),
         "vr_dist_create": (vp, [vp, vp, i32, i32, u32, i32]),
         "vr_dist_render": (i32, [vp, C.POINTER(vr_camera), C.POINTER(vr_params), vp, vp]),
@@ -150,6 +160,8 @@ def lib() -> C.CDLL:
         "vr_timing_read": (i32, [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
         "vr_timing_reset": (i32, [vp]),
         "vr_kernel_name": (C.c_char_p, [vp, C.POINTER(vr_params)]),
+        "vr_debug_set_knob": (i32, [vp, i32, i32]),
+        "vr_debug_get_knob": (i32, [vp, i32, C.POINTER(i32)]),
         "vr_cam_init": (None, [C.POINTER(vr_orbit_camera)]),
         "vr_cam_rotate": (None, [C.POINTER(vr_orbit_camera), f32, f32]),
         "vr_cam_zoom": (None, [C.POINTER(vr_orbit_camera), f32]),
@@ -345,11 +357,18 @@ def write_nrrd_raw(nhdr_path: str, data: np.ndarray) -> None:
 class OffscreenPass:
     """Mirror of Vol::Rendering::OffscreenPass (offscreen_pass.h:40-54) over the C ABI."""
 
-    def __init__(self, width: int, height: int, device: int = 0):
+    def __init__(self, width: int, height: int, device: int = 0, device_mask: Optional[int] = None):
+        """device: the HIP device (vr_create); device_mask: render every frame across these
+        devices instead (vr_create_mask, bit d = device d)."""
         L = lib()
-        self._ctx = L.vr_create(device, width, height)
+        if device_mask is None:
+            self._ctx = L.vr_create(device, width, height)
+            what = "vr_create"
+        else:
+            self._ctx = L.vr_create_mask(device_mask, width, height)
+            what = "vr_create_mask"
         if not self._ctx:
-            raise RuntimeError(f"vr_create failed: {L.vr_last_error(None).decode()}")
+            raise RuntimeError(f"{what} failed: {L.vr_last_error(None).decode()}")
 
     # -- lifecycle --
     def close(self):
@@ -366,6 +385,12 @@ class OffscreenPass:
     def _check(self, rc: int, what: str):
         if rc != 0:
             raise RuntimeError(f"{what} failed ({rc}): {lib().vr_last_error(self._ctx).decode()}")
+
+    @property
+    def device_mask(self) -> int:
+        m = C.c_uint32()
+        self._check(lib().vr_get_device_mask(self._ctx, C.byref(m)), "vr_get_device_mask")
+        return int(m.value)
 
     @property
     def size(self):
@@ -486,6 +511,26 @@ class OffscreenPass:
     def kernel_name(self, params) -> str:
         return lib().vr_kernel_name(self._ctx, C.byref(params)).decode()
 
+    # -- include/vr/vr_debug.h: launch-policy overrides for tests (speed only, never results) --
+    def set_knob(self, name: str, value: int):
+        self._check(lib().vr_debug_set_knob(self._ctx, KNOBS[name], int(value)), f"set_knob({name})")
+
+    def get_knob(self, name: str) -> int:
+        v = C.c_int()
+        self._check(lib().vr_debug_get_knob(self._ctx, KNOBS[name], C.byref(v)), f"get_knob({name})")
+        return int(v.value)
+
+    @contextlib.contextmanager
+    def knobs(self, **kw):
+        """Set knobs for the duration of a with-block (auto values restored after)."""
+        for k, v in kw.items():
+            self.set_knob(k, v)
+        try:
+            yield self
+        finally:
+            for k in kw:
+                self.set_knob(k, KNOB_AUTO[k])
+
 
 def dist_unique_id() -> bytes:
     """Rank 0: a fresh RCCL communicator id (vr_dist_unique_id) to send to every rank."""
@@ -549,6 +594,20 @@ class DistFrames:
             self.close()
         except Exception:
             pass
+
+
+KERNEL_SOURCES = ("csrc/vr_kernels.hip", "csrc/vr_internal.h", "csrc/vr_exact_math.h")
+
+
+def kernel_source_hash() -> str:
+    """sha256 (16 hex digits) of the kernel sources: keys measured per-kernel figures (the PMC
+    traffic bench.py's roofline reads) to the code they were measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(HERE, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def shard_rows(height: int, row_block: int, nranks: int) -> int:
