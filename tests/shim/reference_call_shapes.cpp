@@ -266,10 +266,86 @@ static Vol::Data::Dataset parse_blob()
     return d;
 }
 
+// An 8-bit scan as the reference's loader hands it over: NrrdFileParser::convert makes every
+// voxel a float (nrrd_file_parser.cpp:49-77), here integers 0..255.
+static std::vector<uint8_t> g_u8;
+static Vol::Data::Dataset parse_u8_as_float()
+{
+    Vol::Data::Dataset d;
+    d.dimensions.x = 40;
+    d.dimensions.y = 36;
+    d.dimensions.z = 30;
+    g_u8.resize(40 * 36 * 30);
+    for (uint32_t z = 0; z < 30; ++z)
+        for (uint32_t y = 0; y < 36; ++y)
+            for (uint32_t x = 0; x < 40; ++x) {
+                const float dx = x - 19.5f, dy = y - 17.5f, dz = z - 14.5f;
+                const float v = 255.0f * std::exp(-(dx * dx + dy * dy + dz * dz) / 120.0f);
+                g_u8[x + 40 * (y + 36 * z)] = (uint8_t)(v + 0.5f);
+            }
+    d.data.assign(g_u8.begin(), g_u8.end());
+    d.min = 255.0f;
+    d.max = 0.0f;
+    for (float v : d.data) {
+        d.min = v < d.min ? v : d.min;
+        d.max = v > d.max ? v : d.max;
+    }
+    return d;
+}
+
+// --u8-dataset: the float Dataset of an 8-bit scan through the unchanged import call
+// (importer.cpp:41-46) is stored as 8-bit voxels (an unsigned char march kernel), and its frame
+// equals the frame of the same voxels uploaded natively as u8, byte for byte.
+static int u8_dataset_check()
+{
+    Application &app = Application::main();
+    app.vulkan_context.reset(new Vol::Rendering::VulkanContext());
+    recreate_viewport_texture(96, 80);
+    import_dataset(parse_u8_as_float);
+    vr_gradient *g = vr_gradient_create();
+    vr_gradient_set_alpha_marker(g, 0, 0.0f, 0.0f);
+    std::vector<uint32_t> tf(256);
+    vr_gradient_discretize(g, tf.size(), tf.data());
+    vr_gradient_destroy(g);
+    update_controls(glm::vec3(0.0f, 0.0f, 0.0f), glm::vec3(1.0f, 1.0f, 1.0f), tf);
+    app.get_scene().get_camera().rotate(100.0f, 60.0f);
+    auto *pass = app.get_vulkan_context().get_offscreen_pass();
+    app.get_vulkan_context().get_main_pass()->render();
+    const std::vector<uint32_t> shown = pass->presenter().color.pixels;
+    vr_params p;
+    vr_params_default(&p);
+    const std::string kname = vr_kernel_name(pass->handle(), &p);
+    // the same voxels as native u8 in a context of their own
+    Vol::Rendering::Hip::OffscreenPass native(96, 80);
+    if (vr_set_volume(native.handle(), g_u8.data(), VR_DTYPE_U8, 40, 36, 30, 0.0f, 255.0f) != VR_OK)
+        throw std::runtime_error(vr_last_error(native.handle()));
+    float mm[2];
+    int st_grp = -1, st_nat = -1;
+    vr_debug_volume_info(pass->handle(), nullptr, mm, &st_grp);
+    vr_debug_volume_info(native.handle(), nullptr, nullptr, &st_nat);
+    if (vr_set_volume(native.handle(), g_u8.data(), VR_DTYPE_U8, 40, 36, 30, mm[0], mm[1]) != VR_OK)
+        throw std::runtime_error(vr_last_error(native.handle()));
+    native.transfer_function_changed(tf);
+    const std::vector<uint32_t> &ref = native.render(VkTraits::camera());
+    const bool u8kernel = kname.find("unsigned char") != std::string::npos;
+    const bool same = shown == ref;
+    std::printf("kernel=%s storage=%d native_storage=%d narrow=%d match=%d\n", kname.c_str(), st_grp,
+                st_nat, (int)u8kernel, (int)same);
+    return same && u8kernel && st_grp == st_nat ? 0 : 1;
+}
+
 int main(int argc, char **argv)
 {
     if (argc > 2 && std::string(argv[1]) == "--device-mask")
         VkTraits::mask() = (uint32_t)std::stoul(argv[2], nullptr, 0);
+    if (argc > 1 && std::string(argv[1]) == "--u8-dataset") {
+        try {
+            return u8_dataset_check();
+        } catch (std::exception &e) {
+            std::fprintf(stderr, "error: %s\n", e.what());
+            return 2;
+        }
+    }
     try {
         Application &app = Application::main();
         app.vulkan_context.reset(new Vol::Rendering::VulkanContext());

@@ -1,11 +1,18 @@
 """GPU parity at BASELINE.json's full configuration sizes.
 
-The oracle cannot march a whole 1080p frame of a 512^3 volume in seconds on a few cores, so
-full-size parity is checked (1) against the oracle on a spread of rows of the SAME frame
-(same volume read back from the device, same camera/TF/params), and (2) through
-size-independent properties: row-block sharding reassembles the frame bit for bit,
-rendering is deterministic, and early-ray termination stays within its error bound.
+C1, C2 and C3 are compared with the CPU oracle over WHOLE frames (every pixel, 4 channels;
+the oracle marches a 1080p C3 frame in about 0.4 s on the GPU box's 16 cores), in the float
+parity format (RGBA after blend, before UNORM quantisation: RMSE <= 1e-4, max |d| <= 2e-3,
+SURVEY.md §8c) and in RGBA8 (<= 1 LSB).  C4 and C5 (1 and 8 GiB of voxels) are compared on 64
+rows spread over the frame, plus size-independent properties: row-block sharding reassembles
+the frame bit for bit, rendering is deterministic, early-ray termination stays within its
+bound.  The spec matched is res/shaders/volume.frag:21-52 under the Vulkan fixed-function
+state of offscreen_pass.cpp (oracle/oracle.c).  Measured errors go to $VR_PARITY_LOG (JSON
+lines) when that is set.
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -16,19 +23,62 @@ import vr_amd
 pytestmark = pytest.mark.gpu
 
 
-def rows_parity(rp, vol, vmin, vmax, tf, cam, W, H, p, nrows=24):
+def _log(**kw):
+    path = os.environ.get("VR_PARITY_LOG")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps(kw) + "\n")
+
+
+def frame_parity(rp, vol, vmin, vmax, tf, cam, W, H, p, name, rows=None):
+    """The GPU frame against the oracle: every row (rows=None) or the given rows."""
     img = rp.render(cam, p, vr_amd.OUT_RGBA32F)
-    rows = np.linspace(H // (2 * nrows), H - 1, nrows).astype(int)
+    img8 = rp.render(cam, p, vr_amd.OUT_RGBA8)
     sc = pyoracle.Scene.from_params(vol, vmin, vmax, tf, cam, W, H, p)
-    ref, _ = sc.render_rows(rows)
-    d = img[rows].astype(np.float64) - ref[rows]
+    if rows is None:
+        ref, _ = sc.render()
+        got, got8 = img, img8
+    else:
+        ref, _ = sc.render_rows(rows)
+        ref, got, got8 = ref[rows], img[rows], img8[rows]
+    d = got.astype(np.float64) - ref
     rmse, mx = float(np.sqrt(np.mean(d * d))), float(np.abs(d).max())
-    assert rmse <= 1e-4 and mx <= 2e-3, f"rmse {rmse:.3e} max {mx:.3e}"
+    lsb = int(np.abs(got8.astype(int) - vr_amd.unorm8(ref).astype(int)).max())
+    exact = float(np.mean(got.view(np.uint32) == ref.astype(np.float32).view(np.uint32)))
+    msg = (f"{name}: {'all' if rows is None else len(rows)} rows x {W} px x 4 ch: rmse {rmse:.3e} "
+           f"max {mx:.3e}, RGBA8 max {lsb} LSB, bit-exact channels {exact:.6f}")
+    _log(case=name, rows="all" if rows is None else len(rows), W=W, H=H, rmse=rmse, max=mx,
+         rgba8_max_lsb=lsb, bit_exact_frac=exact)
+    assert rmse <= 1e-4 and mx <= 2e-3 and lsb <= 1, msg
     return img
 
 
-def test_c3_512_f32_1080p_rows_match_oracle(gpu):
-    """C3: 512^3 f32, 1920x1080, camera r=1.6, Phong + ERT and reference semantics."""
+def spread_rows(H, n=64):
+    return np.unique(np.linspace(H // (2 * n), H - 1, n).astype(int))
+
+
+def test_c1_64_f32_256_whole_frame(gpu):
+    """C1: 64^3 f32 Gaussian blob, 256x256, both parity cameras of the
+    reference's default and a frame-filling one, TF-1 and TF-2, with and without Phong."""
+    W = H = 256
+    vol = synth.gaussian_blob(64)
+    ds = synth.dataset(vol)
+    rp = vr_amd.OffscreenPass(W, H)
+    rp.volume_dataset_changed(ds)
+    for tfname in ("tf1", "tf2"):
+        tf = synth.TFS[tfname]()
+        rp.transfer_function_changed(tf)
+        for camname in ("default", "fill"):
+            cam = synth.camera(camname).to_vr_camera()
+            for p in (vr_amd.default_params(), vr_amd.default_params(shading=1, ert_eps=1e-5)):
+                frame_parity(rp, vol, ds.vmin, ds.vmax, tf, cam, W, H, p,
+                             f"C1 {tfname} {camname} shading={p.shading}")
+    rp.close()
+
+
+def test_c3_512_f32_1080p_whole_frame(gpu):
+    """C3: 512^3 f32, 1920x1080, camera r=1.6 and the reference's default camera, Phong + ERT
+    and reference semantics (no shading, no ERT)."""
     W, H = 1920, 1080
     rp = vr_amd.OffscreenPass(W, H)
     lo, hi = rp.generate_volume((512, 512, 512), np.float32, seed=2024)
@@ -36,15 +86,17 @@ def test_c3_512_f32_1080p_rows_match_oracle(gpu):
     assert vol.min() == lo and vol.max() == hi
     tf = synth.tf2()
     rp.transfer_function_changed(tf)
-    cam = synth.camera("fill").to_vr_camera()
-    for p in (vr_amd.default_params(shading=1, ert_eps=1e-5), vr_amd.default_params()):
-        rows_parity(rp, vol, lo, hi, tf, cam, W, H, p)
+    for camname in ("fill", "default"):
+        cam = synth.camera(camname).to_vr_camera()
+        for p in (vr_amd.default_params(shading=1, ert_eps=1e-5), vr_amd.default_params()):
+            frame_parity(rp, vol, lo, hi, tf, cam, W, H, p,
+                         f"C3 {camname} shading={p.shading} ert={p.ert_eps:g}")
     rp.close()
 
 
-def test_c2_256_u8_1024_rows_match_oracle(gpu):
-    """C2: 256^3 u8 synthetic CT head through the NRRD path, 1024x1024, trilinear + 1D TF."""
-    import os
+def test_c2_256_u8_1024_whole_frame(gpu):
+    """C2: 256^3 u8 synthetic CT head through the NRRD path, 1024x1024, trilinear + 1D TF, the
+    frame-filling camera and the reference's default camera."""
     import tempfile
     W, H = 1024, 1024
     head = synth.ct_head(256)
@@ -57,10 +109,26 @@ def test_c2_256_u8_1024_rows_match_oracle(gpu):
     rp.volume_dataset_changed(ds)
     tf = synth.tf2()
     rp.transfer_function_changed(tf)
-    for camname in ("fill", "rotA"):
+    for camname in ("fill", "default", "rotA"):
         cam = synth.camera(camname).to_vr_camera()
-        rows_parity(rp, head.astype(np.float32), ds.vmin, ds.vmax, tf, cam, W, H,
-                    vr_amd.default_params(), nrows=16)
+        frame_parity(rp, head.astype(np.float32), ds.vmin, ds.vmax, tf, cam, W, H,
+                     vr_amd.default_params(), f"C2 {camname}")
+    rp.close()
+
+
+def test_c4_1024_u8_2048_rows_match_oracle(gpu):
+    """C4: 1024^3 u8 (generated on the device, seed 7) at 2048x2048: 64 rows spread over the
+    frame against the oracle marching the same voxels."""
+    W, H, N = 2048, 2048, 1024
+    rp = vr_amd.OffscreenPass(W, H)
+    lo, hi = rp.generate_volume((N, N, N), np.uint8, seed=7)
+    tf = synth.tf2()
+    rp.transfer_function_changed(tf)
+    vol = rp.read_volume(native=True)
+    cam = synth.camera("fill").to_vr_camera()
+    for p in (vr_amd.default_params(), vr_amd.default_params(shading=1, ert_eps=1e-5)):
+        frame_parity(rp, vol, lo, hi, tf, cam, W, H, p, f"C4 shading={p.shading}",
+                     rows=spread_rows(H))
     rp.close()
 
 
@@ -132,7 +200,8 @@ def test_c5_2048_u8_4096_shards_determinism_ert_and_rows(gpu):
     assert float(vol.min()) == lo and float(vol.max()) == hi
     a = None
     for q in (p, vr_amd.default_params(shading=1, ert_eps=1e-5)):
-        img = rows_parity(rp, vol, lo, hi, tf, cam, W, H, q, nrows=8)
+        img = frame_parity(rp, vol, lo, hi, tf, cam, W, H, q, f"C5 shading={q.shading}",
+                           rows=spread_rows(H))
         if a is None:
             a = img
     # ERT at eps: colour error <= T_stop * (C + 0.11 + 1) <= 2.2 eps

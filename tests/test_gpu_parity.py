@@ -623,3 +623,54 @@ def test_host_render_row_bands_equal_device_frame(rp):
                 for i, f in enumerate(frames):
                     assert f.shape == ref.shape
                     assert np.array_equal(f.view(np.uint8), ref.view(np.uint8)), (W, H, shading, skip, fmt, i)
+
+
+@pytest.mark.parametrize("np_native,src", [(np.uint8, np.float32), (np.int8, np.float32),
+                                           (np.uint16, np.float32), (np.int16, np.int32),
+                                           (np.uint8, np.int64)])
+def test_integer_valued_uploads_stored_narrow(rp, np_native, src):
+    """The reference makes every voxel a float (nrrd_file_parser.cpp:49-77): an 8/16-bit scan
+    reaches volume_dataset_changed as floats.  Such an upload is stored in the narrowest exact
+    type (storage code reported by volume_info), and every frame -- unshaded, shaded (stencil vs
+    the f32 difference field), skip-empty -- is byte-identical to the same voxels kept in f32
+    storage (knob narrow = 0) and to their native-dtype upload."""
+    base = synth.gaussians_numpy((37, 33, 41), seed=41)
+    info = np.iinfo(np_native)
+    ints = np.clip(np.rint(info.min + base / base.max() * (int(info.max) - int(info.min))),
+                   info.min, info.max).astype(np_native)
+    want_storage = {np.uint8: 0, np.int8: 1, np.uint16: 2, np.int16: 3}[np_native]
+    W, H = 88, 64
+    rp.framebuffer_size_changed(W, H)
+    tf = synth.tf_band(0.2, 0.9)
+    vmin, vmax = float(ints.min()), float(ints.max())
+    frames = {}
+    for mode in ("narrow", "f32", "native"):
+        data = ints if mode == "native" else ints.astype(src)
+        with rp.knobs(narrow=0 if mode == "f32" else 1):
+            rp.volume_dataset_changed(vr_amd.Dataset(ints.shape[::-1], vmin, vmax, data))
+        st = rp.volume_info()[2]
+        assert st == (4 if mode == "f32" else want_storage), (mode, st)
+        rp.transfer_function_changed(tf)
+        for camname in ("rotA", "fill"):
+            cam = synth.camera(camname).to_vr_camera()
+            for c in (dict(shading=0), dict(shading=1), dict(shading=1, skip_empty=1)):
+                img = rp.render(cam, vr_amd.default_params(**c), vr_amd.OUT_RGBA32F)
+                frames.setdefault((camname, tuple(c.items())), []).append(img)
+    for key, imgs in frames.items():
+        for img in imgs[1:]:
+            assert np.array_equal(img.view(np.uint32), imgs[0].view(np.uint32)), key
+    ref, _ = oracle_render(ints.astype(np.float32), vmin, vmax, tf, synth.camera("rotA").to_vr_camera(),
+                           W, H, vr_amd.default_params(shading=1))
+    check(frames[("rotA", (("shading", 1),))][0], ref)
+
+
+def test_non_integer_uploads_stay_f32(rp):
+    """A fraction, -0.0, NaN or a value beyond 16 bits anywhere keeps the f32 storage."""
+    base = np.rint(synth.gaussians_numpy((12, 10, 14), seed=2) * 200).astype(np.float32)
+    for poke in (0.5, -0.0, np.nan, 70000.0, -40000.0):
+        v = base.copy()
+        v[5, 5, 5] = poke
+        rp.volume_dataset_changed(vr_amd.Dataset(v.shape[::-1], 0.0, 255.0, v))
+        assert rp.volume_info()[2] == 4, poke
+    rp.volume_dataset_changed(vr_amd.Dataset(base.shape[::-1], 0.0, 255.0, base))
+    assert base.min() >= 0 and rp.volume_info()[2] == (0 if base.max() <= 255 else 2)

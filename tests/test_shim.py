@@ -37,3 +37,15 @@ def test_reference_call_shapes_present_the_hip_frame(gpu, mask):
                        text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "match=1" in r.stdout and "device_mask=0x1" in r.stdout
+
+
+@pytest.mark.gpu
+def test_u8_scan_as_float_dataset_is_stored_native(gpu):
+    """SURVEY.md §8f-1 / VERDICT r2: the reference's loader makes every voxel a float
+    (nrrd_file_parser.cpp:49-77), so an 8-bit scan arrives at volume_dataset_changed as a
+    float Dataset.  Through the unchanged import call it is stored as 8-bit voxels (an
+    `unsigned char` march kernel), and the presented frame equals the native-u8 upload's."""
+    exe = EXE if os.path.exists(EXE) else build()
+    r = subprocess.run([exe, "--u8-dataset"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "narrow=1" in r.stdout and "match=1" in r.stdout

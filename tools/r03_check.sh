@@ -8,7 +8,7 @@ O=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+VR_PARITY_LOG=$O/parity_fullsize.jsonl timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
     > $O/gpu_tests.log 2>&1 &&
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_f4.json 2> $O/bench_f4.err &&
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --frames-in-flight 3 > $O/bench_f3.json 2> $O/bench_f3.err &&

@@ -305,6 +305,11 @@ hipError_t launch_generate(int kind, int storage, void *dst_linear, uint32_t nx,
 hipError_t launch_assemble(const void *gathered, void *out, int out_format, uint32_t W,
                            uint32_t H, uint32_t row_block, uint32_t nranks,
                            uint32_t shard_rows, hipStream_t stream);
+// Integer range of a LINEAR buffer of 32-bit or 64-bit voxels (vr_dtype 5..9): out3_dev = {min,
+// max, not-all-integers flag}, pre-set by the caller to {INT_MAX, INT_MIN, 0}.  Integers are
+// counted only in [-32768, 65535]; -0.0, NaN, infinities and fractions set the flag.
+hipError_t launch_int_range(int src_dtype, const void *src, size_t count, int *out3_dev,
+                            hipStream_t stream);
 // min/max over a LINEAR buffer of the storage type (ordered-uint encoding in minmax_dev).
 hipError_t launch_minmax(int storage, const void *linear, size_t count, float *minmax_dev,
                          hipStream_t stream);

@@ -1820,6 +1820,52 @@ __global__ __launch_bounds__(256) void minmax_kernel(const VT *__restrict__ vol,
     }
 }
 
+// ---- narrowest exact storage of 32/64-bit input ---------------------------------------------
+// The reference converts every NRRD element type to float (nrrd_file_parser.cpp:49-77), so an
+// 8-bit CT volume reaches volume_dataset_changed as floats.  out[0] / out[1]: the minimum and
+// maximum voxel (as int) when every voxel is an integer in [kIntRangeLo, kIntRangeHi]; out[2]
+// != 0 otherwise (a fraction, NaN, infinity, -0.0, or a value outside that range).  A float
+// voxel counts as an integer only if v == rint(v) and it is not -0.0, so storing it in an
+// 8/16-bit type and converting back (float(int) is exact) gives the same bits.
+constexpr int kIntRangeLo = -32768, kIntRangeHi = 65535;
+template <typename SrcT>
+__global__ __launch_bounds__(256) void int_range_kernel(const SrcT *__restrict__ src, size_t total,
+                                                        int *out)
+{
+    int lo = kIntRangeHi, hi = kIntRangeLo, bad = 0;
+    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+         g += (size_t)gridDim.x * blockDim.x) {
+        const SrcT v = src[g];
+        int iv;
+        if constexpr (std::is_floating_point<SrcT>::value) {
+            const float f = (float)v;
+            const bool ok = f >= (float)kIntRangeLo && f <= (float)kIntRangeHi && f == rintf(f) &&
+                            !(f == 0.0f && signbit(f));
+            bad |= ok ? 0 : 1;
+            iv = ok ? (int)f : 0;
+        } else {
+            const bool ok = (long long)v >= kIntRangeLo && (long long)v <= kIntRangeHi &&
+                            !(std::is_unsigned<SrcT>::value && (unsigned long long)v > (unsigned long long)kIntRangeHi);
+            bad |= ok ? 0 : 1;
+            iv = ok ? (int)v : 0;
+        }
+        lo = iv < lo ? iv : lo;
+        hi = iv > hi ? iv : hi;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const int l2 = __shfl_xor(lo, off, 64), h2 = __shfl_xor(hi, off, 64), b2 = __shfl_xor(bad, off, 64);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+        bad |= b2;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&out[0], lo);
+        atomicMax(&out[1], hi);
+        if (bad) atomicOr(&out[2], 1);
+    }
+}
+
 // ---- f32 gradient field (shading) ------------------------------------------------------------
 
 // Voxel at padded coordinates (p = logical + kPad) from the bricked z-pair density: component
@@ -2274,6 +2320,21 @@ hipError_t launch_minmax(int storage, const void *linear, size_t count, float *m
         case ST_U16: hipLaunchKernelGGL((minmax_kernel<uint16_t>), dim3(g), dim3(256), 0, s, (const uint16_t *)linear, count, o); break;
         case ST_I16: hipLaunchKernelGGL((minmax_kernel<int16_t>), dim3(g), dim3(256), 0, s, (const int16_t *)linear, count, o); break;
         default: hipLaunchKernelGGL((minmax_kernel<float>), dim3(g), dim3(256), 0, s, (const float *)linear, count, o); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_int_range(int src_dtype, const void *src, size_t count, int *out3_dev,
+                            hipStream_t s)
+{
+    const unsigned g = grid_for(count);
+    switch (src_dtype) {  // enum vr_dtype: the 32/64-bit types NrrdFileParser makes float
+        case 5: hipLaunchKernelGGL((int_range_kernel<int32_t>), dim3(g), dim3(256), 0, s, (const int32_t *)src, count, out3_dev); break;
+        case 6: hipLaunchKernelGGL((int_range_kernel<uint32_t>), dim3(g), dim3(256), 0, s, (const uint32_t *)src, count, out3_dev); break;
+        case 7: hipLaunchKernelGGL((int_range_kernel<int64_t>), dim3(g), dim3(256), 0, s, (const int64_t *)src, count, out3_dev); break;
+        case 8: hipLaunchKernelGGL((int_range_kernel<uint64_t>), dim3(g), dim3(256), 0, s, (const uint64_t *)src, count, out3_dev); break;
+        case 9: hipLaunchKernelGGL((int_range_kernel<float>), dim3(g), dim3(256), 0, s, (const float *)src, count, out3_dev); break;
+        default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
