@@ -43,17 +43,29 @@ def main():
     ap.add_argument("--tile-order", type=int, default=0)
     ap.add_argument("--skip-empty", type=int, default=0)
     ap.add_argument("--wave-shape", type=int, default=0)
+    ap.add_argument("--knob", action="append", default=[],
+                    help="name=value: a vr_debug.h launch-policy knob (e.g. pipeline=1)")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="> 1: frames on this many streams, ms per frame from the wall clock")
+    ap.add_argument("--views", default=",".join(VIEWS))
     args = ap.parse_args()
     W, H = (int(x) for x in args.size.split("x"))
     rp = vr_amd.OffscreenPass(W, H)
     rp.generate_volume((args.n,) * 3, np.dtype(args.dtype), seed=2024)
     rp.transfer_function_changed(synth.TFS[args.tf]())
+    for kv in args.knob:
+        k, v = kv.split("=")
+        rp.set_knob(k, int(v))
     out = torch.empty((H + 16, W), dtype=torch.int32, device="cuda")
+    streams = [torch.cuda.Stream() for _ in range(args.inflight)]
+    outs = [torch.empty((H + 16, W), dtype=torch.int32, device="cuda") for _ in streams]
     stream = torch.cuda.current_stream().cuda_stream
     p = vr_amd.default_params(shading=args.shading, ert_eps=args.ert, tile_order=args.tile_order,
-                              skip_empty=args.skip_empty, wave_shape=args.wave_shape)
+                              skip_empty=args.skip_empty, wave_shape=args.wave_shape,
+                              frames_in_flight=args.inflight)
     res = {}
-    for name, v in VIEWS.items():
+    for name in args.views.split(","):
+        v = VIEWS[name]
         cam = vr_amd.make_camera(**v).to_vr_camera()
         st = rp.count_work(cam, p)
         for _ in range(3):
@@ -66,6 +78,18 @@ def main():
         ms, n = rp.timing_read()
         rp.timing_enable(False)
         kms = ms / n
+        if args.inflight > 1:  # wall-clock period of frames overlapping on the streams
+            import time
+            for i in range(3 * args.inflight):
+                rp.render_device(cam, p, outs[i % len(outs)].data_ptr(), vr_amd.OUT_RGBA8, 16, 0, 1,
+                                 streams[i % len(streams)].cuda_stream)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(args.reps):
+                rp.render_device(cam, p, outs[i % len(outs)].data_ptr(), vr_amd.OUT_RGBA8, 16, 0, 1,
+                                 streams[i % len(streams)].cuda_stream)
+            torch.cuda.synchronize()
+            kms = (time.perf_counter() - t0) / args.reps * 1e3
         res[name] = dict(kernel_ms=round(kms, 4), samples=st["samples"],
                          gsamples_s=round(st["samples"] / (kms * 1e-3) / 1e9, 2),
                          shaded=st["shaded_samples"], skipped=st["skipped_samples"],

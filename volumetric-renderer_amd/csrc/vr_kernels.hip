@@ -191,12 +191,92 @@ __device__ __forceinline__ f2a zpair_load1(const char *__restrict__ base, size_t
     return *reinterpret_cast<const f2a *>(base + e * 8);
 }
 
+// Global loads one Cell8::load issues.
+template <typename VT>
+constexpr int kCellLoads = kZPair<VT> ? (VR_F32_PLAIN ? 4 : 2) : (kPlainByte<VT> ? 2 : 1);
+
+// s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt bits [3:0] + [15:14], expcnt and lgkmcnt left at
+// their no-wait maxima).  The pipelined march places it, in code every active lane runs, where
+// the stage about to be consumed must have landed and the next stage's N loads may stay in
+// flight: the compiler's own wait insertion then knows at the loop latch that the consumed
+// stage's registers are free, instead of draining every load at the loop head.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt()
+{
+    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
 // The 8 voxels of the cell whose low corner element is e:
 //   f32 z-pair: rows y and y+1, elements x and x+1 -> 2 x 16-B loads;
 //   8/16-bit yz-quad: elements x and x+1 -> 1 x 8-B (u8) / 16-B (u16) load.
+// The raw loaded words of one cell, decoded later.  The pipelined march keeps the words of the
+// sample in flight in the Stage and decodes (byte extraction, int -> float) only when the
+// sample is consumed, after the next sample's loads are issued: decoding at load time put the
+// decode, and with it a wait for the loads, before the loop back-edge (vmcnt(0) right after
+// issue), so only one sample per ray was really in flight.
+template <typename VT, typename = void>
+struct CellRaw {  // generic: the decoded cell itself (loaded and decoded together)
+    float v[8];
+};
+template <typename VT>
+struct CellRaw<VT, std::enable_if_t<kZPair<VT> && !VR_F32_PLAIN>> {
+    f4a r0, r1;  // rows y and y + 1: elements x, x + 1 as z-pairs
+};
+template <typename VT>
+struct CellRaw<VT, std::enable_if_t<kPlainByte<VT> && GeomByte::EX == 8>> {
+    u4a q0, q1;    // slices z and z + 1: the 16 bytes from the 4-aligned address at or below e
+    uint32_t sh;   // e mod 4
+};
+
 template <typename VT>
 struct Cell8 {
     float v[8];  // index dx + 2 dy + 4 dz
+    // issue the loads of the cell whose low corner element is e (decode() converts them)
+    static __device__ __forceinline__ void issue(CellRaw<VT> &w, const char *__restrict__ base,
+                                                 size_t e)
+    {
+        if constexpr (kZPair<VT> && !VR_F32_PLAIN) {
+            w.r0 = zpair_load2(base, e);
+            w.r1 = zpair_load2(base, e + GeomWide::Row);
+        } else if constexpr (kPlainByte<VT> && GeomByte::EX == 8) {
+            const size_t a = e & ~(size_t)3;
+            w.sh = (uint32_t)e & 3u;
+            w.q0 = *reinterpret_cast<const u4a *>(base + a);
+            w.q1 = *reinterpret_cast<const u4a *>(base + a + GeomByte::Slice);
+        } else {
+            Cell8 c;
+            c.load(base, e);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) w.v[i] = c.v[i];
+        }
+    }
+    __device__ __forceinline__ void decode(const CellRaw<VT> &w)
+    {
+        if constexpr (kZPair<VT> && !VR_F32_PLAIN) {
+            v[0] = w.r0.x;
+            v[4] = w.r0.y;
+            v[1] = w.r0.z;
+            v[5] = w.r0.w;
+            v[2] = w.r1.x;
+            v[6] = w.r1.y;
+            v[3] = w.r1.z;
+            v[7] = w.r1.w;
+        } else if constexpr (kPlainByte<VT> && GeomByte::EX == 8) {
+            const uint32_t q[4] = {__builtin_amdgcn_alignbyte(w.q0.y, w.q0.x, w.sh),
+                                   __builtin_amdgcn_alignbyte(w.q0.w, w.q0.z, w.sh),
+                                   __builtin_amdgcn_alignbyte(w.q1.y, w.q1.x, w.sh),
+                                   __builtin_amdgcn_alignbyte(w.q1.w, w.q1.z, w.sh)};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {  // r = dy + 2 dz
+                v[2 * r] = byte_value<VT>(q[r], 0);
+                v[2 * r + 1] = byte_value<VT>(q[r], 1);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = w.v[i];
+        }
+    }
     __device__ __forceinline__ void load(const char *__restrict__ base, size_t e)
     {
         if constexpr (kZPair<VT> && VR_F32_PLAIN) {  // rows (y, z), (y+1, z), (y, z+1), (y+1, z+1)
@@ -678,6 +758,9 @@ __device__ unsigned int g_wg_count;
 #ifndef VR_PIPE_DEPTH
 #define VR_PIPE_DEPTH 2  // samples of a ray in flight in the PIPE kernels (2 or 3)
 #endif
+#ifndef VR_PIPE_UNIFORM
+#define VR_PIPE_UNIFORM 0  // 1: the pipelined march as a wave-uniform loop (measured slower)
+#endif
 #ifndef VR_PIPE_MIN_WAVES
 #define VR_PIPE_MIN_WAVES 1
 #endif
@@ -865,16 +948,19 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
         // compiler waits with counted vmcnt(N) and the next sample's loads stay in flight.
         // The TF is LDS-resident (host guarantees tf_n <= kTfLds for PIPE).
         struct Stage {
-            Cell8<VT> c;
+            CellRaw<VT> w;  // loaded words, decoded at consume
             size_t ce;
             float ax, ay, az;
             int pi, pj, pk;
             bool ok, slab;
         };
-        auto prep = [&](Stage &S, int k) {
+        // live = false: a lane whose ray has ended; its stage is not ok and loads the first
+        // brick's first cell (one cached line per wave), so the wave's loads stay unconditional
+        auto prep = [&](Stage &S, int k, bool live = true) {
             const bool interior = (unsigned)(k - 1) < (unsigned)kin;
-            S.ok = k < nsteps && (interior || !(p0 > 1.0f || p1 > 1.0f || p2 > 1.0f ||
-                                                p0 < 0.0f || p1 < 0.0f || p2 < 0.0f));
+            S.ok = live && k < nsteps &&
+                   (interior || !(p0 > 1.0f || p1 > 1.0f || p2 > 1.0f || p0 < 0.0f ||
+                                  p1 < 0.0f || p2 < 0.0f));
             S.slab = S.ok && (interior || (p0 < P.smax[0] && p1 < P.smax[1] && p2 < P.smax[2] &&
                                            p0 > P.smin[0] && p1 > P.smin[1] && p2 > P.smin[2]));
             int i, j, kk;
@@ -886,15 +972,17 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
             S.pj = j + kPad;
             S.pk = kk + kPad;
             S.ce = cell_offset<VT>(S.pi, S.pj, S.pk, P.nbx, P.nby);
-            S.c.load(vol, S.ce);
+            Cell8<VT>::issue(S.w, vol, S.ce);
         };
         auto consume = [&](const Stage &S) -> bool {  // true: the ray ends (T == 0 or ERT)
-            const float d = S.c.tri(S.ax, S.ay, S.az);
+            Cell8<VT> c;
+            c.decode(S.w);
+            const float d = c.tri(S.ax, S.ay, S.az);
             const float tt = div_by_range(d - P.vmin, P);
             float4 sm = tf_lookup(s_tf, P.tf_n, P.tf_nf, tt);
             if (!S.slab) sm.w = 0.0f;
             if (SHADE && sm.w > 0.0f)
-                shade_sample<VT, GF, true>(P, vol, S.ce, S.c, S.pi, S.pj, S.pk, by_stride,
+                shade_sample<VT, GF, true>(P, vol, S.ce, c, S.pi, S.pj, S.pk, by_stride,
                                            bz_stride, S.ax, S.ay, S.az, d0, d1, d2, sm);
             cr = cr + (sm.x * sm.w) * T;
             cg = cg + (sm.y * sm.w) * T;
@@ -931,6 +1019,27 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
         Stage A, B;
         int k = 0;
         prep(A, k);
+#if VR_PIPE_UNIFORM
+        // Ping-pong with a wave-uniform loop: a lane whose ray has ended stops compositing
+        // (`run`) and loads a dummy cell, but the loop, the loads and the two waits below are
+        // uniform, so on every path the wait before a consume leaves exactly the next stage's
+        // loads outstanding.  (With a per-lane `break` between the halves -- or loads under a
+        // per-lane branch -- the CFG had a path on which the consumed stage's loads were not
+        // known to have landed, and the compiler drained every load: one sample in flight.)
+        bool run = A.ok;
+        while (__any(run)) {
+            advance();
+            prep(B, ++k, run);
+            wait_vmcnt<kCellLoads<VT>>();  // A landed; B's loads stay in flight
+            if (run && (consume(A) || !B.ok)) run = false;
+            // no exit here: a second loop exit would give the loop head a path with B's loads
+            // outstanding (one dummy half-iteration per wave instead)
+            advance();
+            prep(A, ++k, run);
+            wait_vmcnt<kCellLoads<VT>>();  // B landed; A's loads stay in flight
+            if (run && (consume(B) || !A.ok)) run = false;
+        }
+#else
         while (A.ok) {  // ping-pong: no register copies between the two stages
             advance();
             prep(B, ++k);
@@ -939,6 +1048,7 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
             prep(A, ++k);
             if (consume(B)) break;
         }
+#endif
 #endif
     } else
     for (int it = 0; it < nsteps; ++it) {
