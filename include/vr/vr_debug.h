@@ -31,9 +31,11 @@ enum vr_knob {
     VR_KNOB_U8_LAYOUT = 6,  /* -1 auto, 0 plain 7x8x8 bricks, 1 yz-quads (next upload)      */
     VR_KNOB_TILE_ORDER = 7, /* tile order used when vr_params.tile_order == 0: 0 auto (4),
                                1..4 as vr_params.tile_order                                */
-    VR_KNOB_NARROW = 8      /* 1 (default): 32/64-bit uploads whose voxels are all integers
+    VR_KNOB_NARROW = 8,     /* 1 (default): 32/64-bit uploads whose voxels are all integers
                                that fit 8/16 bits are stored in that type (same frames); 0:
                                keep f32 storage (next upload)                              */
+    VR_KNOB_ALT_GEOMETRY = 9 /* f32 volumes: -1 auto (oblique and sparse views read a 7x7x8-
+                               brick copy), 0 never, 1 whenever the launch allows it        */
 };
 
 /* Set / read one knob of `ctx` (a multi-device context sets it on every device).

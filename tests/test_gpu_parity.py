@@ -674,3 +674,37 @@ def test_non_integer_uploads_stay_f32(rp):
         assert rp.volume_info()[2] == 4, poke
     rp.volume_dataset_changed(vr_amd.Dataset(base.shape[::-1], 0.0, 255.0, base))
     assert base.min() >= 0 and rp.volume_info()[2] == (0 if base.max() <= 255 else 2)
+
+
+def test_alt_geometry_copy_bit_identical(rp):
+    """f32 volumes keep a second copy in 7x7x8-cell bricks (kAltFlag) that oblique and sparse
+    views read (vr_api.hip want_alt): the frames are byte-identical to the 8^3 bricks' --
+    unshaded and shaded (stencil gradient across both geometries' brick boundaries), single
+    stage and pipelined -- the launch policy picks it for the reference's default camera and
+    the diagonal view but not for the frame-filling one, and a volume change rebuilds it."""
+    W, H = 160, 120
+    rp.framebuffer_size_changed(W, H)
+    tf = synth.tf_band(0.15, 0.9)
+    for seed in (31, 32):
+        vol = synth.gaussians_numpy((64, 60, 66), seed=seed).astype(np.float32)
+        rp.volume_dataset_changed(synth.dataset(vol))
+        rp.transfer_function_changed(tf)
+        for camname, cam in (("default", synth.camera("default")),
+                             ("diag", vr_amd.make_camera(radius=2.0, rotate=(180.0, 140.0))),
+                             ("fill", synth.camera("fill"))):
+            c = cam.to_vr_camera()
+            for shading in (0, 1):
+                for pipe in (0, 1):
+                    p = vr_amd.default_params(shading=shading, ert_eps=1e-5)
+                    with rp.knobs(pipeline=pipe, grad_field=0, alt_geometry=0):
+                        a = rp.render(c, p, vr_amd.OUT_RGBA32F)
+                    with rp.knobs(pipeline=pipe, grad_field=0, alt_geometry=1):
+                        b = rp.render(c, p, vr_amd.OUT_RGBA32F)
+                        assert "F32Alt" in rp.kernel_name(p)
+                    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (seed, camname, shading, pipe)
+            rp.render(c, vr_amd.default_params())  # the policy's own choice for this view
+            picked = "F32Alt" in rp.kernel_name(vr_amd.default_params())
+            assert picked == (camname in ("default", "diag")), (camname, rp.kernel_name(vr_amd.default_params()))
+        ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, synth.camera("default").to_vr_camera(),
+                               W, H, vr_amd.default_params(shading=1, ert_eps=1e-5))
+        check(rp.render(synth.camera("default").to_vr_camera(), vr_amd.default_params(shading=1, ert_eps=1e-5)), ref)

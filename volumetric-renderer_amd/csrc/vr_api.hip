@@ -38,6 +38,12 @@ struct vr_ctx {
     // the last frame's view (view_dense_rows): image x along the bricks' rows, dense sampling
     bool dense_rows = false;
     double pixel_span = 0.0;  // voxels per pixel step at the volume centre (view_dense_rows)
+    double axis_align = 1.0;  // largest |component| of the centre ray's unit direction
+    // f32 volumes: a second resident copy in GeomAlt bricks (kAltFlag) for oblique and sparse
+    // views, built lazily on the first frame that wants it after a volume change
+    void *alt = nullptr;
+    size_t alt_bytes = 0;
+    bool alt_valid = false, alt_failed = false;
     uint32_t nx = 1, ny = 1, nz = 1;
     float vmin = 0.0f, vmax = 1.0f;
     // transfer function (decoded, linear float RGBA)
@@ -98,7 +104,7 @@ struct vr_ctx {
     // product path never reads the process environment
     struct Knobs {
         int pipeline = -1, pair = -1, pair_lanes = 0, grad_field = -1, lds = 0, u8_layout = -1,
-            tile_order = 0, narrow = 1;
+            tile_order = 0, narrow = 1, alt = -1;
     } knobs;
     // multi-device context (vr_create_mask): one member context per device of the mask, the
     // volume/TF/slicing replicated on each, frames rendered across them by `group`
@@ -354,6 +360,7 @@ int set_bricks(vr_ctx *c, int storage, uint32_t nx, uint32_t ny, uint32_t nz, vo
 {
     c->range_valid = c->dist_valid = false;  // the bricks are about to be rewritten
     c->grad_valid = false;
+    c->alt_valid = c->alt_failed = false;
     const size_t bytes = (size_t)bricks_for(nx, 0, storage) * bricks_for(ny, 1, storage) *
                          bricks_for(nz, 2, storage) * brick_elems(storage) * element_size(storage);
     if (c->bricks && c->brick_bytes == bytes) {
@@ -469,9 +476,10 @@ int check_params(vr_ctx *c, const vr_params *p)
 // wavefront's 16-pixel rows follow the bricks' contiguous rows) and spans at most 0.8 voxels
 // (neighbouring lanes share cache lines).  *span = that step's length in voxels.
 bool view_dense_rows(const double *inv, uint32_t W, uint32_t nx, uint32_t ny, uint32_t nz,
-                     double *span)
+                     double *span, double *align)
 {
     *span = 0.0;
+    *align = 1.0;
     auto unproject = [&](double x, double z, double out[3]) {
         double h[4];
         for (int r = 0; r < 4; ++r) h[r] = inv[0 * 4 + r] * x + inv[2 * 4 + r] * z + inv[3 * 4 + r];
@@ -490,6 +498,7 @@ bool view_dense_rows(const double *inv, uint32_t W, uint32_t nx, uint32_t ny, ui
         dd += d[a] * d[a];
     }
     if (!(dd > 0.0)) return false;
+    *align = std::fmax(std::fabs(d[0]), std::fmax(std::fabs(d[1]), std::fabs(d[2]))) / std::sqrt(dd);
     const double t = -od / dd;
     double n2 = 0.0, v2 = 0.0;
     const double nv[3] = {(double)nx, (double)ny, (double)nz};
@@ -630,7 +639,8 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.out_format = out_format;
     P.slab_default = c->smin[0] == 0.0f && c->smin[1] == 0.0f && c->smin[2] == 0.0f &&
                      c->smax[0] == 1.0f && c->smax[1] == 1.0f && c->smax[2] == 1.0f;
-    c->dense_rows = view_dense_rows(P.inv, c->width, c->nx, c->ny, c->nz, &c->pixel_span);
+    c->dense_rows = view_dense_rows(P.inv, c->width, c->nx, c->ny, c->nz, &c->pixel_span,
+                                    &c->axis_align);
     P.pipelined = use_pipeline(p->shading != 0, P.tiles_x * P.tiles_y, c);
     P.lin = c->lin;
     P.lpx = lin_pitch_x(c->nx);
@@ -730,14 +740,85 @@ int ensure_derived(vr_ctx *c, const vr_params *p, MarchParams &P, hipStream_t s)
     return VR_OK;
 }
 
+// f32 frames of oblique views (the centre ray's direction less than kAltAlign along any axis)
+// and sparse views (more than kAltSpan voxels per pixel step) read the GeomAlt copy: in 7x7x8
+// bricks every 64-B row sits inside one 128-B line, and these views' wavefronts put their lanes
+// on different rows.  C3, 4 frames in flight, ms per frame, 8^3 -> 7x7x8 (profiles/r03/
+// layout_ab/): diagonal 0.81 -> 0.71, default camera r = 3 0.33 -> 0.28 (shaded), 0.25 ->
+// 0.23 (unshaded); the frame-filling, side and top views are 2-4% faster in 8^3 and stay there.
+// Not for skip-empty, difference-field, lane-group or LDS-staged launches (the 8^3 copy keeps
+// those structures).  Knob VR_KNOB_ALT_GEOMETRY 0/1 overrides.
+constexpr double kAltAlign = 0.9, kAltSpan = 0.8;
+bool want_alt(const vr_ctx *c, const vr_params *p, const MarchParams &P)
+{
+    if (c->layout != ST_F32 || p->skip_empty || P.lds || P.pair || P.grad) return false;
+    if (c->knobs.alt >= 0) return c->knobs.alt == 1;
+    return !c->dense_rows && (c->axis_align < kAltAlign || c->pixel_span > kAltSpan);
+}
+
+// Bytes of the GeomAlt copy of the current volume.
+size_t alt_bytes_for(const vr_ctx *c)
+{
+    const int lay = ST_F32 | kAltFlag;
+    return (size_t)bricks_for(c->nx, 0, lay) * bricks_for(c->ny, 1, lay) * bricks_for(c->nz, 2, lay) *
+           brick_elems(lay) * element_size(lay);
+}
+
+// The GeomAlt copy, (re)built on `s` from the 8^3 bricks when stale (unbrick to a linear
+// temporary, brick again; stream-ordered allocations).  *ready = false when it cannot exist
+// (memory short beside a 2 GiB reserve): the launch then stays on the 8^3 copy (same frames).
+int ensure_alt(vr_ctx *c, hipStream_t s, bool *ready)
+{
+    *ready = false;
+    const size_t bytes = alt_bytes_for(c);
+    if (c->alt_valid && c->alt && c->alt_bytes == bytes) {
+        *ready = true;
+        return VR_OK;
+    }
+    if (c->alt_failed) return VR_OK;
+    const size_t lin = (size_t)c->nx * c->ny * c->nz * sizeof(float);
+    if (!c->alt || c->alt_bytes != bytes) {
+        if (c->alt) hipFree(c->alt);
+        c->alt = nullptr;
+        c->alt_bytes = 0;
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess ||
+            free_b < bytes + kBrickSlackBytes + lin + (2ull << 30) ||
+            hipMalloc(&c->alt, bytes + kBrickSlackBytes) != hipSuccess) {
+            (void)hipGetLastError();
+            c->alt = nullptr;
+            c->alt_failed = true;
+            return VR_OK;
+        }
+        c->alt_bytes = bytes;
+    }
+    void *tmp = nullptr;
+    HIP_TRY(c, hipMallocAsync(&tmp, lin, s), "hipMallocAsync(alt staging)");
+    hipError_t e = launch_unbrick(c->layout, c->bricks, tmp, c->nx, c->ny, 0, c->nz, s);
+    if (e == hipSuccess)
+        e = launch_brick_from_linear(VR_DTYPE_F32, tmp, c->alt, c->nx, c->ny, c->nz,
+                                     ST_F32 | kAltFlag, s);
+    const hipError_t f = hipFreeAsync(tmp, s);
+    if (e != hipSuccess) return hip_fail(c, e, "alt geometry copy");
+    if (f != hipSuccess) return hip_fail(c, f, "hipFreeAsync(alt staging)");
+    c->alt_valid = true;
+    *ready = true;
+    // frames on other streams that read the copy wait for this build (ensure_derived)
+    if (!c->built_ev)
+        HIP_TRY(c, hipEventCreateWithFlags(&c->built_ev, hipEventDisableTiming), "hipEventCreate");
+    HIP_TRY(c, hipEventRecord(c->built_ev, s), "hipEventRecord(alt build)");
+    c->built_recorded = true;
+    return VR_OK;
+}
+
 // The march variant a launch runs, as part of the schedule key: a shaded, unshaded or
 // skip-empty frame of the same geometry on the same stream has other tile durations, so one
 // variant's order is not learned from another's (speed only; no measured change on the bench,
 // whose runs use fresh streams).
-uint32_t tile_kernel_key(const MarchParams &P, bool shading)
+uint32_t tile_kernel_key(const MarchParams &P, bool shading, bool alt)
 {
     return (shading ? 1u : 0u) | (P.skip_empty ? 2u : 0u) | (P.grad ? 4u : 0u) |
-           (P.pipelined ? 8u : 0u);
+           (P.pipelined ? 8u : 0u) | (alt ? 16u : 0u);
 }
 
 // Adaptive tile order (tile_order 4): the schedule entry of this launch geometry (created on
@@ -896,6 +977,7 @@ int *knob_slot(vr_ctx *c, int knob)
         case VR_KNOB_U8_LAYOUT: return &c->knobs.u8_layout;
         case VR_KNOB_TILE_ORDER: return &c->knobs.tile_order;
         case VR_KNOB_NARROW: return &c->knobs.narrow;
+        case VR_KNOB_ALT_GEOMETRY: return &c->knobs.alt;
         default: return nullptr;
     }
 }
@@ -1104,6 +1186,7 @@ void vr_destroy(vr_ctx *c)
     if (c->brick_range) hipFree(c->brick_range);
     if (c->skip_dist) hipFree(c->skip_dist);
     if (c->grad) hipFree(c->grad);
+    if (c->alt) hipFree(c->alt);
     for (auto &t : c->sched) {
         hipFree(t.cost);
         hipFree(t.perm);
@@ -1461,7 +1544,21 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
         P.tiles_y = (P.local_rows + th - 1) / th;
         P.supers_total = P.supers_x * ((P.tiles_y + kSuper - 1) / kSuper);
     }
-    vr_ctx::TileSched *ts = tile_sched(c, P, stream, tile_kernel_key(P, p->shading != 0));
+    // oblique and sparse f32 views: the GeomAlt copy (want_alt)
+    int layout = c->layout;
+    if (want_alt(c, p, P)) {
+        bool ready = false;
+        rc = ensure_alt(c, s, &ready);
+        if (rc) return rc;
+        if (ready) {
+            layout = ST_F32 | kAltFlag;
+            P.vol = c->alt;
+            P.nbx = bricks_for(c->nx, 0, layout);
+            P.nby = bricks_for(c->ny, 1, layout);
+        }
+    }
+    vr_ctx::TileSched *ts =
+        tile_sched(c, P, stream, tile_kernel_key(P, p->shading != 0, layout != c->layout));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing) {
         e0 = pooled_event(c);
@@ -1469,7 +1566,7 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
         if (!e0 || !e1) return fail(c, VR_EIO, "hipEventCreate failed");
         HIP_TRY(c, hipEventRecord(e0, s), "hipEventRecord");
     }
-    HIP_TRY(c, launch_march(c->layout, p->shading != 0, false, P, s), "march kernel launch");
+    HIP_TRY(c, launch_march(layout, p->shading != 0, false, P, s), "march kernel launch");
     if (c->timing) {
         HIP_TRY(c, hipEventRecord(e1, s), "hipEventRecord");
         c->ev_pending.emplace_back(e0, e1);
@@ -1693,7 +1790,13 @@ const char *vr_kernel_name(const vr_ctx *c, const vr_params *p)
     const bool pipe = use_pipeline(p && p->shading, tiles, c) &&
                       !(p && p->skip_empty) && c->tf_n <= 256;
     if (p && use_lds(c, p)) return march_lds_kernel_name(c->storage, p->shading != 0);
-    return march_kernel_name(c->layout, p && p->shading != 0, false, p && p->skip_empty != 0, gf,
+    int layout = c->layout;
+    if (p && !gf && c->alt_valid) {  // want_alt for the full frame of the last view
+        MarchParams P;
+        std::memset(&P, 0, sizeof P);
+        if (want_alt(c, p, P)) layout = ST_F32 | kAltFlag;
+    }
+    return march_kernel_name(layout, p && p->shading != 0, false, p && p->skip_empty != 0, gf,
                              pipe);
 }
 

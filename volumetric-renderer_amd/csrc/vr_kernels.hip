@@ -59,7 +59,9 @@ typedef uint32_t u2a __attribute__((ext_vector_type(2))) __attribute__((aligned(
 typedef uint32_t u4a __attribute__((ext_vector_type(4))) __attribute__((aligned(4)));
 
 template <typename VT>
-constexpr bool kZPair = std::is_same<VT, float>::value;
+struct is_quad8 : std::false_type {};
+template <typename T>
+struct is_quad8<Quad8<T>> : std::true_type {};
 // bytes per element; 32-bit words per element (quad layouts)
 // VT is the voxel type, or Quad8<T> for 8-bit voxels in yz-quads (vr_internal.h kQuadFlag);
 // Vox<VT> the voxel type either way
@@ -71,10 +73,17 @@ template <typename T>
 struct VoxOf<Quad8<T>> {
     using type = T;
 };
+template <>
+struct VoxOf<F32Alt> {
+    using type = float;
+};
 template <typename VT>
 using Vox = typename VoxOf<VT>::type;
 template <typename VT>
-constexpr bool kIsQuad8 = !std::is_same<VT, Vox<VT>>::value;
+constexpr bool kIsQuad8 = is_quad8<VT>::value;
+// f32 z-pair elements (8^3 bricks, or GeomAlt bricks for F32Alt)
+template <typename VT>
+constexpr bool kZPair = std::is_same<Vox<VT>, float>::value;
 // 8-bit volumes stored one voxel per element (VR_U8_PLAIN, vr_internal.h)
 template <typename VT>
 constexpr bool kPlainByte = sizeof(VT) == 1 && VR_U8_PLAIN && !kIsQuad8<VT>;
@@ -82,7 +91,8 @@ template <typename VT>
 constexpr int kElemBytes = kZPair<VT> ? 4 * (int)kF32VoxelsPerElement
                                       : (kPlainByte<VT> ? 1 : 4 * (int)sizeof(VT));
 template <typename VT>
-using GeomOf = std::conditional_t<kPlainByte<VT>, GeomByte, GeomWide>;
+using GeomOf = std::conditional_t<kPlainByte<VT>, GeomByte,
+                                  std::conditional_t<std::is_same<VT, F32Alt>::value, GeomAlt, GeomWide>>;
 template <typename VT>
 constexpr int kQuadWords = sizeof(VT) == 1 ? 1 : 2;
 
@@ -238,7 +248,7 @@ struct Cell8 {
     {
         if constexpr (kZPair<VT> && !VR_F32_PLAIN) {
             w.r0 = zpair_load2(base, e);
-            w.r1 = zpair_load2(base, e + GeomWide::Row);
+            w.r1 = zpair_load2(base, e + GeomOf<VT>::Row);
         } else if constexpr (kPlainByte<VT> && GeomByte::EX == 8) {
             const size_t a = e & ~(size_t)3;
             w.sh = (uint32_t)e & 3u;
@@ -289,7 +299,7 @@ struct Cell8 {
             }
         } else if constexpr (kZPair<VT>) {
             const f4a r0 = zpair_load2(base, e);
-            const f4a r1 = zpair_load2(base, e + GeomWide::Row);
+            const f4a r1 = zpair_load2(base, e + GeomOf<VT>::Row);
             v[0] = r0.x;
             v[4] = r0.y;
             v[1] = r0.z;
@@ -1790,7 +1800,7 @@ __global__ __launch_bounds__(256) void brick_kernel(const SrcT *__restrict__ src
                                                     uint32_t ny, uint32_t nz, uint32_t nbx,
                                                     uint32_t nby, size_t nbricks)
 {
-    constexpr bool zpair = std::is_same<DstT, float>::value;
+    constexpr bool zpair = kZPair<DstT>;
     using G = GeomOf<DstT>;
     using V = Vox<DstT>;
     // a workgroup per brick (grid-stride over bricks), its threads over the brick's elements:
@@ -2228,6 +2238,18 @@ hipError_t launch_march_vt(bool shade, bool count, const MarchParams &p, hipStre
                  : launch_march_t<VT, false, false, false>(p, s);
 }
 
+// The f32 volume's GeomAlt copy (kAltFlag) serves full-frame launches without skip-empty, the
+// difference field, lane groups or LDS staging (the host picks it for oblique and sparse views
+// only): single-stage or pipelined, shaded (stencil gradient) or not.
+hipError_t launch_march_alt(bool shade, const MarchParams &p, hipStream_t s)
+{
+    if (p.pipelined && p.tf_n <= kTfLds)
+        return shade ? launch_march_t<F32Alt, true, false, false, false, true>(p, s)
+                     : launch_march_t<F32Alt, false, false, false, false, true>(p, s);
+    return shade ? launch_march_t<F32Alt, true, false, false>(p, s)
+                 : launch_march_t<F32Alt, false, false, false>(p, s);
+}
+
 // workgroups for the per-brick kernels (brick_kernel, grad_field_kernel): one per brick
 inline unsigned grid_bricks(size_t nb)
 {
@@ -2275,6 +2297,7 @@ hipError_t brick_from(const void *src, void *dst, uint32_t nx, uint32_t ny, uint
         case ST_I8 | kQuadFlag: hipLaunchKernelGGL((brick_kernel<SrcT, Quad8<int8_t>>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (int8_t *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_U16: hipLaunchKernelGGL((brick_kernel<SrcT, uint16_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (uint16_t *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_I16: hipLaunchKernelGGL((brick_kernel<SrcT, int16_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (int16_t *)dst, nx, ny, nz, nbx, nby, total); break;
+        case ST_F32 | kAltFlag: hipLaunchKernelGGL((brick_kernel<SrcT, F32Alt>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
         default: hipLaunchKernelGGL((brick_kernel<SrcT, float>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
     }
     return hipGetLastError();
@@ -2293,6 +2316,9 @@ hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &
         case ST_U16: return launch_march_vt<uint16_t>(shade, count, p, stream);
         case ST_I16: return launch_march_vt<int16_t>(shade, count, p, stream);
         case ST_F32: return launch_march_vt<float>(shade, count, p, stream);
+        case ST_F32 | kAltFlag:
+            if (count || p.pair || p.lds || p.skip_empty || p.grad) return hipErrorInvalidValue;
+            return launch_march_alt(shade, p, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -2302,10 +2328,10 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
     // demangled names as rocprofv3 reports them (kernel-trace "Kernel_Name"); storage is the
     // layout code (8-bit yz-quads: the Quad8 instantiations)
     static const std::vector<std::string> names = [] {
-        const char *types[7] = {"unsigned char", "signed char", "unsigned short", "short", "float",
-                                "vr::Quad8<unsigned char>", "vr::Quad8<signed char>"};
+        const char *types[8] = {"unsigned char", "signed char", "unsigned short", "short", "float",
+                                "vr::Quad8<unsigned char>", "vr::Quad8<signed char>", "vr::F32Alt"};
         std::vector<std::string> v;
-        for (int t = 0; t < 7; ++t)
+        for (int t = 0; t < 8; ++t)
             for (int k = 0; k < 32; ++k) {
                 std::string n = std::string("void vr::(anonymous namespace)::march_kernel<") + types[t];
                 for (int bit = 4; bit >= 0; --bit) n += (k >> bit) & 1 ? ", true" : ", false";
@@ -2314,7 +2340,8 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
         return v;
     }();
     if (storage & kQuadFlag) storage = 5 + (storage & 0xF);
-    if (storage < 0 || storage > 6) return "march_kernel<?>";
+    if (storage & kAltFlag) storage = 7;
+    if (storage < 0 || storage > 7) return "march_kernel<?>";
     const int k = (shade ? 16 : 0) + (count ? 8 : 0) + (skip ? 4 : 0) + (gf ? 2 : 0) + (pipe ? 1 : 0);
     return names[storage * 32 + k].c_str();
 }
