@@ -34,8 +34,9 @@ enum vr_knob {
     VR_KNOB_NARROW = 8,     /* 1 (default): 32/64-bit uploads whose voxels are all integers
                                that fit 8/16 bits are stored in that type (same frames); 0:
                                keep f32 storage (next upload)                              */
-    VR_KNOB_ALT_GEOMETRY = 9 /* f32 volumes: -1 auto (oblique and sparse views read a 7x7x8-
-                               brick copy), 0 never, 1 whenever the launch allows it        */
+    VR_KNOB_ALT_GEOMETRY = 9 /* f32 volumes: -1 auto (oblique views read a 7x15x8-cell-brick
+                               copy, sparse views a 15x15x8 one), 0 never, 1 the oblique
+                               copy, 2 the sparse copy, whenever the launch allows it      */
 };
 
 /* Set / read one knob of `ctx` (a multi-device context sets it on every device).

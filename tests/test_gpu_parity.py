@@ -677,14 +677,17 @@ def test_non_integer_uploads_stay_f32(rp):
 
 
 def test_alt_geometry_copy_bit_identical(rp):
-    """f32 volumes keep a second copy in 7x7x8-cell bricks (kAltFlag) that oblique and sparse
-    views read (vr_api.hip want_alt): the frames are byte-identical to the 8^3 bricks' --
-    unshaded and shaded (stencil gradient across both geometries' brick boundaries), single
-    stage and pipelined -- the launch policy picks it for the reference's default camera and
-    the diagonal view but not for the frame-filling one, and a volume change rebuilds it."""
+    """f32 volumes keep further copies in alternative brick geometries that oblique views
+    (7x15x8 cells, kernel tag F32Alt) and sparse views (15x15x8, F32Wide) read (vr_api.hip
+    want_alt): the frames are byte-identical to the 8^3 bricks' -- unshaded and shaded (stencil
+    gradient across every geometry's brick boundaries), single stage and pipelined -- the
+    launch policy picks the oblique copy for the diagonal view, the sparse one for the
+    reference's default camera and neither for the frame-filling view, and a volume change
+    rebuilds them."""
     W, H = 160, 120
     rp.framebuffer_size_changed(W, H)
     tf = synth.tf_band(0.15, 0.9)
+    want = {"default": "F32Wide", "diag": "F32Alt", "fill": None}
     for seed in (31, 32):
         vol = synth.gaussians_numpy((64, 60, 66), seed=seed).astype(np.float32)
         rp.volume_dataset_changed(synth.dataset(vol))
@@ -698,13 +701,16 @@ def test_alt_geometry_copy_bit_identical(rp):
                     p = vr_amd.default_params(shading=shading, ert_eps=1e-5)
                     with rp.knobs(pipeline=pipe, grad_field=0, alt_geometry=0):
                         a = rp.render(c, p, vr_amd.OUT_RGBA32F)
-                    with rp.knobs(pipeline=pipe, grad_field=0, alt_geometry=1):
-                        b = rp.render(c, p, vr_amd.OUT_RGBA32F)
-                        assert "F32Alt" in rp.kernel_name(p)
-                    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (seed, camname, shading, pipe)
+                    for alt, tag in ((1, "F32Alt"), (2, "F32Wide")):
+                        with rp.knobs(pipeline=pipe, grad_field=0, alt_geometry=alt):
+                            b = rp.render(c, p, vr_amd.OUT_RGBA32F)
+                            assert tag in rp.kernel_name(p)
+                        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), \
+                            (seed, camname, shading, pipe, tag)
             rp.render(c, vr_amd.default_params())  # the policy's own choice for this view
-            picked = "F32Alt" in rp.kernel_name(vr_amd.default_params())
-            assert picked == (camname in ("default", "diag")), (camname, rp.kernel_name(vr_amd.default_params()))
+            name = rp.kernel_name(vr_amd.default_params())
+            picked = "F32Alt" if "F32Alt" in name else ("F32Wide" if "F32Wide" in name else None)
+            assert picked == want[camname], (camname, name)
         ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, synth.camera("default").to_vr_camera(),
                                W, H, vr_amd.default_params(shading=1, ert_eps=1e-5))
         check(rp.render(synth.camera("default").to_vr_camera(), vr_amd.default_params(shading=1, ert_eps=1e-5)), ref)

@@ -39,11 +39,14 @@ struct vr_ctx {
     bool dense_rows = false;
     double pixel_span = 0.0;  // voxels per pixel step at the volume centre (view_dense_rows)
     double axis_align = 1.0;  // largest |component| of the centre ray's unit direction
-    // f32 volumes: a second resident copy in GeomAlt bricks (kAltFlag) for oblique and sparse
-    // views, built lazily on the first frame that wants it after a volume change
-    void *alt = nullptr;
-    size_t alt_bytes = 0;
-    bool alt_valid = false, alt_failed = false;
+    // f32 volumes: further resident copies in the alternative geometries (kAltFlag for
+    // oblique views, kWideFlag for sparse ones), each built lazily on the first frame that wants
+    // it after a volume change
+    struct AltCopy {
+        void *bricks = nullptr;
+        size_t bytes = 0;
+        bool valid = false, failed = false;
+    } alt[2];
     uint32_t nx = 1, ny = 1, nz = 1;
     float vmin = 0.0f, vmax = 1.0f;
     // transfer function (decoded, linear float RGBA)
@@ -360,7 +363,7 @@ int set_bricks(vr_ctx *c, int storage, uint32_t nx, uint32_t ny, uint32_t nz, vo
 {
     c->range_valid = c->dist_valid = false;  // the bricks are about to be rewritten
     c->grad_valid = false;
-    c->alt_valid = c->alt_failed = false;
+    for (auto &a : c->alt) a.valid = a.failed = false;
     const size_t bytes = (size_t)bricks_for(nx, 0, storage) * bricks_for(ny, 1, storage) *
                          bricks_for(nz, 2, storage) * brick_elems(storage) * element_size(storage);
     if (c->bricks && c->brick_bytes == bytes) {
@@ -740,68 +743,76 @@ int ensure_derived(vr_ctx *c, const vr_params *p, MarchParams &P, hipStream_t s)
     return VR_OK;
 }
 
-// f32 frames of oblique views (the centre ray's direction less than kAltAlign along any axis)
-// and sparse views (more than kAltSpan voxels per pixel step) read the GeomAlt copy: in 7x7x8
-// bricks every 64-B row sits inside one 128-B line, and these views' wavefronts put their lanes
-// on different rows.  C3, 4 frames in flight, ms per frame, 8^3 -> 7x7x8 (profiles/r03/
-// layout_ab/): diagonal 0.81 -> 0.71, default camera r = 3 0.33 -> 0.28 (shaded), 0.25 ->
-// 0.23 (unshaded); the frame-filling, side and top views are 2-4% faster in 8^3 and stay there.
-// Not for skip-empty, difference-field, lane-group or LDS-staged launches (the 8^3 copy keeps
-// those structures).  Knob VR_KNOB_ALT_GEOMETRY 0/1 overrides.
+// f32 frames of oblique views (the centre ray's direction less than kAltAlign along every axis)
+// read the kAltFlag copy (7x15x8-cell bricks), sparse axis-aligned views (more than kAltSpan
+// voxels per pixel step) the kWideFlag copy (15x15x8): their rows never straddle a 128-B line,
+// and these views' wavefronts put their lanes on different brick rows.  C3, 4 frames in flight,
+// ms per frame (profiles/r03/alt_geometry/): diagonal 0.81 (8^3) -> 0.72 (7x7x8) -> 0.68
+// (7x15x8), shaded default camera r = 3 0.34 (8^3) -> 0.31 (7x7x8) -> 0.28 (15x15x8); the
+// frame-filling, side and top views are 2-4% faster in 8^3 and stay there.  Not for
+// skip-empty, difference-field, lane-group or LDS-staged launches (the 8^3 copy keeps those
+// structures).  Returns the layout code to launch: c->layout, or ST_F32 | kAltFlag / kWideFlag.
+// Knob VR_KNOB_ALT_GEOMETRY: 0 never, 1 the oblique copy, 2 the sparse copy.
 constexpr double kAltAlign = 0.9, kAltSpan = 0.8;
-bool want_alt(const vr_ctx *c, const vr_params *p, const MarchParams &P)
+int want_alt(const vr_ctx *c, const vr_params *p, const MarchParams &P)
 {
-    if (c->layout != ST_F32 || p->skip_empty || P.lds || P.pair || P.grad) return false;
-    if (c->knobs.alt >= 0) return c->knobs.alt == 1;
-    return !c->dense_rows && (c->axis_align < kAltAlign || c->pixel_span > kAltSpan);
+    if (c->layout != ST_F32 || p->skip_empty || P.lds || P.pair || P.grad) return c->layout;
+    int which = 0;
+    if (c->knobs.alt >= 0)
+        which = c->knobs.alt;
+    else if (!c->dense_rows)
+        which = c->axis_align < kAltAlign ? 1 : (c->pixel_span > kAltSpan ? 2 : 0);
+    return which == 1 ? (ST_F32 | kAltFlag) : (which == 2 ? (ST_F32 | kWideFlag) : c->layout);
 }
 
-// Bytes of the GeomAlt copy of the current volume.
-size_t alt_bytes_for(const vr_ctx *c)
+int alt_index(int layout) { return (layout & kAltFlag) ? 0 : 1; }
+
+// Bytes of the copy of the current volume in layout `lay`.
+size_t alt_bytes_for(const vr_ctx *c, int lay)
 {
-    const int lay = ST_F32 | kAltFlag;
     return (size_t)bricks_for(c->nx, 0, lay) * bricks_for(c->ny, 1, lay) * bricks_for(c->nz, 2, lay) *
            brick_elems(lay) * element_size(lay);
 }
 
-// The GeomAlt copy, (re)built on `s` from the 8^3 bricks when stale (unbrick to a linear
-// temporary, brick again; stream-ordered allocations).  *ready = false when it cannot exist
-// (memory short beside a 2 GiB reserve): the launch then stays on the 8^3 copy (same frames).
-int ensure_alt(vr_ctx *c, hipStream_t s, bool *ready)
+// The copy in layout `lay` (kAltFlag or kWideFlag), (re)built on `s` from the 8^3 bricks when
+// stale (unbrick to a linear temporary, brick again; stream-ordered allocations).  *ready =
+// false when it cannot exist (memory short beside a 2 GiB reserve): the launch then stays on
+// the 8^3 copy (same frames).
+int ensure_alt(vr_ctx *c, int lay, hipStream_t s, bool *ready)
 {
     *ready = false;
-    const size_t bytes = alt_bytes_for(c);
-    if (c->alt_valid && c->alt && c->alt_bytes == bytes) {
+    vr_ctx::AltCopy &a = c->alt[alt_index(lay)];
+    const size_t bytes = alt_bytes_for(c, lay);
+    if (a.valid && a.bricks && a.bytes == bytes) {
         *ready = true;
         return VR_OK;
     }
-    if (c->alt_failed) return VR_OK;
+    if (a.failed) return VR_OK;
     const size_t lin = (size_t)c->nx * c->ny * c->nz * sizeof(float);
-    if (!c->alt || c->alt_bytes != bytes) {
-        if (c->alt) hipFree(c->alt);
-        c->alt = nullptr;
-        c->alt_bytes = 0;
+    if (!a.bricks || a.bytes != bytes) {
+        if (a.bricks) hipFree(a.bricks);
+        a.bricks = nullptr;
+        a.bytes = 0;
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess ||
             free_b < bytes + kBrickSlackBytes + lin + (2ull << 30) ||
-            hipMalloc(&c->alt, bytes + kBrickSlackBytes) != hipSuccess) {
+            hipMalloc(&a.bricks, bytes + kBrickSlackBytes) != hipSuccess) {
             (void)hipGetLastError();
-            c->alt = nullptr;
-            c->alt_failed = true;
+            a.bricks = nullptr;
+            a.failed = true;
             return VR_OK;
         }
-        c->alt_bytes = bytes;
+        a.bytes = bytes;
     }
     void *tmp = nullptr;
     HIP_TRY(c, hipMallocAsync(&tmp, lin, s), "hipMallocAsync(alt staging)");
     hipError_t e = launch_unbrick(c->layout, c->bricks, tmp, c->nx, c->ny, 0, c->nz, s);
     if (e == hipSuccess)
-        e = launch_brick_from_linear(VR_DTYPE_F32, tmp, c->alt, c->nx, c->ny, c->nz,
-                                     ST_F32 | kAltFlag, s);
+        e = launch_brick_from_linear(VR_DTYPE_F32, tmp, a.bricks, c->nx, c->ny, c->nz, lay, s);
     const hipError_t f = hipFreeAsync(tmp, s);
     if (e != hipSuccess) return hip_fail(c, e, "alt geometry copy");
     if (f != hipSuccess) return hip_fail(c, f, "hipFreeAsync(alt staging)");
-    c->alt_valid = true;
+    a.valid = true;
     *ready = true;
     // frames on other streams that read the copy wait for this build (ensure_derived)
     if (!c->built_ev)
@@ -815,10 +826,10 @@ int ensure_alt(vr_ctx *c, hipStream_t s, bool *ready)
 // skip-empty frame of the same geometry on the same stream has other tile durations, so one
 // variant's order is not learned from another's (speed only; no measured change on the bench,
 // whose runs use fresh streams).
-uint32_t tile_kernel_key(const MarchParams &P, bool shading, bool alt)
+uint32_t tile_kernel_key(const MarchParams &P, bool shading, int layout)
 {
     return (shading ? 1u : 0u) | (P.skip_empty ? 2u : 0u) | (P.grad ? 4u : 0u) |
-           (P.pipelined ? 8u : 0u) | (alt ? 16u : 0u);
+           (P.pipelined ? 8u : 0u) | ((uint32_t)layout << 8);
 }
 
 // Adaptive tile order (tile_order 4): the schedule entry of this launch geometry (created on
@@ -988,6 +999,7 @@ bool knob_value_ok(int knob, int v)
         case VR_KNOB_PAIR_LANES: return v == 0 || v == 2 || v == 4;
         case VR_KNOB_LDS:
         case VR_KNOB_NARROW: return v == 0 || v == 1;
+        case VR_KNOB_ALT_GEOMETRY: return v >= -1 && v <= 2;
         case VR_KNOB_TILE_ORDER: return v >= 0 && v <= 4;
         default: return v >= -1 && v <= 1;
     }
@@ -1186,7 +1198,8 @@ void vr_destroy(vr_ctx *c)
     if (c->brick_range) hipFree(c->brick_range);
     if (c->skip_dist) hipFree(c->skip_dist);
     if (c->grad) hipFree(c->grad);
-    if (c->alt) hipFree(c->alt);
+    for (auto &a : c->alt)
+        if (a.bricks) hipFree(a.bricks);
     for (auto &t : c->sched) {
         hipFree(t.cost);
         hipFree(t.perm);
@@ -1544,21 +1557,21 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
         P.tiles_y = (P.local_rows + th - 1) / th;
         P.supers_total = P.supers_x * ((P.tiles_y + kSuper - 1) / kSuper);
     }
-    // oblique and sparse f32 views: the GeomAlt copy (want_alt)
+    // oblique and sparse f32 views: an alternative-geometry copy (want_alt)
     int layout = c->layout;
-    if (want_alt(c, p, P)) {
+    if (const int lay = want_alt(c, p, P); lay != c->layout) {
         bool ready = false;
-        rc = ensure_alt(c, s, &ready);
+        rc = ensure_alt(c, lay, s, &ready);
         if (rc) return rc;
         if (ready) {
-            layout = ST_F32 | kAltFlag;
-            P.vol = c->alt;
+            layout = lay;
+            P.vol = c->alt[alt_index(lay)].bricks;
             P.nbx = bricks_for(c->nx, 0, layout);
             P.nby = bricks_for(c->ny, 1, layout);
         }
     }
     vr_ctx::TileSched *ts =
-        tile_sched(c, P, stream, tile_kernel_key(P, p->shading != 0, layout != c->layout));
+        tile_sched(c, P, stream, tile_kernel_key(P, p->shading != 0, layout));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing) {
         e0 = pooled_event(c);
@@ -1791,10 +1804,11 @@ const char *vr_kernel_name(const vr_ctx *c, const vr_params *p)
                       !(p && p->skip_empty) && c->tf_n <= 256;
     if (p && use_lds(c, p)) return march_lds_kernel_name(c->storage, p->shading != 0);
     int layout = c->layout;
-    if (p && !gf && c->alt_valid) {  // want_alt for the full frame of the last view
+    if (p && !gf) {  // want_alt for the full frame of the last view, once its copy exists
         MarchParams P;
         std::memset(&P, 0, sizeof P);
-        if (want_alt(c, p, P)) layout = ST_F32 | kAltFlag;
+        const int lay = want_alt(c, p, P);
+        if (lay != c->layout && c->alt[alt_index(lay)].valid) layout = lay;
     }
     return march_kernel_name(layout, p && p->shading != 0, false, p && p->skip_empty != 0, gf,
                              pipe);

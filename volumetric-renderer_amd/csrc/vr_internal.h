@@ -142,18 +142,29 @@ template <typename T>
 struct Quad8 {
     T v;
 };
-// Brick layout code flag kAltFlag: f32 z-pairs in GeomAlt bricks (7 x 7 x 8 cells: 8-element,
-// 64-B rows, 4608-B bricks = 36 whole 128-B lines), a second resident copy of an f32 volume
-// for oblique and sparse views, where a wavefront's lanes sit on different brick rows and
-// every line a row straddles costs an L1 miss (diagonal and default-camera
-// views 12-15% faster, the frame-filling view 2% slower than in 8^3 bricks).
+// Alternative f32 geometries: further resident copies of an f32 volume in bricks whose z-pair
+// rows never straddle a 128-B line, for the views where a wavefront's lanes sit on different
+// brick rows and every straddled line is another L1 miss:
+//   kAltFlag  (F32Alt):  7 x 15 x 8 cells (8-element, 64-B rows; 8704-B bricks, 68 lines), for
+//                        oblique views (diagonal: 0.81 -> 0.68 ms per C3 frame);
+//   kWideFlag (F32Wide): 15 x 15 x 8 cells (16-element, 128-B rows; 18432-B bricks), for sparse
+//                        axis-aligned views (the reference's default camera: 0.34 -> 0.28 ms).
+// The frame-filling, side and top views stay in 8^3 bricks (2-4% faster there).
 constexpr int kAltFlag = 0x20;
+constexpr int kWideFlag = 0x40;
 #ifndef VR_ALT_BRICK_CELLS
-#define VR_ALT_BRICK_CELLS 7, 7, 8
+#define VR_ALT_BRICK_CELLS 7, 15, 8
+#endif
+#ifndef VR_WIDE_BRICK_CELLS
+#define VR_WIDE_BRICK_CELLS 15, 15, 8
 #endif
 using GeomAlt = BrickGeom<VR_ALT_BRICK_CELLS>;
-// kernel-side tag type of f32 voxels in the kAltFlag layout
+using GeomWideRows = BrickGeom<VR_WIDE_BRICK_CELLS>;
+// kernel-side tag types of f32 voxels in the kAltFlag / kWideFlag layouts
 struct F32Alt {
+    float v;
+};
+struct F32Wide {
     float v;
 };
 
@@ -182,11 +193,13 @@ inline size_t element_size(int st) { return storage_size(st) * voxels_per_elemen
 inline int brick_cells(int st, int a)
 {
     if (st & kAltFlag) return GeomAlt::cells(a);
+    if (st & kWideFlag) return GeomWideRows::cells(a);
     return byte_storage(st) ? GeomByte::cells(a) : GeomWide::cells(a);
 }
 inline size_t brick_elems(int st)
 {
     if (st & kAltFlag) return GeomAlt::Elems;
+    if (st & kWideFlag) return GeomWideRows::Elems;
     return byte_storage(st) ? GeomByte::Elems : GeomWide::Elems;
 }
 

@@ -77,6 +77,10 @@ template <>
 struct VoxOf<F32Alt> {
     using type = float;
 };
+template <>
+struct VoxOf<F32Wide> {
+    using type = float;
+};
 template <typename VT>
 using Vox = typename VoxOf<VT>::type;
 template <typename VT>
@@ -92,7 +96,9 @@ constexpr int kElemBytes = kZPair<VT> ? 4 * (int)kF32VoxelsPerElement
                                       : (kPlainByte<VT> ? 1 : 4 * (int)sizeof(VT));
 template <typename VT>
 using GeomOf = std::conditional_t<kPlainByte<VT>, GeomByte,
-                                  std::conditional_t<std::is_same<VT, F32Alt>::value, GeomAlt, GeomWide>>;
+                                  std::conditional_t<std::is_same<VT, F32Alt>::value, GeomAlt,
+                                  std::conditional_t<std::is_same<VT, F32Wide>::value, GeomWideRows,
+                                                     GeomWide>>>;
 template <typename VT>
 constexpr int kQuadWords = sizeof(VT) == 1 ? 1 : 2;
 
@@ -2241,13 +2247,14 @@ hipError_t launch_march_vt(bool shade, bool count, const MarchParams &p, hipStre
 // The f32 volume's GeomAlt copy (kAltFlag) serves full-frame launches without skip-empty, the
 // difference field, lane groups or LDS staging (the host picks it for oblique and sparse views
 // only): single-stage or pipelined, shaded (stencil gradient) or not.
+template <typename VT>
 hipError_t launch_march_alt(bool shade, const MarchParams &p, hipStream_t s)
 {
     if (p.pipelined && p.tf_n <= kTfLds)
-        return shade ? launch_march_t<F32Alt, true, false, false, false, true>(p, s)
-                     : launch_march_t<F32Alt, false, false, false, false, true>(p, s);
-    return shade ? launch_march_t<F32Alt, true, false, false>(p, s)
-                 : launch_march_t<F32Alt, false, false, false>(p, s);
+        return shade ? launch_march_t<VT, true, false, false, false, true>(p, s)
+                     : launch_march_t<VT, false, false, false, false, true>(p, s);
+    return shade ? launch_march_t<VT, true, false, false>(p, s)
+                 : launch_march_t<VT, false, false, false>(p, s);
 }
 
 // workgroups for the per-brick kernels (brick_kernel, grad_field_kernel): one per brick
@@ -2298,6 +2305,7 @@ hipError_t brick_from(const void *src, void *dst, uint32_t nx, uint32_t ny, uint
         case ST_U16: hipLaunchKernelGGL((brick_kernel<SrcT, uint16_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (uint16_t *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_I16: hipLaunchKernelGGL((brick_kernel<SrcT, int16_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (int16_t *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_F32 | kAltFlag: hipLaunchKernelGGL((brick_kernel<SrcT, F32Alt>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
+        case ST_F32 | kWideFlag: hipLaunchKernelGGL((brick_kernel<SrcT, F32Wide>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
         default: hipLaunchKernelGGL((brick_kernel<SrcT, float>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
     }
     return hipGetLastError();
@@ -2317,8 +2325,10 @@ hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &
         case ST_I16: return launch_march_vt<int16_t>(shade, count, p, stream);
         case ST_F32: return launch_march_vt<float>(shade, count, p, stream);
         case ST_F32 | kAltFlag:
+        case ST_F32 | kWideFlag:
             if (count || p.pair || p.lds || p.skip_empty || p.grad) return hipErrorInvalidValue;
-            return launch_march_alt(shade, p, stream);
+            return (storage & kAltFlag) ? launch_march_alt<F32Alt>(shade, p, stream)
+                                        : launch_march_alt<F32Wide>(shade, p, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -2328,10 +2338,11 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
     // demangled names as rocprofv3 reports them (kernel-trace "Kernel_Name"); storage is the
     // layout code (8-bit yz-quads: the Quad8 instantiations)
     static const std::vector<std::string> names = [] {
-        const char *types[8] = {"unsigned char", "signed char", "unsigned short", "short", "float",
-                                "vr::Quad8<unsigned char>", "vr::Quad8<signed char>", "vr::F32Alt"};
+        const char *types[9] = {"unsigned char", "signed char", "unsigned short", "short", "float",
+                                "vr::Quad8<unsigned char>", "vr::Quad8<signed char>", "vr::F32Alt",
+                                "vr::F32Wide"};
         std::vector<std::string> v;
-        for (int t = 0; t < 8; ++t)
+        for (int t = 0; t < 9; ++t)
             for (int k = 0; k < 32; ++k) {
                 std::string n = std::string("void vr::(anonymous namespace)::march_kernel<") + types[t];
                 for (int bit = 4; bit >= 0; --bit) n += (k >> bit) & 1 ? ", true" : ", false";
@@ -2341,7 +2352,8 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
     }();
     if (storage & kQuadFlag) storage = 5 + (storage & 0xF);
     if (storage & kAltFlag) storage = 7;
-    if (storage < 0 || storage > 7) return "march_kernel<?>";
+    if (storage & kWideFlag) storage = 8;
+    if (storage < 0 || storage > 8) return "march_kernel<?>";
     const int k = (shade ? 16 : 0) + (count ? 8 : 0) + (skip ? 4 : 0) + (gf ? 2 : 0) + (pipe ? 1 : 0);
     return names[storage * 32 + k].c_str();
 }
