@@ -424,7 +424,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--frames-in-flight", type=int, default=4,
+    # 3 frames in flight on the box's 4 hardware queues: C3 318.9-326.4 Gsamples/s against
+    # 309.6-312.2 with 4 and 317.8-322.3 with 6 (profiles/r03/frames_in_flight/)
+    ap.add_argument("--frames-in-flight", type=int, default=3,
                     help="frames in flight on separate streams (1 = serial frame loop)")
     ap.add_argument("--serial-gather", action="store_true",
                     help="= --frames-in-flight 1: each frame's gather waited for before the next render")
