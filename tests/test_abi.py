@@ -126,3 +126,16 @@ def test_no_cpu_fallback_in_product():
             assert needle not in txt, (path, needle)
     out = subprocess.run(["nm", "-D", vr_amd.LIB_PATH], capture_output=True, text=True).stdout
     assert "or_render_rows" not in out
+
+
+def test_committed_pmc_traffic_matches_the_kernel_sources():
+    """profiles/pmc_traffic.json (the measured HBM bytes bench.py's roofline divides by its
+    frame period) was measured on these kernel sources: the headline C3 entry carries the
+    current vr_amd.kernel_source_hash, so a kernel change cannot leave a stale roofline
+    behind (re-measure with tools/measure_round.sh)."""
+    import json
+    d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    for cfg in ("c3", "c3_default", "c3_ref"):
+        e = d[cfg]
+        assert e["source_hash"] == vr_amd.kernel_source_hash(), (cfg, e["source_hash"])
+        assert e["hbm_bytes_per_launch"] > 0 and e["layout"].startswith("st4:")

@@ -91,7 +91,8 @@ def main():
                         method="rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate runs of "
                                f"bench.py --config {cfg} --no-variants, mean over the frame "
                                "kernel's dispatches; FETCH_SIZE x2 gfx950 correction",
-                        source=src)
+                        source=os.path.relpath(src, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+                        if os.path.isabs(src) else src)
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
