@@ -545,6 +545,37 @@ __device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e
 #ifndef VR_GRAD_ZPACK
 #define VR_GRAD_ZPACK 1  // A/B: 0 = (Dx, Dy)-packed tri8x2 + scalar Dz
 #endif
+// The difference field's rows y and y + 1 of a cell (elements x, x + 1: 3 x 16 B each).
+struct FieldRows {
+    f4a a0, a1, a2, b0, b1, b2;
+};
+__device__ __forceinline__ void field_rows_load(const char *__restrict__ gbase, size_t e,
+                                                FieldRows &r)
+{
+    const char *row0 = gbase + e * kGradElemBytes;
+    const char *row1 = row0 + (size_t)GeomWide::Row * kGradElemBytes;
+    r.a0 = *reinterpret_cast<const f4a *>(row0);       // Dx(x) z,z+1  Dy(x) z,z+1
+    r.a1 = *reinterpret_cast<const f4a *>(row0 + 16);  // Dz(x) z,z+1  Dx(x+1) z,z+1
+    r.a2 = *reinterpret_cast<const f4a *>(row0 + 32);  // Dy(x+1) ...  Dz(x+1) ...
+    r.b0 = *reinterpret_cast<const f4a *>(row1);
+    r.b1 = *reinterpret_cast<const f4a *>(row1 + 16);
+    r.b2 = *reinterpret_cast<const f4a *>(row1 + 32);
+}
+// Each axis filtered with its z = 0 / z = 1 halves as packed pairs, which the field's element
+// layout already holds adjacent ({D(z), D(z+1)}): lerp2 over x of rows y and y + 1 gives
+// {c00, c01} and {c10, c11}, lerp2 over y {c0, c1}, then the z lerp -- tri8's IEEE operations
+// per element, without repacking (Dx, Dy) pairs.
+__device__ __forceinline__ void field_rows_filter(const FieldRows &r, float ax, float ay,
+                                                  float az, float &gx, float &gy, float &gz)
+{
+    auto axis = [&](f2v y0x0, f2v y0x1, f2v y1x0, f2v y1x1) {
+        const f2v q = lerp2(lerp2(y0x0, y0x1, ax), lerp2(y1x0, y1x1, ax), ay);
+        return lerpf(q.x, q.y, az);
+    };
+    gx = axis(f2v{r.a0.x, r.a0.y}, f2v{r.a1.z, r.a1.w}, f2v{r.b0.x, r.b0.y}, f2v{r.b1.z, r.b1.w});
+    gy = axis(f2v{r.a0.z, r.a0.w}, f2v{r.a2.x, r.a2.y}, f2v{r.b0.z, r.b0.w}, f2v{r.b2.x, r.b2.y});
+    gz = axis(f2v{r.a1.x, r.a1.y}, f2v{r.a2.z, r.a2.w}, f2v{r.b1.x, r.b1.y}, f2v{r.b2.z, r.b2.w});
+}
 // Gradient from the precomputed f32 field: the cell's 8 corners of {Dx, Dy, Dz}, rows y and
 // y + 1 of elements x, x + 1 (48 B each: 3 x 16-B loads), filtered as grad_filter.
 template <bool PACKED>
@@ -553,25 +584,9 @@ __device__ __forceinline__ void grad_field(const char *__restrict__ gbase, size_
 {
 #if VR_GRAD_ZPACK
     if constexpr (PACKED) {
-        // Each axis filtered with its z = 0 / z = 1 halves as packed pairs, which the field's
-        // element layout already holds adjacent ({D(z), D(z+1)}): lerp2 over x of rows y and
-        // y + 1 gives {c00, c01} and {c10, c11}, lerp2 over y {c0, c1}, then the z lerp --
-        // tri8's IEEE operations per element, without repacking (Dx, Dy) pairs.
-        const char *row0 = gbase + e * kGradElemBytes;
-        const char *row1 = row0 + (size_t)GeomWide::Row * kGradElemBytes;
-        const f4a a0 = *reinterpret_cast<const f4a *>(row0);       // Dx(x) z,z+1  Dy(x) z,z+1
-        const f4a a1 = *reinterpret_cast<const f4a *>(row0 + 16);  // Dz(x) z,z+1  Dx(x+1) z,z+1
-        const f4a a2 = *reinterpret_cast<const f4a *>(row0 + 32);  // Dy(x+1) ...  Dz(x+1) ...
-        const f4a b0 = *reinterpret_cast<const f4a *>(row1);
-        const f4a b1 = *reinterpret_cast<const f4a *>(row1 + 16);
-        const f4a b2 = *reinterpret_cast<const f4a *>(row1 + 32);
-        auto axis = [&](f2v y0x0, f2v y0x1, f2v y1x0, f2v y1x1) {
-            const f2v q = lerp2(lerp2(y0x0, y0x1, ax), lerp2(y1x0, y1x1, ax), ay);
-            return lerpf(q.x, q.y, az);
-        };
-        gx = axis(f2v{a0.x, a0.y}, f2v{a1.z, a1.w}, f2v{b0.x, b0.y}, f2v{b1.z, b1.w});
-        gy = axis(f2v{a0.z, a0.w}, f2v{a2.x, a2.y}, f2v{b0.z, b0.w}, f2v{b2.x, b2.y});
-        gz = axis(f2v{a1.x, a1.y}, f2v{a2.z, a2.w}, f2v{b1.x, b1.y}, f2v{b2.z, b2.w});
+        FieldRows r;
+        field_rows_load(gbase, e, r);
+        field_rows_filter(r, ax, ay, az, gx, gy, gz);
         return;
     }
 #endif
@@ -774,17 +789,22 @@ __device__ unsigned int g_wg_count;
 #ifndef VR_PIPE_DEPTH
 #define VR_PIPE_DEPTH 2  // samples of a ray in flight in the PIPE kernels (2 or 3)
 #endif
+#ifndef VR_DEFER_SHADE
+#define VR_DEFER_SHADE 1  // pipelined + difference field: shade a sample one sample later
+#endif
 #ifndef VR_PIPE_UNIFORM
 #define VR_PIPE_UNIFORM 0  // 1: the pipelined march as a wave-uniform loop (measured slower)
 #endif
 #ifndef VR_PIPE_MIN_WAVES
 #define VR_PIPE_MIN_WAVES 1
 #endif
-// The pipelined shaded kernel with the difference field (the C3 headline kernel): 6 waves
-// (78 VGPRs, no spills) against 5 unconstrained (84): C3 +1.1% (309 -> 313 Gsamples/s, three
-// alternating rounds), side view -4.5% (profiles/r02/pipeline/min_waves6_*).
+// The pipelined shaded kernel with the difference field (the C3 headline kernel).  Round 2,
+// without deferred shading: 6 waves (78 VGPRs, no spills) against 5 unconstrained (84): C3
+// +1.1% (profiles/r02/pipeline/min_waves6_*).  Deferred shading holds 24 more VGPRs of field
+// rows: 94 VGPRs at 5 waves (at 6 it spills); C3 +1.2% against the round-2 kernel, shaded
+// fill/oblique/top views 1-2% faster (profiles/r03/deferred_shading/).
 #ifndef VR_PIPE_GF_MIN_WAVES
-#define VR_PIPE_GF_MIN_WAVES 6
+#define VR_PIPE_GF_MIN_WAVES (VR_DEFER_SHADE ? 5 : 6)
 #endif
 template <bool COUNT, bool SKIP, bool GF, bool PIPE>
 constexpr int kMarchMinWaves =
@@ -990,21 +1010,58 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
             S.ce = cell_offset<VT>(S.pi, S.pj, S.pk, P.nbx, P.nby);
             Cell8<VT>::issue(S.w, vol, S.ce);
         };
+        auto composite = [&](const float4 &sm) -> bool {  // volume.frag:44-45
+            cr = cr + (sm.x * sm.w) * T;
+            cg = cg + (sm.y * sm.w) * T;
+            cb = cb + (sm.z * sm.w) * T;
+            T = T * (1.0f - sm.w);
+            return T == 0.0f || T < P.ert_eps;
+        };
+        // Deferred shading (shaded frames with the difference field): a sample with alpha > 0
+        // issues its 6 field loads and is shaded and composited one sample later, when the next
+        // sample is consumed (its loads landed under the same wait as that sample's density
+        // loads, with the sample after it in flight).  Composites keep the sample order, an
+        // alpha-0 sample composites exactly nothing (C += (rgb 0) T = +0, T *= 1) and is not
+        // held back, and the ray still ends at the first T == 0 / T < eps: the same bits.
+        constexpr bool kDefer = VR_DEFER_SHADE && SHADE && GF;
+        struct Pend {
+            FieldRows g;
+            float4 sm;
+            float ax, ay, az;
+            bool on;
+        } X;
+        X.on = false;
+        auto finish = [&]() -> bool {  // shade + composite the held sample; true: the ray ends
+            if (!kDefer || !X.on) return false;
+            X.on = false;
+            float gx, gy_, gz;
+            field_rows_filter(X.g, X.ax, X.ay, X.az, gx, gy_, gz);
+            phong(P, gx, gy_, gz, d0, d1, d2, X.sm);
+            return composite(X.sm);
+        };
         auto consume = [&](const Stage &S) -> bool {  // true: the ray ends (T == 0 or ERT)
+            if (kDefer && finish()) return true;
             Cell8<VT> c;
             c.decode(S.w);
             const float d = c.tri(S.ax, S.ay, S.az);
             const float tt = div_by_range(d - P.vmin, P);
             float4 sm = tf_lookup(s_tf, P.tf_n, P.tf_nf, tt);
             if (!S.slab) sm.w = 0.0f;
+            if constexpr (kDefer) {
+                if (sm.w > 0.0f) {
+                    field_rows_load(reinterpret_cast<const char *>(P.grad), S.ce, X.g);
+                    X.sm = sm;
+                    X.ax = S.ax;
+                    X.ay = S.ay;
+                    X.az = S.az;
+                    X.on = true;
+                }
+                return false;
+            }
             if (SHADE && sm.w > 0.0f)
                 shade_sample<VT, GF, true>(P, vol, S.ce, c, S.pi, S.pj, S.pk, by_stride,
                                            bz_stride, S.ax, S.ay, S.az, d0, d1, d2, sm);
-            cr = cr + (sm.x * sm.w) * T;
-            cg = cg + (sm.y * sm.w) * T;
-            cb = cb + (sm.z * sm.w) * T;
-            T = T * (1.0f - sm.w);
-            return T == 0.0f || T < P.ert_eps;
+            return composite(sm);
         };
         auto advance = [&]() {
             p0 = p0 + d0 * P.step;
@@ -1065,6 +1122,7 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
             if (consume(B)) break;
         }
 #endif
+        finish();  // deferred shading: the sample still held when the ray left the volume
 #endif
     } else
     for (int it = 0; it < nsteps; ++it) {
