@@ -205,7 +205,8 @@ def run_variant(rp, cfg, steps, warmup, rank, world, inflight, row_block=8, grou
     W, H = cfg["W"], cfg["H"]
     cam = synth.camera(cfg["cam"]).to_vr_camera()
     p = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"],
-                              skip_empty=cfg.get("skip_empty", 0), frames_in_flight=inflight)
+                              skip_empty=cfg.get("skip_empty", 0), frames_in_flight=inflight,
+                              exact_gradient=cfg.get("exact_gradient", 0))
     sr = vr_amd.shard_rows(H, row_block, world)
     if BACKEND != "nccl":
         inflight = 1  # host-staged gloo rehearsal: serial
@@ -586,6 +587,18 @@ def main():
                 (f3["samples"] + f3["skipped_samples"]) * args.steps / V["secs"] / 1e9, 3),
             samples_per_frame=f3["samples"], skipped_samples_per_frame=f3["skipped_samples"],
             warmup_frames=V["warmup_frames"])
+        # exact f32 central differences (vr_params.exact_gradient = 1): every frame bit-identical
+        # to the f32 oracle; the headline's default reads the binary16 difference field
+        ecfg = dict(CONFIGS["c3"], exact_gradient=1)
+        V = run_variant(rp, ecfg, args.steps, warm, rank, world, inflight, group=group)
+        variants["c3_exact_gradient"] = dict(
+            value=round(V["frame"]["samples"] * args.steps / V["secs"] / 1e9, 3), unit="Gsamples/s",
+            ms_per_step=round(V["secs"] / args.steps * 1e3, 4), fps=round(args.steps / V["secs"], 2),
+            kernel_ms=round(V["kms"], 4),
+            kernel=rp.kernel_name(vr_amd.default_params(shading=1, exact_gradient=1)),
+            note="vr_params.exact_gradient = 1: f32 differences (6 field loads per shaded sample), "
+                 "bit-identical to the f32 oracle",
+            warmup_frames=V["warmup_frames"])
 
     if not args.no_variants and world == 1 and not group:
         # PCIe-inclusive: vr_render into (pageable) host memory, the drop-in record() path.
@@ -660,6 +673,11 @@ def main():
                 "viewport": f"{cfg['W']}x{cfg['H']}",
                 "camera": synth.CAMERAS[cfg["cam"]],
                 "tf": cfg["tf"], "shading": cfg["shading"], "ert_eps": cfg["ert"],
+                "exact_gradient": cfg.get("exact_gradient", 0),
+                "gradient": ("binary16 difference field scaled by 2^k (vr_params.exact_gradient = 0; "
+                             "bit-identical to the oracle restating that rounding; C3 within RMSE "
+                             "1.8e-6 of the exact frame)" if cfg["shading"] and cfg["dtype"] == np.float32
+                             else None),
                 "parallelism": parallelism + f", {inflight} frames in flight",
                 "frames_in_flight": inflight,
                 "hw_queues": HW_QUEUES,

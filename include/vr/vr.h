@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 4
+#define VR_ABI_VERSION 5
 
 /* ---- status codes (negative errno style) ---- */
 #define VR_OK 0
@@ -128,6 +128,16 @@ typedef struct vr_params {
      * this one drains, and every launch runs the single-lane kernels, which do the least
      * work per sample.  Must be in [0, 16]. */
     int32_t frames_in_flight;
+    /* Shading of f32 volumes only: how a frame that reads the precomputed difference field
+     * (the shaded dense-row views) holds the central differences.
+     * 0 (default): as binary16 scaled by 2^k, k from the volume's min/max so that every
+     * difference lies in f16's range (|D| 2^k <= 65504).  The shading normalises the gradient,
+     * so the scale cancels exactly; the f16 rounding perturbs the normal by <= 2^-11 relative
+     * per difference (C3: RMSE 1.8e-6, max 3.3e-4 against the f32 frame; the oracle restates
+     * the rounding bit for bit).  3 instead of 6 loads per shaded sample.
+     * 1: exact f32 differences: every frame bit-identical to the f32 oracle.
+     * Frames that form the gradient from the density stencil are exact either way. */
+    int32_t exact_gradient;
 } vr_params;
 
 /* Work counters of one frame (filled by vr_count_work). */

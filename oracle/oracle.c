@@ -273,6 +273,57 @@ static inline float grad_cell(const vsrc *v, int nx, int ny, int nz, int i, int 
     return lerpf(c0, c1, az);
 }
 
+/* The device's binary16 difference field (extension, vr_params.exact_gradient == 0; the
+ * kernel's field_half): D * 2^k clamped to +-65504 (NaN passes), rounded to the nearest
+ * binary16, ties to even, subnormals kept. */
+int or_field_scale_log2(float vmin, float vmax)
+{
+    const double B = (double)(vmax > 0.0f ? vmax : 0.0f) - (double)(vmin < 0.0f ? vmin : 0.0f);
+    if (!(B > 0.0) || B > 1e300) return 0;
+    int k = 0;
+    while (k > -120 && B * ldexp(1.0, k) > 65504.0) --k;
+    while (k < 120 && B * ldexp(1.0, k + 1) <= 65504.0) ++k;
+    return k;
+}
+
+float or_round_f16(float x)
+{
+    if (x != x) return x;
+    const float a = fabsf(x);
+    float r;
+    if (a < 6.103515625e-05f) {            /* below 2^-14: binary16 subnormals, step 2^-24 */
+        r = rintf(a * 16777216.0f) * 5.9604644775390625e-08f;
+    } else {                               /* normal: keep 10 of the 23 mantissa bits */
+        uint32_t u;
+        memcpy(&u, &a, sizeof u);
+        u += 0x0FFFu + ((u >> 13) & 1u);   /* round to nearest, ties to even */
+        u &= ~0x1FFFu;
+        memcpy(&r, &u, sizeof r);
+    }
+    return x < 0.0f ? -r : r;
+}
+
+static inline float dvox_f16(const vsrc *v, int nx, int ny, int nz, int x, int y, int z, int axis,
+                             float scale)
+{
+    float d = dvox(v, nx, ny, nz, x, y, z, axis) * scale;
+    d = d > 65504.0f ? 65504.0f : (d < -65504.0f ? -65504.0f : d);
+    return or_round_f16(d);
+}
+static inline float grad_cell_f16(const vsrc *v, int nx, int ny, int nz, int i, int j, int k,
+                                  float ax, float ay, float az, int axis, float scale)
+{
+#define DV(x, y, z) dvox_f16(v, nx, ny, nz, x, y, z, axis, scale)
+    float c00 = lerpf(DV(i, j, k), DV(i + 1, j, k), ax);
+    float c10 = lerpf(DV(i, j + 1, k), DV(i + 1, j + 1, k), ax);
+    float c01 = lerpf(DV(i, j, k + 1), DV(i + 1, j, k + 1), ax);
+    float c11 = lerpf(DV(i, j + 1, k + 1), DV(i + 1, j + 1, k + 1), ax);
+#undef DV
+    float c0 = lerpf(c00, c10, ay);
+    float c1 = lerpf(c01, c11, ay);
+    return lerpf(c0, c1, az);
+}
+
 /* Normalised coordinate -> texel space: u = s*N - 0.5 (texel i's centre at (i+0.5)/N). */
 static inline void texel_coord(float p, int n, int *i, float *a)
 {
@@ -391,9 +442,17 @@ static void march_pixel(const or_scene *s, const ray_frame *f, const float *lut,
             st->samples++;
             if (s->shading && sc[3] > 0.0f) {
                 /* extension: central differences one texel apart, same weights (grad_cell) */
-                const float gx = grad_cell(&src, nx, ny, nz, i, j, k, ax, ay, az, 0);
-                const float gy = grad_cell(&src, nx, ny, nz, i, j, k, ax, ay, az, 1);
-                const float gz = grad_cell(&src, nx, ny, nz, i, j, k, ax, ay, az, 2);
+                float gx, gy, gz;
+                if (s->grad_f16) {
+                    const float sc = ldexpf(1.0f, or_field_scale_log2(s->vmin, s->vmax));
+                    gx = grad_cell_f16(&src, nx, ny, nz, i, j, k, ax, ay, az, 0, sc);
+                    gy = grad_cell_f16(&src, nx, ny, nz, i, j, k, ax, ay, az, 1, sc);
+                    gz = grad_cell_f16(&src, nx, ny, nz, i, j, k, ax, ay, az, 2, sc);
+                } else {
+                    gx = grad_cell(&src, nx, ny, nz, i, j, k, ax, ay, az, 0);
+                    gy = grad_cell(&src, nx, ny, nz, i, j, k, ax, ay, az, 1);
+                    gz = grad_cell(&src, nx, ny, nz, i, j, k, ax, ay, az, 2);
+                }
                 st->shaded_samples++;
                 const float wx = gx * (float)nx, wy = gy * (float)ny, wz = gz * (float)nz;
                 const float g2 = wx * wx + wy * wy + wz * wz;

@@ -88,6 +88,10 @@ typedef struct or_scene {
     int32_t spec_power;
     /* u8 voxels instead of vol (same layout; float(v) exact), for multi-GiB u8 volumes */
     const uint8_t *vol_u8;
+    /* shading: 1 = the device's binary16 difference field (vr_params.exact_gradient == 0 on a
+     * frame that reads the field): every central difference D becomes round_f16(D * 2^k),
+     * k = or_field_scale_log2(vmin, vmax); 0 = exact f32 differences */
+    int32_t grad_f16;
 } or_scene;
 
 typedef struct or_stats {
@@ -112,6 +116,13 @@ void or_tf_sample(const uint32_t *tf, int n, float t, float out[4]);
  * tex_out = in_tex_coords, frag_out = in_frag_position, dir_out = normalize(frag - cam). */
 int or_pixel_ray(const or_scene *s, int px, int py, float tex_out[3], float frag_out[3],
                  float dir_out[3]);
+
+/* The binary16 field's scale exponent (vr_internal.h field_scale_log2, restated): the largest
+ * k in [-120, 120] with (max(vmax, 0) - min(vmin, 0)) 2^k <= 65504; 0 if that bound is 0 or
+ * not finite. */
+int or_field_scale_log2(float vmin, float vmax);
+/* x rounded to binary16, round to nearest even, returned as float; |x| <= 65504 or NaN. */
+float or_round_f16(float x);
 
 /* Number of OpenMP threads this build would use by default. */
 int or_max_threads(void);

@@ -34,6 +34,7 @@ class or_scene(C.Structure):
         ("shading", C.c_int32), ("clear", C.c_float * 4),
         ("ka", C.c_float), ("kd", C.c_float), ("ks", C.c_float), ("spec_power", C.c_int32),
         ("vol_u8", C.POINTER(C.c_uint8)),
+        ("grad_f16", C.c_int32),
     ]
 
 
@@ -80,7 +81,7 @@ class Scene:
     def __init__(self, vol, vmin, vmax, tf, view, cam_pos, width, height, smin=(0, 0, 0),
                  smax=(1, 1, 1), step=0.005, ray_dist=1.8, ert_eps=0.0, shading=0,
                  clear=(0.11, 0.11, 0.11, 1.0), ka=0.3, kd=0.7, ks=0.25, spec_power=16,
-                 fovy_deg=40.0, znear=0.1, zfar=10.0):
+                 fovy_deg=40.0, znear=0.1, zfar=10.0, grad_f16=False):
         # (nz, ny, nx); u8 volumes are kept as u8 (float(v) is exact: same samples, 1/4 the
         # host memory of a float copy, e.g. C5's 2048^3)
         if np.asarray(vol).dtype == np.uint8:
@@ -110,19 +111,22 @@ class Scene:
         for i in range(4):
             s.clear[i] = float(clear[i])
         s.ka, s.kd, s.ks, s.spec_power = ka, kd, ks, int(spec_power)
+        s.grad_f16 = 1 if grad_f16 else 0
         self.s = s
 
     @classmethod
     def from_params(cls, vol, vmin, vmax, tf, camera, width, height, params, smin=(0, 0, 0),
-                    smax=(1, 1, 1)):
-        """Build from a vr_amd vr_camera / vr_params pair (same meaning as the C ABI)."""
+                    smax=(1, 1, 1), grad_f16=False):
+        """Build from a vr_amd vr_camera / vr_params pair (same meaning as the C ABI).
+        grad_f16: restate the device's binary16 difference field (a shaded f32 frame with
+        params.exact_gradient == 0 whose kernel reads the field, vr_amd.reads_half_field)."""
         return cls(vol, vmin, vmax, tf, list(camera.view), list(camera.position), width, height,
                    smin=smin, smax=smax, step=params.step, ray_dist=params.ray_dist,
                    ert_eps=params.ert_eps, shading=params.shading,
                    clear=list(params.clear_color), ka=params.ambient, kd=params.diffuse,
                    ks=params.specular, spec_power=params.spec_power,
                    fovy_deg=camera.fovy_deg or 40.0, znear=camera.znear or 0.1,
-                   zfar=camera.zfar or 10.0)
+                   zfar=camera.zfar or 10.0, grad_f16=grad_f16)
 
     def render(self, row0=0, row1=None, nthreads=0):
         """Float RGBA (H, W, 4) and work stats; rows outside [row0, row1) are left at NaN."""
@@ -176,6 +180,18 @@ def tf_sample(tf, t):
     out = np.empty(4, np.float32)
     lib().or_tf_sample(tf.ctypes.data, int(tf.size), float(t), out.ctypes.data)
     return out
+
+
+def field_scale_log2(vmin, vmax):
+    lib().or_field_scale_log2.restype = C.c_int
+    lib().or_field_scale_log2.argtypes = [C.c_float, C.c_float]
+    return int(lib().or_field_scale_log2(vmin, vmax))
+
+
+def round_f16(x):
+    lib().or_round_f16.restype = C.c_float
+    lib().or_round_f16.argtypes = [C.c_float]
+    return float(lib().or_round_f16(x))
 
 
 def max_threads():

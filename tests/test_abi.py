@@ -58,7 +58,7 @@ def test_product_never_reads_the_environment():
 
 def test_library_loads_and_pure_entry_points():
     L = vr_amd.lib()
-    assert L.vr_abi_version() == 4
+    assert L.vr_abi_version() == 5
     p = vr_amd.default_params()
     assert p.step == pytest.approx(0.005) and p.ray_dist == pytest.approx(1.8)
     assert list(p.clear_color) == pytest.approx([0.11, 0.11, 0.11, 1.0])
@@ -73,15 +73,15 @@ def test_library_loads_and_pure_entry_points():
 def test_struct_layouts_match_header():
     # sizes of the ABI structs as declared in vr.h (no padding surprises across the boundary)
     assert C.sizeof(vr_amd.vr_camera) == 4 * (16 + 3 + 3)
-    assert C.sizeof(vr_amd.vr_params) == 4 * (3 + 1 + 4 + 3 + 1 + 4)
+    assert C.sizeof(vr_amd.vr_params) == 4 * (3 + 1 + 4 + 3 + 1 + 5)
     assert C.sizeof(vr_amd.vr_stats) == 40
     src = open(os.path.join(ROOT, "include", "vr", "vr.h")).read()
     test = r"""
 #include "vr/vr.h"
 #include <stdio.h>
 #include <stddef.h>
-int main(void) { printf("%zu %zu %zu %zu %zu %zu\n", sizeof(vr_camera), sizeof(vr_params),
-  sizeof(vr_stats), offsetof(vr_params, spec_power), offsetof(vr_params, skip_empty), offsetof(vr_params, frames_in_flight)); return 0; }
+int main(void) { printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(vr_camera), sizeof(vr_params),
+  sizeof(vr_stats), offsetof(vr_params, spec_power), offsetof(vr_params, skip_empty), offsetof(vr_params, frames_in_flight), offsetof(vr_params, exact_gradient)); return 0; }
 """
     tmp = os.path.join("/tmp", "vr_abi_layout")
     with open(tmp + ".c", "w") as f:
@@ -91,8 +91,9 @@ int main(void) { printf("%zu %zu %zu %zu %zu %zu\n", sizeof(vr_camera), sizeof(v
     assert [int(x) for x in out] == [C.sizeof(vr_amd.vr_camera), C.sizeof(vr_amd.vr_params),
                                      C.sizeof(vr_amd.vr_stats), vr_amd.vr_params.spec_power.offset,
                                      vr_amd.vr_params.skip_empty.offset,
-                                     vr_amd.vr_params.frames_in_flight.offset]
-    assert "VR_ABI_VERSION 4" in src
+                                     vr_amd.vr_params.frames_in_flight.offset,
+                                     vr_amd.vr_params.exact_gradient.offset]
+    assert "VR_ABI_VERSION 5" in src
 
 
 def test_create_without_device_fails_cleanly():

@@ -31,25 +31,34 @@ def _log(**kw):
 
 
 def frame_parity(rp, vol, vmin, vmax, tf, cam, W, H, p, name, rows=None):
-    """The GPU frame against the oracle: every row (rows=None) or the given rows."""
+    """The GPU frame against the oracle: every row (rows=None) or the given rows.  A frame
+    that read the binary16 difference field (kernel tag F32H, vr_params.exact_gradient = 0)
+    must also equal the oracle restating that rounding bit for bit."""
     img = rp.render(cam, p, vr_amd.OUT_RGBA32F)
     img8 = rp.render(cam, p, vr_amd.OUT_RGBA8)
+    half = "F32H" in rp.kernel_name(p)
     sc = pyoracle.Scene.from_params(vol, vmin, vmax, tf, cam, W, H, p)
+    sc16 = pyoracle.Scene.from_params(vol, vmin, vmax, tf, cam, W, H, p, grad_f16=True) if half else None
     if rows is None:
         ref, _ = sc.render()
+        ref16 = sc16.render()[0] if half else None
         got, got8 = img, img8
     else:
         ref, _ = sc.render_rows(rows)
+        ref16 = sc16.render_rows(rows)[0][rows] if half else None
         ref, got, got8 = ref[rows], img[rows], img8[rows]
     d = got.astype(np.float64) - ref
     rmse, mx = float(np.sqrt(np.mean(d * d))), float(np.abs(d).max())
     lsb = int(np.abs(got8.astype(int) - vr_amd.unorm8(ref).astype(int)).max())
     exact = float(np.mean(got.view(np.uint32) == ref.astype(np.float32).view(np.uint32)))
+    exact16 = float(np.mean(got.view(np.uint32) == ref16.view(np.uint32))) if half else None
     msg = (f"{name}: {'all' if rows is None else len(rows)} rows x {W} px x 4 ch: rmse {rmse:.3e} "
-           f"max {mx:.3e}, RGBA8 max {lsb} LSB, bit-exact channels {exact:.6f}")
+           f"max {mx:.3e}, RGBA8 max {lsb} LSB, bit-exact channels {exact:.6f}"
+           + (f", binary16 field: bit-exact vs its restatement {exact16:.6f}" if half else ""))
     _log(case=name, rows="all" if rows is None else len(rows), W=W, H=H, rmse=rmse, max=mx,
-         rgba8_max_lsb=lsb, bit_exact_frac=exact)
+         rgba8_max_lsb=lsb, bit_exact_frac=exact, half_field=half, bit_exact_frac_half=exact16)
     assert rmse <= 1e-4 and mx <= 2e-3 and lsb <= 1, msg
+    assert not half or exact16 == 1.0, msg
     return img
 
 
@@ -88,9 +97,12 @@ def test_c3_512_f32_1080p_whole_frame(gpu):
     rp.transfer_function_changed(tf)
     for camname in ("fill", "default"):
         cam = synth.camera(camname).to_vr_camera()
-        for p in (vr_amd.default_params(shading=1, ert_eps=1e-5), vr_amd.default_params()):
+        for p in (vr_amd.default_params(shading=1, ert_eps=1e-5),
+                  vr_amd.default_params(shading=1, ert_eps=1e-5, exact_gradient=1),
+                  vr_amd.default_params()):
             frame_parity(rp, vol, lo, hi, tf, cam, W, H, p,
-                         f"C3 {camname} shading={p.shading} ert={p.ert_eps:g}")
+                         f"C3 {camname} shading={p.shading} ert={p.ert_eps:g} "
+                         f"exact_gradient={p.exact_gradient}")
     rp.close()
 
 

@@ -20,8 +20,9 @@ MAX_TOL = 2e-3
 
 
 def oracle_render(vol_f32, vmin, vmax, tf, cam, W, H, params, smin=(0, 0, 0), smax=(1, 1, 1),
-                  row0=0, row1=None):
-    sc = pyoracle.Scene.from_params(vol_f32, vmin, vmax, tf, cam, W, H, params, smin, smax)
+                  row0=0, row1=None, grad_f16=False):
+    sc = pyoracle.Scene.from_params(vol_f32, vmin, vmax, tf, cam, W, H, params, smin, smax,
+                                    grad_f16=grad_f16)
     return sc.render(row0, row1)
 
 
@@ -462,7 +463,7 @@ def test_f32_gradient_field_equals_stencil_gradient(rp):
     for camname in ("rotA", "fill_oblique", "rotB"):
         cam = synth.camera(camname).to_vr_camera()
         for skip in (0, 1):
-            p = vr_amd.default_params(shading=1, skip_empty=skip)
+            p = vr_amd.default_params(shading=1, skip_empty=skip, exact_gradient=1)
             # the field for every view (the launch policy reads it on dense-row views only)
             with rp.knobs(grad_field=1):
                 a = rp.render(cam, p, vr_amd.OUT_RGBA32F)
@@ -472,6 +473,7 @@ def test_f32_gradient_field_equals_stencil_gradient(rp):
     ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), synth.tf_band(0.2, 0.9), cam,
                            W, H, vr_amd.default_params(shading=1))
     check(a, ref)
+    assert np.array_equal(a.view(np.uint32), ref.view(np.uint32))
 
 
 def test_sparse_views_take_the_stencil_gradient(rp):
@@ -490,10 +492,13 @@ def test_sparse_views_take_the_stencil_gradient(rp):
         cam = synth.camera(camname).to_vr_camera()
         img = rp.render(cam, p, vr_amd.OUT_RGBA32F)
         name = rp.kernel_name(p)
-        gf = "<float, true, false, false, true," in name
+        gf = "<vr::F32H, true, false, false, true," in name
         assert gf == field, (camname, name)
         ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p)
         check(img, ref)
+        ref16, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p,
+                                 grad_f16=gf)
+        assert np.array_equal(img.view(np.uint32), ref16.view(np.uint32)), camname
 
 
 @pytest.mark.parametrize("shading", [0, 1])
@@ -508,7 +513,9 @@ def test_kernel_variants_bit_identical(rp, shading):
     tf = synth.tf_band(0.15, 0.95)
     rp.transfer_function_changed(tf)
     cam = synth.camera("fill_oblique").to_vr_camera()
-    p = vr_amd.default_params(shading=shading, ert_eps=1e-4)
+    # exact differences: the stencil and the f32 field give the same bytes (the binary16 field
+    # variants are compared among themselves in test_half_field_bit_exact)
+    p = vr_amd.default_params(shading=shading, ert_eps=1e-4, exact_gradient=1)
     combos = [dict(pipeline=0, pair=0), dict(pipeline=1, pair=0),
               dict(pair=1, pair_lanes=2), dict(pair=1, pair_lanes=4),
               dict(pair=1, pair_lanes=4, grad_field=0),
@@ -546,7 +553,8 @@ def test_lds_staged_kernel_bit_identical(rp, np_dtype):
         for shading in (0, 1):
             for camname in ("rotA", "fill_oblique"):
                 cam = synth.camera(camname).to_vr_camera()
-                imgs.append(rp.render(cam, vr_amd.default_params(shading=shading, ert_eps=1e-4),
+                imgs.append(rp.render(cam, vr_amd.default_params(shading=shading, ert_eps=1e-4,
+                                                                 exact_gradient=1),
                                       vr_amd.OUT_RGBA32F))
         if base_bytes is None:
             base_bytes = imgs
@@ -654,7 +662,8 @@ def test_integer_valued_uploads_stored_narrow(rp, np_native, src):
         for camname in ("rotA", "fill"):
             cam = synth.camera(camname).to_vr_camera()
             for c in (dict(shading=0), dict(shading=1), dict(shading=1, skip_empty=1)):
-                img = rp.render(cam, vr_amd.default_params(**c), vr_amd.OUT_RGBA32F)
+                # exact differences: the f32 storage's field against the narrow stencil
+                img = rp.render(cam, vr_amd.default_params(exact_gradient=1, **c), vr_amd.OUT_RGBA32F)
                 frames.setdefault((camname, tuple(c.items())), []).append(img)
     for key, imgs in frames.items():
         for img in imgs[1:]:
@@ -714,3 +723,51 @@ def test_alt_geometry_copy_bit_identical(rp):
         ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, synth.camera("default").to_vr_camera(),
                                W, H, vr_amd.default_params(shading=1, ert_eps=1e-5))
         check(rp.render(synth.camera("default").to_vr_camera(), vr_amd.default_params(shading=1, ert_eps=1e-5)), ref)
+
+
+HALF_FIELD_VOLUMES = {
+    # values in [0, 1] (scale 2^15), a CT-like signed range (2^4), tiny values (2^39), and a
+    # volume whose stated max is below its data (differences clamp at +-65504, kept in the
+    # restatement)
+    "unit": (lambda v: v, None),
+    "ct": (lambda v: v * 4000.0 - 1000.0, None),
+    "tiny": (lambda v: v * 1e-7, None),
+    "clamped": (lambda v: v * 3e5, (0.0, 1.0)),
+}
+
+
+@pytest.mark.parametrize("vname", list(HALF_FIELD_VOLUMES))
+def test_half_field_bit_exact(rp, vname):
+    """Shaded f32 frames with vr_params.exact_gradient = 0 (the default) read the difference
+    field as binary16 scaled by 2^k (vr_internal.h field_scale_log2): every frame equals the
+    oracle restating that rounding (oracle.c grad_cell_f16) bit for bit, on every kernel that
+    reads the field (single lane, pipelined, lane groups of 2 and 4, skip-empty); it stays
+    within the parity tolerance of the exact f32 frame, and exact_gradient = 1 reproduces the
+    exact oracle bit for bit."""
+    W, H = 192, 120
+    rp.framebuffer_size_changed(W, H)
+    f, mm = HALF_FIELD_VOLUMES[vname]
+    vol = f(synth.gaussians_numpy((64, 64, 64), seed=51).astype(np.float64)).astype(np.float32)
+    vmin, vmax = (float(vol.min()), float(vol.max())) if mm is None else mm
+    rp.volume_dataset_changed(vr_amd.Dataset(vol.shape[::-1], vmin, vmax, vol))
+    assert rp.volume_info()[2] == 4  # f32 storage (not integer-valued)
+    tf = synth.tf_band(0.15, 0.9)
+    rp.transfer_function_changed(tf)
+    cam = synth.camera("fill").to_vr_camera()
+    for skip in (0, 1):
+        p = vr_amd.default_params(shading=1, ert_eps=1e-5, skip_empty=skip)
+        ref16, _ = oracle_render(vol, vmin, vmax, tf, cam, W, H, p, grad_f16=True)
+        ref32, _ = oracle_render(vol, vmin, vmax, tf, cam, W, H, p)
+        for env in (dict(), dict(pipeline=0, pair=0), dict(pipeline=1, pair=0),
+                    dict(pair=1, pair_lanes=2), dict(pair=1, pair_lanes=4)):
+            with rp.knobs(**env):
+                img = rp.render(cam, p, vr_amd.OUT_RGBA32F)
+            assert np.array_equal(img.view(np.uint32), ref16.view(np.uint32)), (vname, skip, env)
+        assert "F32H" in rp.kernel_name(p), rp.kernel_name(p)
+        if mm is None:  # the clamped volume's differences are not the exact ones
+            check(img, ref32)
+        exact = rp.render(cam, vr_amd.default_params(shading=1, ert_eps=1e-5, skip_empty=skip,
+                                                     exact_gradient=1), vr_amd.OUT_RGBA32F)
+        assert np.array_equal(exact.view(np.uint32), ref32.view(np.uint32)), (vname, skip)
+    with pytest.raises(RuntimeError):
+        rp.render(cam, vr_amd.default_params(shading=1, exact_gradient=2))

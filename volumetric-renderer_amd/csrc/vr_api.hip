@@ -66,6 +66,8 @@ struct vr_ctx {
     float *grad = nullptr;
     size_t grad_bytes = 0;
     bool grad_valid = false;
+    bool grad_half = false;      // the field's precision (vr_params.exact_gradient == 0: binary16)
+    int grad_scale_log2 = 0;     // and its scale (field_scale_log2 of the volume's min/max)
     // adaptive tile order (tile_order 4): per launch geometry, the last launch's per-tile
     // durations and the workgroup -> tile permutation built from them
     // Keyed by the launch stream too: frames in flight on different streams each own their
@@ -468,6 +470,8 @@ int check_params(vr_ctx *c, const vr_params *p)
         return fail(c, VR_EINVAL, "params.spec_power must be in [0, 256]");
     if (p->frames_in_flight < 0 || p->frames_in_flight > 16)
         return fail(c, VR_EINVAL, "params.frames_in_flight must be in [0, 16]");
+    if (p->exact_gradient != 0 && p->exact_gradient != 1)
+        return fail(c, VR_EINVAL, "params.exact_gradient must be 0 or 1");
     const float n = p->ray_dist / p->step;
     if (n > 1.0e8f) return fail(c, VR_EINVAL, "params.ray_dist / step too large");
     return VR_OK;
@@ -691,10 +695,20 @@ int ensure_skip(vr_ctx *c, MarchParams &P, hipStream_t s)
 
 // Shaded f32 frames: (re)build the gradient field when stale.  It needs 3 x the bricked
 // density; when that does not fit beside a 2 GiB reserve the kernel forms the differences
-// from the 4-wide stencil instead (same values, bit for bit).
-void ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s)
+// from the 4-wide stencil instead (exact f32 differences).  half: the binary16 field
+// (vr_params.exact_gradient == 0), the same 24-B elements.  Switching precision rebuilds the
+// field in place after the device has drained (frames in flight may still read it).
+void ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s, bool half)
 {
     if (!use_grad_field(c)) return;
+    const int k = half ? field_scale_log2(c->vmin, c->vmax) : 0;
+    if (c->grad_valid && (c->grad_half != half || c->grad_scale_log2 != k)) {
+        if (hipDeviceSynchronize() != hipSuccess) {
+            (void)hipGetLastError();
+            return;
+        }
+        c->grad_valid = false;
+    }
     const size_t bytes = c->brick_bytes / element_size(ST_F32) * kGradElemBytes;
     if (!c->grad || c->grad_bytes != bytes) {
         if (c->grad) hipFree(c->grad);
@@ -713,11 +727,14 @@ void ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s)
     }
     if (!c->grad_valid) {
         if (launch_grad_field(static_cast<const float *>(c->bricks), c->grad, c->nx, c->ny, c->nz,
-                              s) != hipSuccess)
+                              half, k, s) != hipSuccess)
             return;
         c->grad_valid = true;
+        c->grad_half = half;
+        c->grad_scale_log2 = k;
     }
     P.grad = c->grad;
+    P.grad_half = half ? 1 : 0;
 }
 
 // The derived fields a frame reads (skip-empty classification, gradient field), built on `s`
@@ -730,7 +747,7 @@ int ensure_derived(vr_ctx *c, const vr_params *p, MarchParams &P, hipStream_t s)
         int rc = ensure_skip(c, P, s);
         if (rc) return rc;
     }
-    if (p->shading) ensure_grad(c, P, s);
+    if (p->shading) ensure_grad(c, P, s, p->exact_gradient == 0);
     const bool built = (!r0 && c->range_valid) || (!d0 && c->dist_valid) || (!g0 && c->grad_valid);
     if (built) {
         if (!c->built_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->built_ev, hipEventDisableTiming),
@@ -829,7 +846,7 @@ int ensure_alt(vr_ctx *c, int lay, hipStream_t s, bool *ready)
 uint32_t tile_kernel_key(const MarchParams &P, bool shading, int layout)
 {
     return (shading ? 1u : 0u) | (P.skip_empty ? 2u : 0u) | (P.grad ? 4u : 0u) |
-           (P.pipelined ? 8u : 0u) | ((uint32_t)layout << 8);
+           (P.pipelined ? 8u : 0u) | (P.grad && P.grad_half ? 16u : 0u) | ((uint32_t)layout << 8);
 }
 
 // Adaptive tile order (tile_order 4): the schedule entry of this launch geometry (created on
@@ -1810,6 +1827,7 @@ const char *vr_kernel_name(const vr_ctx *c, const vr_params *p)
         const int lay = want_alt(c, p, P);
         if (lay != c->layout && c->alt[alt_index(lay)].valid) layout = lay;
     }
+    if (gf && p->exact_gradient == 0 && c->storage == ST_F32) layout |= kHalfFieldFlag;
     return march_kernel_name(layout, p && p->shading != 0, false, p && p->skip_empty != 0, gf,
                              pipe);
 }

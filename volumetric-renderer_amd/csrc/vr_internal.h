@@ -6,6 +6,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <cmath>
 #include <type_traits>
 
 namespace vr {
@@ -167,6 +168,13 @@ struct F32Alt {
 struct F32Wide {
     float v;
 };
+// kernel-side tag type of the f32 8^3-brick volume read with the difference field in binary16
+// (MarchParams::grad_half); kHalfFieldFlag marks that variant in kernel names and schedule keys
+// only (the bricks are the ST_F32 ones)
+struct F32H {
+    float v;
+};
+constexpr int kHalfFieldFlag = 0x80;
 
 // Bytes of one voxel of storage type (or layout code) st.
 inline size_t storage_size(int st)
@@ -261,6 +269,9 @@ struct MarchParams {
     // f32 shading: precomputed central differences, element e = {Dx, Dy, Dz} x {z, z + 1}
     // (24 B, same element index as the density); null -> formed from the stencil
     const float *grad;
+    // the field holds {Dx, Dy, Dz} x {(y,z), (y,z+1), (y+1,z), (y+1,z+1)} as binary16, scaled by
+    // 2^k (field_scale_log2; the shading normalises the gradient, so the scale cancels)
+    int32_t grad_half;
     float inv_range;        // RN(1 / range) (div_fast)
     // LDS-staged march (march_lds_kernel): the volume as a LINEAR x-fastest array of the
     // storage type with kPad zero voxels on every side (padded index = logical + 2), row pitch
@@ -352,8 +363,22 @@ hipError_t launch_minmax(int storage, const void *linear, size_t count, float *m
 constexpr int kSkipCap = 16;
 // f32 gradient field (see MarchParams::grad) from the bricked density: same brick grid.
 constexpr size_t kGradElemBytes = 24;
+// half: the binary16 field of MarchParams::grad_half, each difference times 2^scale_log2 and
+// clamped to +-65504 (NaN kept) before rounding to nearest even
 hipError_t launch_grad_field(const float *bricks, float *grad, uint32_t nx, uint32_t ny,
-                             uint32_t nz, hipStream_t stream);
+                             uint32_t nz, bool half, int scale_log2, hipStream_t stream);
+// The binary16 field's scale: the largest k in [-120, 120] with B 2^k <= 65504, where
+// B = max(vmax, 0) - min(vmin, 0) bounds every central difference of voxels in [vmin, vmax]
+// (and of the zero border); 0 when B is 0 or not finite.  oracle/oracle.c restates it.
+inline int field_scale_log2(float vmin, float vmax)
+{
+    const double B = (double)(vmax > 0.0f ? vmax : 0.0f) - (double)(vmin < 0.0f ? vmin : 0.0f);
+    if (!(B > 0.0) || B > 1e300) return 0;
+    int k = 0;
+    while (k > -120 && B * std::ldexp(1.0, k) > 65504.0) --k;
+    while (k < 120 && B * std::ldexp(1.0, k + 1) <= 65504.0) ++k;
+    return k;
+}
 hipError_t launch_brick_range(int storage, const void *bricks, uint32_t nbx, uint32_t nby,
                               uint32_t nbz, float2 *range_dev, hipStream_t stream);
 hipError_t launch_skip_dist(const float2 *range_dev, uint32_t nbx, uint32_t nby, uint32_t nbz,

@@ -81,10 +81,17 @@ template <>
 struct VoxOf<F32Wide> {
     using type = float;
 };
+template <>
+struct VoxOf<F32H> {
+    using type = float;
+};
 template <typename VT>
 using Vox = typename VoxOf<VT>::type;
 template <typename VT>
 constexpr bool kIsQuad8 = is_quad8<VT>::value;
+// the f32 volume read with the binary16 difference field (MarchParams::grad_half)
+template <typename VT>
+constexpr bool kHalfField = std::is_same<VT, F32H>::value;
 // f32 z-pair elements (8^3 bricks, or GeomAlt bricks for F32Alt)
 template <typename VT>
 constexpr bool kZPair = std::is_same<Vox<VT>, float>::value;
@@ -545,12 +552,49 @@ __device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e
 #ifndef VR_GRAD_ZPACK
 #define VR_GRAD_ZPACK 1  // A/B: 0 = (Dx, Dy)-packed tri8x2 + scalar Dz
 #endif
-// The difference field's rows y and y + 1 of a cell (elements x, x + 1: 3 x 16 B each).
-struct FieldRows {
+// The difference field's words one shaded sample reads.  f32 (H = false): rows y and y + 1 of
+// the cell, elements x and x + 1, 3 x 16 B each.  binary16 (H = true): element e holds per
+// axis {D(y,z), D(y,z+1), D(y+1,z), D(y+1,z+1)}, so elements x and x + 1 are 48 contiguous
+// bytes: 3 x 16 B.
+template <bool H>
+struct FieldRowsT {
     f4a a0, a1, a2, b0, b1, b2;
 };
+template <>
+struct FieldRowsT<true> {
+    u4a a0, a1, a2;
+};
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v h2f(uint32_t w)  // two binary16 -> two f32 (exact)
+{
+    return __builtin_convertvector(__builtin_bit_cast(h2v, w), f2v);
+}
 __device__ __forceinline__ void field_rows_load(const char *__restrict__ gbase, size_t e,
-                                                FieldRows &r)
+                                                FieldRowsT<true> &r)
+{
+    const char *p = gbase + e * kGradElemBytes;
+    r.a0 = *reinterpret_cast<const u4a *>(p);
+    r.a1 = *reinterpret_cast<const u4a *>(p + 16);
+    r.a2 = *reinterpret_cast<const u4a *>(p + 32);
+}
+// The f32 path's filter (below) on the converted pairs: per axis a, words 2a / 2a + 1 of
+// element x are the y / y + 1 pairs {D(z), D(z+1)}, words 6 + 2a / 7 + 2a those of x + 1.
+__device__ __forceinline__ void field_rows_filter(const FieldRowsT<true> &r, float ax, float ay,
+                                                  float az, float &gx, float &gy, float &gz)
+{
+    const uint32_t w[12] = {r.a0.x, r.a0.y, r.a0.z, r.a0.w, r.a1.x, r.a1.y,
+                            r.a1.z, r.a1.w, r.a2.x, r.a2.y, r.a2.z, r.a2.w};
+    auto axis = [&](int a) {
+        const f2v q = lerp2(lerp2(h2f(w[2 * a]), h2f(w[6 + 2 * a]), ax),
+                            lerp2(h2f(w[2 * a + 1]), h2f(w[7 + 2 * a]), ax), ay);
+        return lerpf(q.x, q.y, az);
+    };
+    gx = axis(0);
+    gy = axis(1);
+    gz = axis(2);
+}
+__device__ __forceinline__ void field_rows_load(const char *__restrict__ gbase, size_t e,
+                                                FieldRowsT<false> &r)
 {
     const char *row0 = gbase + e * kGradElemBytes;
     const char *row1 = row0 + (size_t)GeomWide::Row * kGradElemBytes;
@@ -565,7 +609,7 @@ __device__ __forceinline__ void field_rows_load(const char *__restrict__ gbase, 
 // layout already holds adjacent ({D(z), D(z+1)}): lerp2 over x of rows y and y + 1 gives
 // {c00, c01} and {c10, c11}, lerp2 over y {c0, c1}, then the z lerp -- tri8's IEEE operations
 // per element, without repacking (Dx, Dy) pairs.
-__device__ __forceinline__ void field_rows_filter(const FieldRows &r, float ax, float ay,
+__device__ __forceinline__ void field_rows_filter(const FieldRowsT<false> &r, float ax, float ay,
                                                   float az, float &gx, float &gy, float &gz)
 {
     auto axis = [&](f2v y0x0, f2v y0x1, f2v y1x0, f2v y1x1) {
@@ -578,13 +622,19 @@ __device__ __forceinline__ void field_rows_filter(const FieldRows &r, float ax, 
 }
 // Gradient from the precomputed f32 field: the cell's 8 corners of {Dx, Dy, Dz}, rows y and
 // y + 1 of elements x, x + 1 (48 B each: 3 x 16-B loads), filtered as grad_filter.
-template <bool PACKED>
+template <bool PACKED, bool H = false>
 __device__ __forceinline__ void grad_field(const char *__restrict__ gbase, size_t e, float ax,
                                            float ay, float az, float &gx, float &gy, float &gz)
 {
+    if constexpr (H) {
+        FieldRowsT<true> r;
+        field_rows_load(gbase, e, r);
+        field_rows_filter(r, ax, ay, az, gx, gy, gz);
+        return;
+    }
 #if VR_GRAD_ZPACK
     if constexpr (PACKED) {
-        FieldRows r;
+        FieldRowsT<false> r;
         field_rows_load(gbase, e, r);
         field_rows_filter(r, ax, ay, az, gx, gy, gz);
         return;
@@ -910,7 +960,8 @@ __device__ __forceinline__ void shade_sample(const MarchParams &P, const char *_
         gy_ = c.v[2] - c.v[0];
         gz = c.v[4] - c.v[0];
     } else if constexpr (GF) {  // f32: precomputed difference field
-        grad_field<PACKED>(reinterpret_cast<const char *>(P.grad), ce, ax, ay, az, gx, gy_, gz);
+        grad_field<PACKED, kHalfField<VT>>(reinterpret_cast<const char *>(P.grad), ce, ax, ay, az,
+                                           gx, gy_, gz);
     } else {
         gradient<VT, PACKED>(vol, ce, c, pi, pj, pk, P.nbx, P.nby, by_stride, bz_stride, ax, ay,
                              az, gx, gy_, gz);
@@ -1025,7 +1076,7 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
         // held back, and the ray still ends at the first T == 0 / T < eps: the same bits.
         constexpr bool kDefer = VR_DEFER_SHADE && SHADE && GF;
         struct Pend {
-            FieldRows g;
+            FieldRowsT<kHalfField<VT>> g;
             float4 sm;
             float ax, ay, az;
             bool on;
@@ -2064,12 +2115,24 @@ __device__ __forceinline__ float padded_voxel(const float *__restrict__ bricks, 
     return bricks[kF32VoxelsPerElement * cell_offset<float>(px, py, pz, nbx, nby)];
 }
 
-// One thread per stored element: D_e(p) = v(p + e) - v(p - e) (the oracle's dvox) for the
-// element's two voxels p = (x, y, z) and (x, y, z + 1), written as {Dx, Dx', Dy, Dy', Dz, Dz'}.
+// binary16 of d * 2^k (scale = 2^k): clamped to +-65504 first (NaN passes), rounded to nearest
+// even (v_cvt_f16_f32; f16 denormals kept).  The oracle's round_f16 restates it.
+__device__ __forceinline__ _Float16 field_half(float d, float scale)
+{
+    float x = d * scale;
+    x = x > 65504.0f ? 65504.0f : (x < -65504.0f ? -65504.0f : x);
+    return (_Float16)x;
+}
+
+// One thread per stored element: D_e(p) = v(p + e) - v(p - e) (the oracle's dvox).  f32 (H =
+// false): the element's two voxels p = (x, y, z) and (x, y, z + 1), written as {Dx, Dx', Dy,
+// Dy', Dz, Dz'}.  binary16 (H = true): the four voxels (x, y + dy, z + dz), per axis
+// {D(y,z), D(y,z+1), D(y+1,z), D(y+1,z+1)}, each field_half(D, scale).
+template <bool H>
 __global__ __launch_bounds__(256) void grad_field_kernel(const float *__restrict__ bricks,
                                                          float *__restrict__ grad, uint32_t nx,
                                                          uint32_t ny, uint32_t nz, uint32_t nbx,
-                                                         uint32_t nby, size_t nbricks)
+                                                         uint32_t nby, size_t nbricks, float scale)
 {
     using G = GeomWide;
     // a workgroup per brick (grid-stride over bricks), its threads over the brick's elements:
@@ -2082,6 +2145,26 @@ __global__ __launch_bounds__(256) void grad_field_kernel(const float *__restrict
         uint32_t bx, by, bz;
         brick_coords((uint32_t)bidx, nbx, nby, bx, by, bz);
         const int x = (int)(bx * G::BX + lx), y = (int)(by * G::BY + lyy), z = (int)(bz * G::BZ + lz);
+        if constexpr (H) {
+            _Float16 hv[12];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {  // q = dz + 2 dy
+                const int yy = y + (q >> 1), zz = z + (q & 1);
+                auto V = [&](int dx, int dy, int dz) {
+                    return padded_voxel(bricks, x + dx, yy + dy, zz + dz, nx, ny, nz, nbx, nby);
+                };
+                hv[0 + q] = field_half(V(1, 0, 0) - V(-1, 0, 0), scale);
+                hv[4 + q] = field_half(V(0, 1, 0) - V(0, -1, 0), scale);
+                hv[8 + q] = field_half(V(0, 0, 1) - V(0, 0, -1), scale);
+            }
+            uint2 *o = reinterpret_cast<uint2 *>(grad) + 3 * g;  // 24-B element, 8-B aligned
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const h2v lo = {hv[4 * i], hv[4 * i + 1]}, hi = {hv[4 * i + 2], hv[4 * i + 3]};
+                o[i] = make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
+            }
+            continue;
+        }
         float out[6];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -2302,6 +2385,21 @@ hipError_t launch_march_vt(bool shade, bool count, const MarchParams &p, hipStre
                  : launch_march_t<VT, false, false, false>(p, s);
 }
 
+// The f32 volume with the binary16 difference field (MarchParams::grad_half; shaded launches
+// that read the field, not LDS-staged): the field variants of launch_march_vt.
+template <typename VT>
+hipError_t launch_march_half_field(bool count, const MarchParams &p, hipStream_t s)
+{
+    if (p.pair) return launch_pair_t<VT, true, true>(p, s);
+    if (p.pipelined && !count && !p.skip_empty && p.tf_n <= kTfLds)
+        return launch_march_t<VT, true, false, false, true, true>(p, s);
+    if (p.skip_empty)
+        return count ? launch_march_t<VT, true, true, true, true>(p, s)
+                     : launch_march_t<VT, true, false, true, true>(p, s);
+    return count ? launch_march_t<VT, true, true, false, true>(p, s)
+                 : launch_march_t<VT, true, false, false, true>(p, s);
+}
+
 // The f32 volume's GeomAlt copy (kAltFlag) serves full-frame launches without skip-empty, the
 // difference field, lane groups or LDS staging (the host picks it for oblique and sparse views
 // only): single-stage or pipelined, shaded (stencil gradient) or not.
@@ -2381,7 +2479,10 @@ hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &
         case ST_I8 | kQuadFlag: return launch_march_vt<Quad8<int8_t>>(shade, count, p, stream);
         case ST_U16: return launch_march_vt<uint16_t>(shade, count, p, stream);
         case ST_I16: return launch_march_vt<int16_t>(shade, count, p, stream);
-        case ST_F32: return launch_march_vt<float>(shade, count, p, stream);
+        case ST_F32:
+            if (shade && p.grad && p.grad_half && !p.lds)
+                return launch_march_half_field<F32H>(count, p, stream);
+            return launch_march_vt<float>(shade, count, p, stream);
         case ST_F32 | kAltFlag:
         case ST_F32 | kWideFlag:
             if (count || p.pair || p.lds || p.skip_empty || p.grad) return hipErrorInvalidValue;
@@ -2396,11 +2497,11 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
     // demangled names as rocprofv3 reports them (kernel-trace "Kernel_Name"); storage is the
     // layout code (8-bit yz-quads: the Quad8 instantiations)
     static const std::vector<std::string> names = [] {
-        const char *types[9] = {"unsigned char", "signed char", "unsigned short", "short", "float",
-                                "vr::Quad8<unsigned char>", "vr::Quad8<signed char>", "vr::F32Alt",
-                                "vr::F32Wide"};
+        const char *types[10] = {"unsigned char", "signed char", "unsigned short", "short", "float",
+                                 "vr::Quad8<unsigned char>", "vr::Quad8<signed char>", "vr::F32Alt",
+                                 "vr::F32Wide", "vr::F32H"};
         std::vector<std::string> v;
-        for (int t = 0; t < 9; ++t)
+        for (int t = 0; t < 10; ++t)
             for (int k = 0; k < 32; ++k) {
                 std::string n = std::string("void vr::(anonymous namespace)::march_kernel<") + types[t];
                 for (int bit = 4; bit >= 0; --bit) n += (k >> bit) & 1 ? ", true" : ", false";
@@ -2411,7 +2512,8 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
     if (storage & kQuadFlag) storage = 5 + (storage & 0xF);
     if (storage & kAltFlag) storage = 7;
     if (storage & kWideFlag) storage = 8;
-    if (storage < 0 || storage > 8) return "march_kernel<?>";
+    if (storage & kHalfFieldFlag) storage = 9;
+    if (storage < 0 || storage > 9) return "march_kernel<?>";
     const int k = (shade ? 16 : 0) + (count ? 8 : 0) + (skip ? 4 : 0) + (gf ? 2 : 0) + (pipe ? 1 : 0);
     return names[storage * 32 + k].c_str();
 }
@@ -2577,13 +2679,18 @@ hipError_t launch_brick_range(int storage, const void *bricks, uint32_t nbx, uin
 }
 
 hipError_t launch_grad_field(const float *bricks, float *grad, uint32_t nx, uint32_t ny,
-                             uint32_t nz, hipStream_t s)
+                             uint32_t nz, bool half, int scale_log2, hipStream_t s)
 {
     const uint32_t nbx = bricks_for(nx, 0, ST_F32), nby = bricks_for(ny, 1, ST_F32),
                    nbz = bricks_for(nz, 2, ST_F32);
     const size_t total = (size_t)nbx * nby * nbz;  // bricks
-    hipLaunchKernelGGL(grad_field_kernel, dim3(grid_bricks(total)), dim3(256), 0, s, bricks, grad,
-                       nx, ny, nz, nbx, nby, total);
+    const float scale = std::ldexp(1.0f, scale_log2);
+    if (half)
+        hipLaunchKernelGGL(grad_field_kernel<true>, dim3(grid_bricks(total)), dim3(256), 0, s,
+                           bricks, grad, nx, ny, nz, nbx, nby, total, scale);
+    else
+        hipLaunchKernelGGL(grad_field_kernel<false>, dim3(grid_bricks(total)), dim3(256), 0, s,
+                           bricks, grad, nx, ny, nz, nbx, nby, total, scale);
     return hipGetLastError();
 }
 
