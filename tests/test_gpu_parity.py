@@ -478,9 +478,10 @@ def test_f32_gradient_field_equals_stencil_gradient(rp):
 
 def test_sparse_views_take_the_stencil_gradient(rp):
     """Launch policy (vr_api.hip use_grad_field): a shaded f32 frame reads the difference
-    field on dense-row views (the frame-filling r = 1.6 view, 0.6 voxels per pixel here) and
-    forms the gradient from the density stencil elsewhere (the reference's default camera,
-    r = 3, 1.2 voxels per pixel here).  Both match the oracle."""
+    field on dense-row views (the frame-filling r = 1.6 view, 0.6 voxels per pixel here), on
+    axis-aligned side views when the field is binary16, and forms the gradient from the
+    density stencil elsewhere (the reference's default camera, r = 3, 1.2 voxels per pixel
+    here).  All match the oracle (the field frames its binary16 restatement bit for bit)."""
     W, H = 192, 120
     rp.framebuffer_size_changed(W, H)
     vol = synth.gaussians_numpy((64, 64, 64), seed=21).astype(np.float32)
@@ -488,12 +489,17 @@ def test_sparse_views_take_the_stencil_gradient(rp):
     tf = synth.tf_band(0.15, 0.9)
     rp.transfer_function_changed(tf)
     p = vr_amd.default_params(shading=1)
-    for camname, field in (("fill", True), ("default", False), ("fill", True)):
-        cam = synth.camera(camname).to_vr_camera()
+    side = vr_amd.make_camera(radius=1.6, rotate=(360.0, 0.0))  # image x along the bricks' z
+    for camname, field in (("fill", True), ("default", False), ("side", True), ("fill", True)):
+        cam = (side if camname == "side" else synth.camera(camname)).to_vr_camera()
         img = rp.render(cam, p, vr_amd.OUT_RGBA32F)
         name = rp.kernel_name(p)
         gf = "<vr::F32H, true, false, false, true," in name
         assert gf == field, (camname, name)
+        if camname == "side":  # the side view reads the field in binary16 only
+            pe = vr_amd.default_params(shading=1, exact_gradient=1)
+            rp.render(cam, pe)
+            assert "<float, true, false, false, false," in rp.kernel_name(pe), rp.kernel_name(pe)
         ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p)
         check(img, ref)
         ref16, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p,
@@ -687,12 +693,13 @@ def test_non_integer_uploads_stay_f32(rp):
 
 def test_alt_geometry_copy_bit_identical(rp):
     """f32 volumes keep further copies in alternative brick geometries that oblique views
-    (7x15x8 cells, kernel tag F32Alt) and sparse views (15x15x8, F32Wide) read (vr_api.hip
-    want_alt): the frames are byte-identical to the 8^3 bricks' -- unshaded and shaded (stencil
-    gradient across every geometry's brick boundaries), single stage and pipelined -- the
-    launch policy picks the oblique copy for the diagonal view, the sparse one for the
-    reference's default camera and neither for the frame-filling view, and a volume change
-    rebuilds them."""
+    (7x15x8 cells, kernel tag F32Alt) and sparse views (15x15x8, F32Wide; or plain one-voxel
+    elements, F32P) read (vr_api.hip want_alt): the frames are byte-identical to the 8^3
+    bricks' -- unshaded and shaded (stencil gradient across every geometry's brick
+    boundaries), single stage and pipelined -- the
+    launch policy picks the oblique copy for the diagonal view, a sparse one for the
+    reference's default camera (z-pairs shaded, plain unshaded) and neither for the
+    frame-filling view, and a volume change rebuilds them."""
     W, H = 160, 120
     rp.framebuffer_size_changed(W, H)
     tf = synth.tf_band(0.15, 0.9)
@@ -710,16 +717,21 @@ def test_alt_geometry_copy_bit_identical(rp):
                     p = vr_amd.default_params(shading=shading, ert_eps=1e-5)
                     with rp.knobs(pipeline=pipe, grad_field=0, alt_geometry=0):
                         a = rp.render(c, p, vr_amd.OUT_RGBA32F)
-                    for alt, tag in ((1, "F32Alt"), (2, "F32Wide")):
+                    for alt, tag in ((1, "F32Alt"), (2, "F32Wide"), (3, "F32P")):
                         with rp.knobs(pipeline=pipe, grad_field=0, alt_geometry=alt):
                             b = rp.render(c, p, vr_amd.OUT_RGBA32F)
                             assert tag in rp.kernel_name(p)
                         assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), \
                             (seed, camname, shading, pipe, tag)
-            rp.render(c, vr_amd.default_params())  # the policy's own choice for this view
-            name = rp.kernel_name(vr_amd.default_params())
-            picked = "F32Alt" if "F32Alt" in name else ("F32Wide" if "F32Wide" in name else None)
-            assert picked == want[camname], (camname, name)
+            for shading in (0, 1):  # the policy's own choice for this view
+                p = vr_amd.default_params(shading=shading, exact_gradient=1)
+                rp.render(c, p)
+                name = rp.kernel_name(p)
+                picked = next((t for t in ("F32Alt", "F32Wide", "F32P") if t in name), None)
+                w = want[camname]
+                if w == "F32Wide" and not shading:
+                    w = "F32P"  # sparse and unshaded: the plain copy
+                assert picked == w, (camname, shading, name)
         ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, synth.camera("default").to_vr_camera(),
                                W, H, vr_amd.default_params(shading=1, ert_eps=1e-5))
         check(rp.render(synth.camera("default").to_vr_camera(), vr_amd.default_params(shading=1, ert_eps=1e-5)), ref)

@@ -46,7 +46,7 @@ struct vr_ctx {
         void *bricks = nullptr;
         size_t bytes = 0;
         bool valid = false, failed = false;
-    } alt[2];
+    } alt[3];
     uint32_t nx = 1, ny = 1, nz = 1;
     float vmin = 0.0f, vmax = 1.0f;
     // transfer function (decoded, linear float RGBA)
@@ -527,12 +527,19 @@ bool view_dense_rows(const double *inv, uint32_t W, uint32_t nx, uint32_t ny, ui
 // ray already holds.  C3, 3 frames in flight, ms per frame (field -> stencil + pipelined;
 // profiles/r02/sparse_view_grad/): default camera r = 3 0.363 -> 0.302, diagonal 0.812 ->
 // 0.770, side 0.600 -> 0.587; the fill view keeps the field (stencil: 0.500 -> 0.565).
+// With the binary16 field (half: vr_params.exact_gradient == 0, 3 loads per shaded sample)
+// the axis-aligned views that are neither oblique nor sparse (want_alt keeps them on the 8^3
+// bricks: the side views) read the field too; the diagonal and the default camera keep the
+// stencil and their alternative copies.  C3, 3 frames in flight, ms per frame, two rounds
+// (profiles/r03/field_views/): side 0.566 / 0.563 -> 0.541 / 0.542; diagonal 0.651 -> 0.80 and
+// default camera 0.244 -> 0.307 with the field, so those stay.
 // Knob VR_KNOB_GRAD_FIELD 0 / 1: the stencil / the field for every view (A/B, tests).
-bool use_grad_field(const vr_ctx *c)
+constexpr double kAltAlign = 0.9, kAltSpan = 0.8;
+bool use_grad_field(const vr_ctx *c, bool half)
 {
     if (c->storage != ST_F32) return false;
     if (c->knobs.grad_field >= 0) return c->knobs.grad_field == 1;
-    return c->dense_rows;
+    return c->dense_rows || (half && c->axis_align >= kAltAlign && c->pixel_span <= kAltSpan);
 }
 
 // Pipelined march (two samples of a ray in flight, vr_kernels.hip PIPE): for launches of
@@ -700,7 +707,7 @@ int ensure_skip(vr_ctx *c, MarchParams &P, hipStream_t s)
 // field in place after the device has drained (frames in flight may still read it).
 void ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s, bool half)
 {
-    if (!use_grad_field(c)) return;
+    if (!use_grad_field(c, half)) return;
     const int k = half ? field_scale_log2(c->vmin, c->vmax) : 0;
     if (c->grad_valid && (c->grad_half != half || c->grad_scale_log2 != k)) {
         if (hipDeviceSynchronize() != hipSuccess) {
@@ -768,9 +775,16 @@ int ensure_derived(vr_ctx *c, const vr_params *p, MarchParams &P, hipStream_t s)
 // (7x15x8), shaded default camera r = 3 0.34 (8^3) -> 0.31 (7x7x8) -> 0.28 (15x15x8); the
 // frame-filling, side and top views are 2-4% faster in 8^3 and stay there.  Not for
 // skip-empty, difference-field, lane-group or LDS-staged launches (the 8^3 copy keeps those
-// structures).  Returns the layout code to launch: c->layout, or ST_F32 | kAltFlag / kWideFlag.
-// Knob VR_KNOB_ALT_GEOMETRY: 0 never, 1 the oblique copy, 2 the sparse copy.
-constexpr double kAltAlign = 0.9, kAltSpan = 0.8;
+// structures).  Returns the layout code to launch: c->layout, or ST_F32 | kAltFlag / kWideFlag
+// / kPlainF32Flag.  Knob VR_KNOB_ALT_GEOMETRY: 0 never, 1 the oblique copy, 2 the z-pair sparse
+// copy, 3 the plain f32 copy.
+// Sparse views read the whole copy from HBM every frame, so unshaded they take the plain f32
+// copy (kPlainF32Flag, 15^3-cell bricks, 1.2x the voxels: 0.65 GB for 512^3 against 1.37 GB of
+// z-pairs); shaded, the stencil gradient's extra loads cost more there than the bytes save.
+// C3 volume, default camera r = 3, 3 frames in flight, ms per frame, two rounds
+// (profiles/r03/plain_copy/): unshaded 0.205 / 0.208 (15x15x8 z-pairs) -> 0.191 / 0.191
+// (plain); shaded 0.256 / 0.260 -> 0.260 / 0.262.  Plain bricks of 15x15x7 or 31x15x7 cells
+// measured 1-2% slower than 15^3.
 int want_alt(const vr_ctx *c, const vr_params *p, const MarchParams &P)
 {
     if (c->layout != ST_F32 || p->skip_empty || P.lds || P.pair || P.grad) return c->layout;
@@ -778,11 +792,16 @@ int want_alt(const vr_ctx *c, const vr_params *p, const MarchParams &P)
     if (c->knobs.alt >= 0)
         which = c->knobs.alt;
     else if (!c->dense_rows)
-        which = c->axis_align < kAltAlign ? 1 : (c->pixel_span > kAltSpan ? 2 : 0);
-    return which == 1 ? (ST_F32 | kAltFlag) : (which == 2 ? (ST_F32 | kWideFlag) : c->layout);
+        which = c->axis_align < kAltAlign ? 1 : (c->pixel_span > kAltSpan ? (p->shading ? 2 : 3) : 0);
+    switch (which) {
+        case 1: return ST_F32 | kAltFlag;
+        case 2: return ST_F32 | kWideFlag;
+        case 3: return ST_F32 | kPlainF32Flag;
+        default: return c->layout;
+    }
 }
 
-int alt_index(int layout) { return (layout & kAltFlag) ? 0 : 1; }
+int alt_index(int layout) { return (layout & kAltFlag) ? 0 : ((layout & kWideFlag) ? 1 : 2); }
 
 // Bytes of the copy of the current volume in layout `lay`.
 size_t alt_bytes_for(const vr_ctx *c, int lay)
@@ -1016,7 +1035,7 @@ bool knob_value_ok(int knob, int v)
         case VR_KNOB_PAIR_LANES: return v == 0 || v == 2 || v == 4;
         case VR_KNOB_LDS:
         case VR_KNOB_NARROW: return v == 0 || v == 1;
-        case VR_KNOB_ALT_GEOMETRY: return v >= -1 && v <= 2;
+        case VR_KNOB_ALT_GEOMETRY: return v >= -1 && v <= 3;
         case VR_KNOB_TILE_ORDER: return v >= 0 && v <= 4;
         default: return v >= -1 && v <= 1;
     }
@@ -1814,7 +1833,8 @@ const char *vr_kernel_name(const vr_ctx *c, const vr_params *p)
     if (!c) return "";
     if (is_group(c)) return vr_kernel_name(c->members[0], p);
     // the variant the next vr_render_device launches (after a shaded frame built the field)
-    const bool gf = p && p->shading && use_grad_field(c) && c->grad && c->grad_valid;
+    const bool gf = p && p->shading && use_grad_field(c, p->exact_gradient == 0) && c->grad &&
+                    c->grad_valid;
     // the full frame (row_block 16, one rank), as vr_render launches it
     const uint32_t tiles = ((c->width + 15) / 16) * ((c->height + kMarchRows - 1) / kMarchRows);
     const bool pipe = use_pipeline(p && p->shading, tiles, c) &&

@@ -85,6 +85,10 @@ template <>
 struct VoxOf<F32H> {
     using type = float;
 };
+template <>
+struct VoxOf<F32P> {
+    using type = float;
+};
 template <typename VT>
 using Vox = typename VoxOf<VT>::type;
 template <typename VT>
@@ -95,17 +99,21 @@ constexpr bool kHalfField = std::is_same<VT, F32H>::value;
 // f32 z-pair elements (8^3 bricks, or GeomAlt bricks for F32Alt)
 template <typename VT>
 constexpr bool kZPair = std::is_same<Vox<VT>, float>::value;
+// f32 voxels one per element (the F32P copy, or every f32 volume in VR_F32_PLAIN builds)
+template <typename VT>
+constexpr bool kPlainF32 = std::is_same<VT, F32P>::value || (kZPair<VT> && VR_F32_PLAIN);
 // 8-bit volumes stored one voxel per element (VR_U8_PLAIN, vr_internal.h)
 template <typename VT>
 constexpr bool kPlainByte = sizeof(VT) == 1 && VR_U8_PLAIN && !kIsQuad8<VT>;
 template <typename VT>
-constexpr int kElemBytes = kZPair<VT> ? 4 * (int)kF32VoxelsPerElement
+constexpr int kElemBytes = kZPair<VT> ? (kPlainF32<VT> ? 4 : 8)
                                       : (kPlainByte<VT> ? 1 : 4 * (int)sizeof(VT));
 template <typename VT>
 using GeomOf = std::conditional_t<kPlainByte<VT>, GeomByte,
                                   std::conditional_t<std::is_same<VT, F32Alt>::value, GeomAlt,
                                   std::conditional_t<std::is_same<VT, F32Wide>::value, GeomWideRows,
-                                                     GeomWide>>>;
+                                  std::conditional_t<std::is_same<VT, F32P>::value, GeomPlainRows,
+                                                     GeomWide>>>>;
 template <typename VT>
 constexpr int kQuadWords = sizeof(VT) == 1 ? 1 : 2;
 
@@ -216,7 +224,7 @@ __device__ __forceinline__ f2a zpair_load1(const char *__restrict__ base, size_t
 
 // Global loads one Cell8::load issues.
 template <typename VT>
-constexpr int kCellLoads = kZPair<VT> ? (VR_F32_PLAIN ? 4 : 2) : (kPlainByte<VT> ? 2 : 1);
+constexpr int kCellLoads = kZPair<VT> ? (kPlainF32<VT> ? 4 : 2) : (kPlainByte<VT> ? 2 : 1);
 
 // s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt bits [3:0] + [15:14], expcnt and lgkmcnt left at
 // their no-wait maxima).  The pipelined march places it, in code every active lane runs, where
@@ -243,7 +251,7 @@ struct CellRaw {  // generic: the decoded cell itself (loaded and decoded togeth
     float v[8];
 };
 template <typename VT>
-struct CellRaw<VT, std::enable_if_t<kZPair<VT> && !VR_F32_PLAIN>> {
+struct CellRaw<VT, std::enable_if_t<kZPair<VT> && !kPlainF32<VT>>> {
     f4a r0, r1;  // rows y and y + 1: elements x, x + 1 as z-pairs
 };
 template <typename VT>
@@ -259,7 +267,7 @@ struct Cell8 {
     static __device__ __forceinline__ void issue(CellRaw<VT> &w, const char *__restrict__ base,
                                                  size_t e)
     {
-        if constexpr (kZPair<VT> && !VR_F32_PLAIN) {
+        if constexpr (kZPair<VT> && !kPlainF32<VT>) {
             w.r0 = zpair_load2(base, e);
             w.r1 = zpair_load2(base, e + GeomOf<VT>::Row);
         } else if constexpr (kPlainByte<VT> && GeomByte::EX == 8) {
@@ -276,7 +284,7 @@ struct Cell8 {
     }
     __device__ __forceinline__ void decode(const CellRaw<VT> &w)
     {
-        if constexpr (kZPair<VT> && !VR_F32_PLAIN) {
+        if constexpr (kZPair<VT> && !kPlainF32<VT>) {
             v[0] = w.r0.x;
             v[4] = w.r0.y;
             v[1] = w.r0.z;
@@ -302,11 +310,12 @@ struct Cell8 {
     }
     __device__ __forceinline__ void load(const char *__restrict__ base, size_t e)
     {
-        if constexpr (kZPair<VT> && VR_F32_PLAIN) {  // rows (y, z), (y+1, z), (y, z+1), (y+1, z+1)
+        if constexpr (kPlainF32<VT>) {  // rows (y, z), (y+1, z), (y, z+1), (y+1, z+1)
+            using G = GeomOf<VT>;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const f2a q = *reinterpret_cast<const f2a *>(
-                    base + (e + (size_t)((r & 1) * GeomWide::Row + (r >> 1) * GeomWide::Slice)) * 4);
+                    base + (e + (size_t)((r & 1) * G::Row + (r >> 1) * G::Slice)) * 4);
                 v[2 * r] = q.x;
                 v[2 * r + 1] = q.y;
             }
@@ -435,7 +444,7 @@ __device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e
     (void)dzp;
     const float *v = c.v;
     float Dx[8], Dy[8], Dz[8];
-    if constexpr (kZPair<VT> && VR_F32_PLAIN) {
+    if constexpr (kPlainF32<VT>) {
         auto ld1 = [&](long o) { return *reinterpret_cast<const float *>(base + (e + o) * 4); };
         auto ld2 = [&](long o) { return *reinterpret_cast<const f2a *>(base + (e + o) * 4); };
 #pragma unroll
@@ -1936,7 +1945,7 @@ __global__ __launch_bounds__(256) void brick_kernel(const SrcT *__restrict__ src
             return (V)src[(size_t)xx + (size_t)nx * ((size_t)yy + (size_t)ny * (size_t)zz)];
         };
         // one store per element (a u8 quad is one dword, not four byte stores)
-        if constexpr ((zpair && VR_F32_PLAIN) || kPlainByte<DstT>) {
+        if constexpr (kPlainF32<DstT> || kPlainByte<DstT>) {
             dst[g] = at(x, y, z);
         } else if constexpr (zpair) {
             reinterpret_cast<float2 *>(dst)[g] = make_float2(at(x, y, z), at(x, y, z + 1));
@@ -2462,6 +2471,7 @@ hipError_t brick_from(const void *src, void *dst, uint32_t nx, uint32_t ny, uint
         case ST_I16: hipLaunchKernelGGL((brick_kernel<SrcT, int16_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (int16_t *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_F32 | kAltFlag: hipLaunchKernelGGL((brick_kernel<SrcT, F32Alt>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_F32 | kWideFlag: hipLaunchKernelGGL((brick_kernel<SrcT, F32Wide>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
+        case ST_F32 | kPlainF32Flag: hipLaunchKernelGGL((brick_kernel<SrcT, F32P>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
         default: hipLaunchKernelGGL((brick_kernel<SrcT, float>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
     }
     return hipGetLastError();
@@ -2485,7 +2495,9 @@ hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &
             return launch_march_vt<float>(shade, count, p, stream);
         case ST_F32 | kAltFlag:
         case ST_F32 | kWideFlag:
+        case ST_F32 | kPlainF32Flag:
             if (count || p.pair || p.lds || p.skip_empty || p.grad) return hipErrorInvalidValue;
+            if (storage & kPlainF32Flag) return launch_march_alt<F32P>(shade, p, stream);
             return (storage & kAltFlag) ? launch_march_alt<F32Alt>(shade, p, stream)
                                         : launch_march_alt<F32Wide>(shade, p, stream);
         default: return hipErrorInvalidValue;
@@ -2497,11 +2509,11 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
     // demangled names as rocprofv3 reports them (kernel-trace "Kernel_Name"); storage is the
     // layout code (8-bit yz-quads: the Quad8 instantiations)
     static const std::vector<std::string> names = [] {
-        const char *types[10] = {"unsigned char", "signed char", "unsigned short", "short", "float",
+        const char *types[11] = {"unsigned char", "signed char", "unsigned short", "short", "float",
                                  "vr::Quad8<unsigned char>", "vr::Quad8<signed char>", "vr::F32Alt",
-                                 "vr::F32Wide", "vr::F32H"};
+                                 "vr::F32Wide", "vr::F32H", "vr::F32P"};
         std::vector<std::string> v;
-        for (int t = 0; t < 10; ++t)
+        for (int t = 0; t < 11; ++t)
             for (int k = 0; k < 32; ++k) {
                 std::string n = std::string("void vr::(anonymous namespace)::march_kernel<") + types[t];
                 for (int bit = 4; bit >= 0; --bit) n += (k >> bit) & 1 ? ", true" : ", false";
@@ -2513,7 +2525,8 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
     if (storage & kAltFlag) storage = 7;
     if (storage & kWideFlag) storage = 8;
     if (storage & kHalfFieldFlag) storage = 9;
-    if (storage < 0 || storage > 9) return "march_kernel<?>";
+    if (storage & kPlainF32Flag) storage = 10;
+    if (storage < 0 || storage > 10) return "march_kernel<?>";
     const int k = (shade ? 16 : 0) + (count ? 8 : 0) + (skip ? 4 : 0) + (gf ? 2 : 0) + (pipe ? 1 : 0);
     return names[storage * 32 + k].c_str();
 }
