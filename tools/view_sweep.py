@@ -51,11 +51,11 @@ def main():
     args = ap.parse_args()
     W, H = (int(x) for x in args.size.split("x"))
     rp = vr_amd.OffscreenPass(W, H)
-    rp.generate_volume((args.n,) * 3, np.dtype(args.dtype), seed=2024)
-    rp.transfer_function_changed(synth.TFS[args.tf]())
-    for kv in args.knob:
+    for kv in args.knob:  # before the upload: layout knobs (u8_layout) apply to it
         k, v = kv.split("=")
         rp.set_knob(k, int(v))
+    rp.generate_volume((args.n,) * 3, np.dtype(args.dtype), seed=2024)
+    rp.transfer_function_changed(synth.TFS[args.tf]())
     out = torch.empty((H + 16, W), dtype=torch.int32, device="cuda")
     streams = [torch.cuda.Stream() for _ in range(args.inflight)]
     outs = [torch.empty((H + 16, W), dtype=torch.int32, device="cuda") for _ in streams]
