@@ -130,8 +130,7 @@ def test_native_dtypes(rp, np_dtype):
 @pytest.mark.parametrize("np_dtype", [np.uint8, np.int8])
 def test_byte_layouts_plain_and_quad_identical(rp, np_dtype):
     """8-bit volumes are bricked as yz-quads up to kQuadMaxVoxels voxels and as plain 7x8x8-cell
-    bricks above (vr_internal.h), or as z-pairs in 3x8x8-cell bricks (ZPair8, knob value 2);
-    the layouts, forced through the u8_layout knob at upload, read
+    bricks above (vr_internal.h); both layouts, forced through the u8_layout knob at upload, read
     back the volume exactly and render the same bytes -- single lane, pipelined, lane pairs,
     shaded (stencil gradient across brick boundaries and the border), skip-empty -- and match
     the oracle."""
@@ -146,12 +145,10 @@ def test_byte_layouts_plain_and_quad_identical(rp, np_dtype):
               dict(shading=0, skip_empty=1), dict(shading=1, skip_empty=1)]
     envs = [dict(pipeline=0, pair=0), dict(pipeline=1, pair=0), dict(pair=1, pair_lanes=2)]
     out = {}
-    knob = {"quad": 1, "plain": 0, "zpair": 2}
-    for layout in ("quad", "plain", "zpair"):
-        with rp.knobs(u8_layout=knob[layout]):
+    for layout in ("quad", "plain"):
+        with rp.knobs(u8_layout=1 if layout == "quad" else 0):
             rp.volume_dataset_changed(synth.dataset(vol))
         assert ("Quad8" in rp.kernel_name(vr_amd.default_params())) == (layout == "quad")
-        assert ("ZPair8" in rp.kernel_name(vr_amd.default_params())) == (layout == "zpair")
         rp.transfer_function_changed(tf)
         assert np.array_equal(rp.read_volume(), vol.astype(np.float32)), layout
         for camname in ("rotA", "fill_oblique"):
@@ -162,9 +159,8 @@ def test_byte_layouts_plain_and_quad_identical(rp, np_dtype):
                         img = rp.render(cam, vr_amd.default_params(ert_eps=1e-4, **c), vr_amd.OUT_RGBA32F)
                     key = (camname, tuple(c.items()), tuple(env.items()))
                     out.setdefault(key, []).append(img)
-    for key, (a, b, z) in out.items():
+    for key, (a, b) in out.items():
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), key
-        assert np.array_equal(a.view(np.uint32), z.view(np.uint32)), key
     cam = synth.camera("rotA").to_vr_camera()
     ds = synth.dataset(vol)
     for shading in (0, 1):

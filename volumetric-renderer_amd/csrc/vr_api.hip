@@ -326,7 +326,6 @@ struct SplitMix {
 int brick_layout(const vr_ctx *c, int st, uint32_t nx, uint32_t ny, uint32_t nz)
 {
     if (!VR_U8_PLAIN || (st != ST_U8 && st != ST_I8)) return st;
-    if (c->knobs.u8_layout == 2) return st | kZPair8Flag;
     bool quad = (size_t)nx * ny * nz <= kQuadMaxVoxels;
     if (c->knobs.u8_layout >= 0) quad = c->knobs.u8_layout == 1;
     return quad ? (st | kQuadFlag) : st;
@@ -1037,7 +1036,6 @@ bool knob_value_ok(int knob, int v)
         case VR_KNOB_LDS:
         case VR_KNOB_NARROW: return v == 0 || v == 1;
         case VR_KNOB_ALT_GEOMETRY: return v >= -1 && v <= 3;
-        case VR_KNOB_U8_LAYOUT: return v >= -1 && v <= 2;
         case VR_KNOB_TILE_ORDER: return v >= 0 && v <= 4;
         default: return v >= -1 && v <= 1;
     }

@@ -143,19 +143,6 @@ template <typename T>
 struct Quad8 {
     T v;
 };
-// 8-bit voxels in z-pair elements {v(z), v(z+1)} (2 B), bricks of 3 x 8 x 8 cells: a brick row
-// is 4 elements = 8 B, so rows y and y + 1 of a cell are 16 contiguous bytes and ONE 16-B load
-// holds all 8 voxels of a sample (the plain 7x8x8 bricks take two: one per z slice); 3.4x the
-// voxels against 1.45x.  Layout code st | kZPair8Flag, kernel tag ZPair8<T>.
-constexpr int kZPair8Flag = 0x200;
-#ifndef VR_ZP8_BRICK_CELLS
-#define VR_ZP8_BRICK_CELLS 3, 8, 8
-#endif
-using GeomZP8 = BrickGeom<VR_ZP8_BRICK_CELLS>;
-template <typename T>
-struct ZPair8 {
-    T v;
-};
 // Alternative f32 geometries: further resident copies of an f32 volume in bricks whose z-pair
 // rows never straddle a 128-B line, for the views where a wavefront's lanes sit on different
 // brick rows and every straddled line is another L1 miss:
@@ -220,7 +207,6 @@ inline bool byte_storage(int st)
 inline size_t voxels_per_element(int st)
 {
     if (st & kPlainF32Flag) return 1;
-    if (st & kZPair8Flag) return 2;
     return (st & 0xF) == ST_F32 ? kF32VoxelsPerElement : (byte_storage(st) ? 1 : 4);
 }
 inline size_t element_size(int st) { return storage_size(st) * voxels_per_element(st); }
@@ -230,7 +216,6 @@ inline int brick_cells(int st, int a)
     if (st & kAltFlag) return GeomAlt::cells(a);
     if (st & kWideFlag) return GeomWideRows::cells(a);
     if (st & kPlainF32Flag) return GeomPlainRows::cells(a);
-    if (st & kZPair8Flag) return GeomZP8::cells(a);
     return byte_storage(st) ? GeomByte::cells(a) : GeomWide::cells(a);
 }
 inline size_t brick_elems(int st)
@@ -238,7 +223,6 @@ inline size_t brick_elems(int st)
     if (st & kAltFlag) return GeomAlt::Elems;
     if (st & kWideFlag) return GeomWideRows::Elems;
     if (st & kPlainF32Flag) return GeomPlainRows::Elems;
-    if (st & kZPair8Flag) return GeomZP8::Elems;
     return byte_storage(st) ? GeomByte::Elems : GeomWide::Elems;
 }
 

@@ -73,10 +73,6 @@ template <typename T>
 struct VoxOf<Quad8<T>> {
     using type = T;
 };
-template <typename T>
-struct VoxOf<ZPair8<T>> {
-    using type = T;
-};
 template <>
 struct VoxOf<F32Alt> {
     using type = float;
@@ -97,13 +93,6 @@ template <typename VT>
 using Vox = typename VoxOf<VT>::type;
 template <typename VT>
 constexpr bool kIsQuad8 = is_quad8<VT>::value;
-template <typename VT>
-struct is_zpair8 : std::false_type {};
-template <typename T>
-struct is_zpair8<ZPair8<T>> : std::true_type {};
-// 8-bit z-pair elements in 3x8x8-cell bricks (vr_internal.h kZPair8Flag)
-template <typename VT>
-constexpr bool kZPair8 = is_zpair8<VT>::value;
 // the f32 volume read with the binary16 difference field (MarchParams::grad_half)
 template <typename VT>
 constexpr bool kHalfField = std::is_same<VT, F32H>::value;
@@ -115,16 +104,16 @@ template <typename VT>
 constexpr bool kPlainF32 = std::is_same<VT, F32P>::value || (kZPair<VT> && VR_F32_PLAIN);
 // 8-bit volumes stored one voxel per element (VR_U8_PLAIN, vr_internal.h)
 template <typename VT>
-constexpr bool kPlainByte = sizeof(VT) == 1 && VR_U8_PLAIN && !kIsQuad8<VT> && !kZPair8<VT>;
+constexpr bool kPlainByte = sizeof(VT) == 1 && VR_U8_PLAIN && !kIsQuad8<VT>;
 template <typename VT>
 constexpr int kElemBytes = kZPair<VT> ? (kPlainF32<VT> ? 4 : 8)
-                                      : (kPlainByte<VT> ? 1 : (kZPair8<VT> ? 2 : 4 * (int)sizeof(VT)));
+                                      : (kPlainByte<VT> ? 1 : 4 * (int)sizeof(VT));
 template <typename VT>
 using GeomOf = std::conditional_t<kPlainByte<VT>, GeomByte,
                                   std::conditional_t<std::is_same<VT, F32Alt>::value, GeomAlt,
                                   std::conditional_t<std::is_same<VT, F32Wide>::value, GeomWideRows,
                                   std::conditional_t<std::is_same<VT, F32P>::value, GeomPlainRows,
-                                  std::conditional_t<kZPair8<VT>, GeomZP8, GeomWide>>>>>;
+                                                     GeomWide>>>>;
 template <typename VT>
 constexpr int kQuadWords = sizeof(VT) == 1 ? 1 : 2;
 
@@ -236,7 +225,6 @@ __device__ __forceinline__ f2a zpair_load1(const char *__restrict__ base, size_t
 // Global loads one Cell8::load issues.
 template <typename VT>
 constexpr int kCellLoads = kZPair<VT> ? (kPlainF32<VT> ? 4 : 2) : (kPlainByte<VT> ? 2 : 1);
-static_assert(GeomZP8::EX == 4, "8-bit z-pair rows are 4 elements (8 B)");
 
 // s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt bits [3:0] + [15:14], expcnt and lgkmcnt left at
 // their no-wait maxima).  The pipelined march places it, in code every active lane runs, where
@@ -271,11 +259,6 @@ struct CellRaw<VT, std::enable_if_t<kPlainByte<VT> && GeomByte::EX == 8>> {
     u4a q0, q1;    // slices z and z + 1: the 16 bytes from the 4-aligned address at or below e
     uint32_t sh;   // e mod 4
 };
-template <typename VT>
-struct CellRaw<VT, std::enable_if_t<kZPair8<VT>>> {
-    u4a q;        // rows y and y + 1 (8 B each) from the row start
-    uint32_t sh;  // byte offset of element x in the row: 2 (x mod 4)
-};
 
 template <typename VT>
 struct Cell8 {
@@ -292,10 +275,6 @@ struct Cell8 {
             w.sh = (uint32_t)e & 3u;
             w.q0 = *reinterpret_cast<const u4a *>(base + a);
             w.q1 = *reinterpret_cast<const u4a *>(base + a + GeomByte::Slice);
-        } else if constexpr (kZPair8<VT>) {
-            // rows are 4 elements and bricks 4-element aligned: the row starts at e & ~3
-            w.sh = 2u * ((uint32_t)e & 3u);
-            w.q = *reinterpret_cast<const u4a *>(base + 2 * (e & ~(size_t)3));
         } else {
             Cell8 c;
             c.load(base, e);
@@ -324,20 +303,6 @@ struct Cell8 {
                 v[2 * r] = byte_value<VT>(q[r], 0);
                 v[2 * r + 1] = byte_value<VT>(q[r], 1);
             }
-        } else if constexpr (kZPair8<VT>) {
-            // bytes {v(x,z), v(x,z+1), v(x+1,z), v(x+1,z+1)} of rows y and y + 1 (v_alignbyte
-            // shifts by sh mod 4 only: for x mod 4 = 2 the window is the row's second dword)
-            const bool upper = w.sh >= 4u;
-            const uint32_t r0 = __builtin_amdgcn_alignbyte(w.q.y, upper ? w.q.y : w.q.x, w.sh);
-            const uint32_t r1 = __builtin_amdgcn_alignbyte(w.q.w, upper ? w.q.w : w.q.z, w.sh);
-            v[0] = byte_value<VT>(r0, 0);  // index dx + 2 dy + 4 dz
-            v[4] = byte_value<VT>(r0, 1);
-            v[1] = byte_value<VT>(r0, 2);
-            v[5] = byte_value<VT>(r0, 3);
-            v[2] = byte_value<VT>(r1, 0);
-            v[6] = byte_value<VT>(r1, 1);
-            v[3] = byte_value<VT>(r1, 2);
-            v[7] = byte_value<VT>(r1, 3);
         } else {
 #pragma unroll
             for (int i = 0; i < 8; ++i) v[i] = w.v[i];
@@ -345,12 +310,6 @@ struct Cell8 {
     }
     __device__ __forceinline__ void load(const char *__restrict__ base, size_t e)
     {
-        if constexpr (kZPair8<VT>) {
-            CellRaw<VT> w;
-            issue(w, base, e);
-            decode(w);
-            return;
-        }
         if constexpr (kPlainF32<VT>) {  // rows (y, z), (y+1, z), (y, z+1), (y+1, z+1)
             using G = GeomOf<VT>;
 #pragma unroll
@@ -530,36 +489,6 @@ __device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e
         Dy[4] = v[6] - ym.y;  Dy[5] = v[7] - ym.w;  Dy[6] = yp.y - v[4];  Dy[7] = yp.w - v[5];
         Dz[0] = v[4] - zm0.x; Dz[1] = v[5] - zm0.z; Dz[2] = v[6] - zm1.x; Dz[3] = v[7] - zm1.z;
         Dz[4] = zp0.y - v[0]; Dz[5] = zp0.w - v[1]; Dz[6] = zp1.y - v[2]; Dz[7] = zp1.w - v[3];
-    } else if constexpr (kZPair8<VT>) {
-        // the 24 outer voxels one byte load each, byte h = dz of the z-pair element at offset
-        // o (8-bit shading is off the benchmarked path)
-        auto ld = [&](long o, int h) {
-            return byte_value<VT>((uint32_t)*reinterpret_cast<const uint8_t *>(base + 2 * (e + o) + h), 0);
-        };
-#pragma unroll
-        for (int dz_ = 0; dz_ < 2; ++dz_)
-#pragma unroll
-            for (int dy_ = 0; dy_ < 2; ++dy_) {
-                const int o = 2 * dy_ + 4 * dz_;
-                Dx[o] = v[o + 1] - ld(dxm + dy_ * S, dz_);
-                Dx[o + 1] = ld(dxp + dy_ * S, dz_) - v[o];
-            }
-#pragma unroll
-        for (int dz_ = 0; dz_ < 2; ++dz_)
-#pragma unroll
-            for (int dx_ = 0; dx_ < 2; ++dx_) {
-                const int o = dx_ + 4 * dz_;
-                Dy[o] = v[o + 2] - ld(dym + dx_, dz_);
-                Dy[o + 2] = ld(dyp + dx_, dz_) - v[o];
-            }
-#pragma unroll
-        for (int dy_ = 0; dy_ < 2; ++dy_)
-#pragma unroll
-            for (int dx_ = 0; dx_ < 2; ++dx_) {
-                const int o = dx_ + 2 * dy_;
-                Dz[o] = v[o + 4] - ld(dzm + dx_ + dy_ * S, 0);   // v(z - 1): element z - 1, byte 0
-                Dz[o + 4] = ld(S2 + dx_ + dy_ * S, 1) - v[o];   // v(z + 2): element z + 1, byte 1
-            }
     } else if constexpr (kPlainByte<VT>) {
         // the 24 outer voxels one byte load each (8-bit shading is off the benchmarked path)
         auto ld = [&](long o) {
@@ -2018,9 +1947,6 @@ __global__ __launch_bounds__(256) void brick_kernel(const SrcT *__restrict__ src
         // one store per element (a u8 quad is one dword, not four byte stores)
         if constexpr (kPlainF32<DstT> || kPlainByte<DstT>) {
             dst[g] = at(x, y, z);
-        } else if constexpr (kZPair8<DstT>) {
-            const uint32_t lo = (uint8_t)at(x, y, z), hi = (uint8_t)at(x, y, z + 1);
-            reinterpret_cast<uint16_t *>(dst)[g] = (uint16_t)(lo | (hi << 8));
         } else if constexpr (zpair) {
             reinterpret_cast<float2 *>(dst)[g] = make_float2(at(x, y, z), at(x, y, z + 1));
         } else {
@@ -2517,7 +2443,7 @@ __global__ __launch_bounds__(256) void unbrick_kernel(const Vox<T> *__restrict__
                                                      uint32_t z0, size_t count)
 {
     constexpr size_t vpe = std::is_same<T, float>::value ? kF32VoxelsPerElement
-                                                         : (kPlainByte<T> ? 1 : (kZPair8<T> ? 2 : 4));
+                                                         : (kPlainByte<T> ? 1 : 4);
     for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < count;
          g += (size_t)gridDim.x * blockDim.x) {
         const uint32_t x = (uint32_t)(g % nx);
@@ -2541,8 +2467,6 @@ hipError_t brick_from(const void *src, void *dst, uint32_t nx, uint32_t ny, uint
         case ST_I8: hipLaunchKernelGGL((brick_kernel<SrcT, int8_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (int8_t *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_U8 | kQuadFlag: hipLaunchKernelGGL((brick_kernel<SrcT, Quad8<uint8_t>>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (uint8_t *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_I8 | kQuadFlag: hipLaunchKernelGGL((brick_kernel<SrcT, Quad8<int8_t>>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (int8_t *)dst, nx, ny, nz, nbx, nby, total); break;
-        case ST_U8 | kZPair8Flag: hipLaunchKernelGGL((brick_kernel<SrcT, ZPair8<uint8_t>>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (uint8_t *)dst, nx, ny, nz, nbx, nby, total); break;
-        case ST_I8 | kZPair8Flag: hipLaunchKernelGGL((brick_kernel<SrcT, ZPair8<int8_t>>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (int8_t *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_U16: hipLaunchKernelGGL((brick_kernel<SrcT, uint16_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (uint16_t *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_I16: hipLaunchKernelGGL((brick_kernel<SrcT, int16_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (int16_t *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_F32 | kAltFlag: hipLaunchKernelGGL((brick_kernel<SrcT, F32Alt>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
@@ -2563,8 +2487,6 @@ hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &
         case ST_I8: return launch_march_vt<int8_t>(shade, count, p, stream);
         case ST_U8 | kQuadFlag: return launch_march_vt<Quad8<uint8_t>>(shade, count, p, stream);
         case ST_I8 | kQuadFlag: return launch_march_vt<Quad8<int8_t>>(shade, count, p, stream);
-        case ST_U8 | kZPair8Flag: return launch_march_vt<ZPair8<uint8_t>>(shade, count, p, stream);
-        case ST_I8 | kZPair8Flag: return launch_march_vt<ZPair8<int8_t>>(shade, count, p, stream);
         case ST_U16: return launch_march_vt<uint16_t>(shade, count, p, stream);
         case ST_I16: return launch_march_vt<int16_t>(shade, count, p, stream);
         case ST_F32:
@@ -2587,12 +2509,11 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
     // demangled names as rocprofv3 reports them (kernel-trace "Kernel_Name"); storage is the
     // layout code (8-bit yz-quads: the Quad8 instantiations)
     static const std::vector<std::string> names = [] {
-        const char *types[13] = {"unsigned char", "signed char", "unsigned short", "short", "float",
+        const char *types[11] = {"unsigned char", "signed char", "unsigned short", "short", "float",
                                  "vr::Quad8<unsigned char>", "vr::Quad8<signed char>", "vr::F32Alt",
-                                 "vr::F32Wide", "vr::F32H", "vr::F32P", "vr::ZPair8<unsigned char>",
-                                 "vr::ZPair8<signed char>"};
+                                 "vr::F32Wide", "vr::F32H", "vr::F32P"};
         std::vector<std::string> v;
-        for (int t = 0; t < 13; ++t)
+        for (int t = 0; t < 11; ++t)
             for (int k = 0; k < 32; ++k) {
                 std::string n = std::string("void vr::(anonymous namespace)::march_kernel<") + types[t];
                 for (int bit = 4; bit >= 0; --bit) n += (k >> bit) & 1 ? ", true" : ", false";
@@ -2605,8 +2526,7 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
     if (storage & kWideFlag) storage = 8;
     if (storage & kHalfFieldFlag) storage = 9;
     if (storage & kPlainF32Flag) storage = 10;
-    if (storage & kZPair8Flag) storage = 11 + (storage & 0xF);
-    if (storage < 0 || storage > 12) return "march_kernel<?>";
+    if (storage < 0 || storage > 10) return "march_kernel<?>";
     const int k = (shade ? 16 : 0) + (count ? 8 : 0) + (skip ? 4 : 0) + (gf ? 2 : 0) + (pipe ? 1 : 0);
     return names[storage * 32 + k].c_str();
 }
@@ -2636,7 +2556,6 @@ hipError_t launch_unbrick(int storage, const void *bricks, void *dst, uint32_t n
     switch (storage) {
         case ST_U8: case ST_I8: hipLaunchKernelGGL((unbrick_kernel<uint8_t>), dim3(g), dim3(256), 0, s, (const uint8_t *)bricks, (uint8_t *)dst, nx, ny, bx, by, z0, n); break;
         case ST_U8 | kQuadFlag: case ST_I8 | kQuadFlag: hipLaunchKernelGGL((unbrick_kernel<Quad8<uint8_t>>), dim3(g), dim3(256), 0, s, (const uint8_t *)bricks, (uint8_t *)dst, nx, ny, bx, by, z0, n); break;
-        case ST_U8 | kZPair8Flag: case ST_I8 | kZPair8Flag: hipLaunchKernelGGL((unbrick_kernel<ZPair8<uint8_t>>), dim3(g), dim3(256), 0, s, (const uint8_t *)bricks, (uint8_t *)dst, nx, ny, bx, by, z0, n); break;
         case ST_U16: case ST_I16: hipLaunchKernelGGL((unbrick_kernel<uint16_t>), dim3(g), dim3(256), 0, s, (const uint16_t *)bricks, (uint16_t *)dst, nx, ny, bx, by, z0, n); break;
         default: hipLaunchKernelGGL((unbrick_kernel<float>), dim3(g), dim3(256), 0, s, (const float *)bricks, (float *)dst, nx, ny, bx, by, z0, n); break;
     }
