@@ -300,7 +300,7 @@ float or_round_f16(float x)
         u &= ~0x1FFFu;
         memcpy(&r, &u, sizeof r);
     }
-    return x < 0.0f ? -r : r;
+    return copysignf(r, x);
 }
 
 static inline float dvox_f16(const vsrc *v, int nx, int ny, int nz, int x, int y, int z, int axis,

@@ -74,7 +74,12 @@ def tf_sample(lut, t):
 
 def render(vol, vmin, vmax, tf, view, cam_pos, width, height, smin=(0, 0, 0), smax=(1, 1, 1),
            step=0.005, ray_dist=1.8, clear=(0.11, 0.11, 0.11, 1.0), shading=False,
-           ka=0.3, kd=0.7, ks=0.25, spec_power=16):
+           ka=0.3, kd=0.7, ks=0.25, spec_power=16, grad_f16=False):
+    """grad_f16: the device's binary16 difference field (vr_params.exact_gradient = 0): each
+    per-voxel central difference D (float32) becomes float16(clip(D * 2^k, +-65504)), numpy's
+    round-to-nearest-even, k the largest power of two with (max(vmax,0) - min(vmin,0)) 2^k <=
+    65504 -- restated here independently of oracle.c's or_round_f16."""
+    vol32 = np.asarray(vol, dtype=np.float32)
     vol = np.asarray(vol, dtype=np.float64)
     nz, ny, nx = vol.shape
     N = np.array([nx, ny, nz], dtype=np.float64)
@@ -109,6 +114,27 @@ def render(vol, vmin, vmax, tf, view, cam_pos, width, height, smin=(0, 0, 0), sm
     smin = np.asarray(smin, np.float64)
     smax = np.asarray(smax, np.float64)
 
+    dfield = None
+    if grad_f16:
+        B = max(float(vmax), 0.0) - min(float(vmin), 0.0)
+        k = 0
+        if B > 0 and np.isfinite(B):
+            while k > -120 and B * 2.0 ** k > 65504.0:
+                k -= 1
+            while k < 120 and B * 2.0 ** (k + 1) <= 65504.0:
+                k += 1
+        vp32 = np.pad(vol32, 3)  # D at padded index + 2 needs one more layer
+        dfield = []
+        for ax_ in range(3):
+            sl_p = [slice(1, -1)] * 3
+            sl_m = [slice(1, -1)] * 3
+            # numpy axes (z, y, x): volume axis ax_ is numpy axis 2 - ax_
+            sl_p[2 - ax_] = slice(2, None)
+            sl_m[2 - ax_] = slice(0, -2)
+            D = (vp32[tuple(sl_p)] - vp32[tuple(sl_m)]).astype(np.float32) * np.float32(2.0 ** k)
+            D = np.where(np.isnan(D), D, np.clip(D, -65504.0, 65504.0)).astype(np.float32)
+            dfield.append(D.astype(np.float16).astype(np.float64))
+
     n = pos.shape[0]
     T = np.ones(n)
     Cc = np.zeros((n, 3))
@@ -126,10 +152,11 @@ def render(vol, vmin, vmax, tf, view, cam_pos, width, height, smin=(0, 0, 0), sm
             i0 = np.floor(u).astype(np.int64) + 2
             a = u - np.floor(u)
 
-            def cell(ii):
+            def cell(ii, src=None):
+                src = volp if src is None else src
                 xx, yy, zz = ii[:, 0], ii[:, 1], ii[:, 2]
                 ax, ay, az = a[:, 0], a[:, 1], a[:, 2]
-                v = lambda dx, dy, dz: volp[zz + dz, yy + dy, xx + dx]
+                v = lambda dx, dy, dz: src[zz + dz, yy + dy, xx + dx]
                 c00 = v(0, 0, 0) * (1 - ax) + v(1, 0, 0) * ax
                 c10 = v(0, 1, 0) * (1 - ax) + v(1, 1, 0) * ax
                 c01 = v(0, 0, 1) * (1 - ax) + v(1, 0, 1) * ax
@@ -147,7 +174,10 @@ def render(vol, vmin, vmax, tf, view, cam_pos, width, height, smin=(0, 0, 0), sm
                 for ax_ in range(3):
                     e = np.zeros(3, np.int64)
                     e[ax_] = 1
-                    g[:, ax_] = (cell(i0 + e) - cell(i0 - e)) * N[ax_]
+                    if grad_f16:
+                        g[:, ax_] = cell(i0, dfield[ax_]) * N[ax_]
+                    else:
+                        g[:, ax_] = (cell(i0 + e) - cell(i0 - e)) * N[ax_]
                 g2 = (g * g).sum(axis=1)
                 ok = (alpha > 0) & (g2 > 0)
                 with np.errstate(divide="ignore", invalid="ignore"):

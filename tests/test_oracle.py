@@ -149,3 +149,69 @@ def test_u8_voxel_source_equals_float_copy():
         b, sb = pyoracle.Scene.from_params(vol.astype(np.float32), 0.0, 255.0, synth.tf_color(),
                                            cam, 40, 30, p).render()
         assert np.array_equal(a, b) and sa == sb
+
+
+def test_round_f16_is_ieee_binary16():
+    """oracle.c or_round_f16 (the device's f32 -> binary16 conversion of the difference field,
+    DESIGN.md §3) equals IEEE binary16 round-to-nearest-even (numpy's float16), subnormals,
+    ties and the largest finite value included."""
+    rng = np.random.default_rng(3)
+    mags = 10.0 ** rng.uniform(-9, 4.8, 60000)
+    xs = (rng.choice([-1.0, 1.0], mags.size) * mags).astype(np.float32)
+    ties = (np.arange(1, 3000, dtype=np.float32) + np.float32(0.5)) * np.float32(2.0 ** -24)
+    edge = np.array([0.0, -0.0, 65504.0, -65504.0, 65503.9, 2.0 ** -14, 2.0 ** -24, 2.0 ** -25,
+                     3 * 2.0 ** -26, 1.0 + 2.0 ** -11, 1.0 + 3 * 2.0 ** -11, 6.1e-5], np.float32)
+    xs = np.concatenate([xs[np.abs(xs) <= 65504], ties, edge])
+    got = np.array([pyoracle.round_f16(float(x)) for x in xs], np.float32)
+    want = xs.astype(np.float16).astype(np.float32)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    assert np.isnan(pyoracle.round_f16(float("nan")))
+
+
+def test_field_scale_log2_matches_the_library():
+    """The binary16 field's scale exponent: the oracle's restatement equals the library's
+    field_scale_log2 (vr_internal.h, compiled here on the host) and the definition."""
+    import subprocess
+    import tempfile
+    pairs = [(0.0, 1.0), (-1000.0, 3000.0), (0.0, 0.0), (0.0, 255.0), (-128.0, 127.0),
+             (0.0, 65504.0), (0.0, 65505.0), (1e-7, 3e-7), (-1e30, 1e30), (5.0, 5.0),
+             (-3.5, -1.25), (0.0, 1e-30), (0.0, float("inf")), (2.0, 1.0)]
+    src = ('#include "vr_internal.h"\n#include <cstdio>\nint main(){float p[][2]={'
+           + ",".join("{%s,%s}" % tuple("INFINITY" if v == float("inf") else f"{v!r}f" for v in ab)
+                      for ab in pairs)
+           + '};for(auto&q:p)std::printf("%d\\n",vr::field_scale_log2(q[0],q[1]));}\n')
+    csrc = os.path.join(os.path.dirname(vr_amd.__file__), "csrc")
+    with tempfile.TemporaryDirectory() as d:
+        with open(os.path.join(d, "t.cpp"), "w") as f:
+            f.write(src)
+        subprocess.run(["/opt/rocm/bin/hipcc", "-x", "hip", "--offload-arch=gfx950", "-std=c++17",
+                        "-I", csrc, os.path.join(d, "t.cpp"), "-o", os.path.join(d, "t")],
+                       check=True, capture_output=True)
+        lib_k = [int(x) for x in subprocess.run([os.path.join(d, "t")], capture_output=True,
+                                                text=True, check=True).stdout.split()]
+    for (a, b), k in zip(pairs, lib_k):
+        assert pyoracle.field_scale_log2(a, b) == k, (a, b)
+        B = max(b, 0.0) - min(a, 0.0)
+        if B > 0 and np.isfinite(B) and B * 2.0 ** -120 <= 65504 and B * 2.0 ** 120 > 65504:
+            assert B * 2.0 ** k <= 65504 < B * 2.0 ** (k + 1), (a, b, k)
+
+
+@pytest.mark.parametrize("scale", [1.0, 4000.0, 1e-6])
+def test_oracle_binary16_gradient_mode(scale):
+    """oracle.c's binary16 field mode (grad_f16) against the independent float64 restatement of
+    the same rounding (ref_numpy grad_f16, numpy float16), and against the exact mode: within
+    the parity tolerance, and not identical."""
+    vol = (synth.gaussians_numpy((14, 11, 17), seed=21) * scale).astype(np.float32)
+    vmin, vmax = float(vol.min()), float(vol.max())
+    tf = synth.tf_color()
+    cam = synth.camera("fill_oblique").to_vr_camera()
+    p = vr_amd.default_params(shading=1)
+    h, _ = pyoracle.Scene.from_params(vol, vmin, vmax, tf, cam, 40, 30, p, grad_f16=True).render()
+    x, _ = pyoracle.Scene.from_params(vol, vmin, vmax, tf, cam, 40, 30, p).render()
+    ref = ref_numpy.render(vol, vmin, vmax, tf, list(cam.view), list(cam.position), 40, 30,
+                           shading=True, grad_f16=True)
+    d = h.astype(np.float64) - ref
+    assert np.sqrt(np.mean(d * d)) < 3e-5 and np.abs(d).max() < 2e-3
+    e = h.astype(np.float64) - x
+    assert np.sqrt(np.mean(e * e)) <= 1e-4 and np.abs(e).max() <= 2e-3
+    assert not np.array_equal(h, x)
