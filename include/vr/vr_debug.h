@@ -4,8 +4,9 @@
  * Not part of the drop-in boundary (the reference has no equivalent): the library picks the
  * march kernel variant, the 8-bit brick layout and the tile order from the volume, the view
  * and vr_params alone (DESIGN.md §5 "Which kernel a launch runs").  Every variant renders the
- * same bytes, so these knobs change speed, never results; the GPU tests use them to render
- * each variant and compare.  The library never reads the process environment, except in
+ * same bytes, so these knobs change speed, never results -- except VR_KNOB_GRAD_FIELD when
+ * vr_params.exact_gradient is 0 (the field then holds binary16 differences, the stencil exact
+ * ones); the GPU tests use them to render each variant and compare.  The library never reads the process environment, except in
  * experiment builds (`make EXTRA=-DVR_EXPERIMENTS`), where vr_create() seeds the knobs from
  * VR_PIPELINE, VR_PAIR, VR_PAIR_LANES, VR_NO_GRAD_FIELD / VR_GRAD_FIELD_ALWAYS, VR_LDS,
  * VR_U8_LAYOUT and VR_TILE_ORDER_DEFAULT (the names the round-1/2 A/B scripts under tools/

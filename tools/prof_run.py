@@ -6,7 +6,7 @@ profile's per-dispatch durations can be matched.  Frames go to a device buffer i
 each (vr_render_device): vr_render splits host-output frames into row bands.
   python tools/prof_run.py [--n 512] [--dtype float32] [--size 1920x1080] [--cam fill]
                            [--tf tf2] [--shading 1] [--ert 1e-5] [--frames 10] [--tile-order 0]
-                           [--skip-empty 0]
+                           [--skip-empty 0] [--exact-gradient 0]
 """
 import argparse
 import json
@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--tile-order", type=int, default=0)
     ap.add_argument("--skip-empty", type=int, default=0)
     ap.add_argument("--wave-shape", type=int, default=0)
+    ap.add_argument("--exact-gradient", type=int, default=0)
     a = ap.parse_args()
     W, H = (int(x) for x in a.size.split("x"))
     rp = vr_amd.OffscreenPass(W, H)
@@ -43,7 +44,8 @@ def main():
     rp.transfer_function_changed(synth.TFS[a.tf]())
     cam = synth.camera(a.cam).to_vr_camera()
     p = vr_amd.default_params(shading=a.shading, ert_eps=a.ert, tile_order=a.tile_order,
-                              skip_empty=a.skip_empty, wave_shape=a.wave_shape)
+                              skip_empty=a.skip_empty, wave_shape=a.wave_shape,
+                              exact_gradient=a.exact_gradient)
     import torch
     frame = torch.empty((H, W), dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
