@@ -24,6 +24,15 @@
 
 using namespace vr;
 
+// vr_render (host output): row bands per frame, each copied to the host while later bands
+// render (kHostBandMinRows rows at least, vr_internal.h).  C3 into pageable host memory, ms
+// per frame, three rounds (profiles/r03/host_bands/): 4 bands 0.589-0.603 shaded, 0.470-0.488
+// unshaded; 8 bands 0.730-0.753 / 0.557-0.560; 16 bands 1.13-1.63 / 0.86-0.90.
+#ifndef VR_HOST_BANDS
+#define VR_HOST_BANDS 4
+#endif
+constexpr int kRenderBands = VR_HOST_BANDS;
+
 struct vr_ctx {
     int device = 0;
     uint32_t width = 0, height = 0;
@@ -98,7 +107,7 @@ struct vr_ctx {
     // to the host on a third, so the PCIe copy hides behind the rest of the frame
     hipStream_t band_stream[2] = {nullptr, nullptr};
     hipStream_t copy_stream = nullptr;
-    hipEvent_t band_ev[kHostBands] = {};
+    hipEvent_t band_ev[kRenderBands] = {};
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
@@ -1658,9 +1667,9 @@ int vr_render(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out, in
         HIP_TRY(c, hipStreamSynchronize(c->group_stream), "hipStreamSynchronize(frame)");
         return VR_OK;
     }
-    // kHostBands row bands of R rows (a multiple of the 16-row tile): band b is the row shard
-    // (row_block R, rank b, nranks kHostBands), rendered densely at rows [b R, b R + R)
-    const int nb = H >= kHostBandMinRows ? kHostBands : 1;
+    // kRenderBands row bands of R rows (a multiple of the 16-row tile): band b is the row shard
+    // (row_block R, rank b, nranks kRenderBands), rendered densely at rows [b R, b R + R)
+    const int nb = H >= kHostBandMinRows ? kRenderBands : 1;
     const uint32_t R = nb == 1 ? 16 : ((H + nb - 1) / nb + 15) / 16 * 16;
     const size_t bytes = (size_t)W * (nb == 1 ? H : (size_t)R * nb) * bpp;
     if (c->frame_bytes < bytes) {
