@@ -27,6 +27,7 @@ VIEWS = {
     "side_x": dict(radius=1.6, rotate=(360.0, 0.0)),
     "top_z": dict(radius=1.6, rotate=(0.0, 360.0)),
     "diag": dict(radius=2.0, rotate=(180.0, 140.0)),
+    "diag2": dict(radius=1.8, rotate=(120.0, 60.0)),
     "default": dict(radius=3.0, rotate=None),
 }
 
