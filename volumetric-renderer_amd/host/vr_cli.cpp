@@ -7,8 +7,8 @@
 // RGBA8 image as a binary PPM (the presentation shim of SURVEY.md §8f-3, headless form).
 //
 //   vr_cli <file.nhdr|file.nrrd|synthetic:N> <out.ppm> [--size WxH] [--radius R]
-//          [--rotate DX,DY] [--tf default|demo] [--shading] [--ert EPS] [--skip-empty]
-//          [--frames K] [--device-mask M]   (M: render every frame across these GPUs)
+//          [--rotate DX,DY] [--tf default|demo] [--shading] [--exact-gradient] [--ert EPS]
+//          [--skip-empty] [--frames K] [--device-mask M]   (M: render every frame across these GPUs)
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -23,7 +23,7 @@ int main(int argc, char **argv)
 {
     if (argc < 3) {
         std::fprintf(stderr, "usage: %s <file.nhdr|synthetic:N> <out.ppm> [--size WxH] [--radius R] "
-                             "[--rotate DX,DY] [--tf default|demo] [--shading] [--ert EPS] [--skip-empty] "
+                             "[--rotate DX,DY] [--tf default|demo] [--shading] [--exact-gradient] [--ert EPS] [--skip-empty] "
                              "[--frames K] [--device-mask M]\n",
                      argv[0]);
         return 2;
@@ -31,7 +31,7 @@ int main(int argc, char **argv)
     std::string src = argv[1], out = argv[2];
     uint32_t W = 800, H = 600;
     float radius = 3.0f, rx = 0.0f, ry = 0.0f, ert = 0.0f;
-    int shading = 0, skip_empty = 0, frames = 1;
+    int shading = 0, skip_empty = 0, frames = 1, exact_gradient = 0;
     uint32_t mask = 0;
     std::string tfname = "default";
     for (int i = 3; i < argc; ++i) {
@@ -41,6 +41,7 @@ int main(int argc, char **argv)
         else if (a == "--rotate" && i + 1 < argc) std::sscanf(argv[++i], "%f,%f", &rx, &ry);
         else if (a == "--tf" && i + 1 < argc) tfname = argv[++i];
         else if (a == "--shading") shading = 1;
+        else if (a == "--exact-gradient") exact_gradient = 1;
         else if (a == "--skip-empty") skip_empty = 1;
         else if (a == "--ert" && i + 1 < argc) ert = std::strtof(argv[++i], nullptr);
         else if (a == "--frames" && i + 1 < argc) frames = std::atoi(argv[++i]);
@@ -89,6 +90,7 @@ int main(int argc, char **argv)
         vr_cam_view(&oc, cam.view);
         vr_cam_position(&oc, cam.position);
         pass.params().shading = shading;
+        pass.params().exact_gradient = exact_gradient;
         pass.params().skip_empty = skip_empty;
         pass.params().ert_eps = ert;
 
