@@ -282,6 +282,32 @@ def test_edge_viewports_and_empty_frames(rp):
     assert st["rays"] == 0
 
 
+@pytest.mark.parametrize("radius,rotate", [(0.7, (40.0, 25.0)), (0.75, (60.0, 45.0))])
+def test_near_plane_clips_part_of_the_front_face(rp, radius, rotate):
+    """A camera so close that the near plane cuts the cube's front face: the reference builds
+    glm::perspectiveRH in its [-1, 1] depth form (GLM_FORCE_DEPTH_ZERO_TO_ONE is defined in
+    offscreen_pass.cpp:3 after glm.hpp was first included through offscreen_pass.h:3) and
+    Vulkan clips at z_ndc = 0, i.e. at a view depth of 2 n f / (f + n) = 0.198 instead of
+    n = 0.1.  Part of the frame is clipped to the clear colour (with the [0, 1] form all of it
+    would be covered); the GPU clips exactly the oracle's pixels."""
+    vol = synth.gaussians_numpy((16, 16, 16), seed=2)
+    rp.volume_dataset_changed(synth.dataset(vol))
+    tf = synth.tf_color()
+    rp.transfer_function_changed(tf)
+    W, H = 64, 48
+    rp.framebuffer_size_changed(W, H)
+    cam = vr_amd.make_camera(radius=radius, rotate=rotate).to_vr_camera()
+    for shading in (0, 1):
+        p = vr_amd.default_params(shading=shading)
+        img = rp.render(cam, p, vr_amd.OUT_RGBA32F)
+        ref, st = oracle_render(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p)
+        assert 0 < st["rays"] < W * H, st
+        assert rp.count_work(cam, p) == st
+        clear = np.all(ref == np.float32([0.11, 0.11, 0.11, 1.0]), axis=2)
+        assert np.array_equal(np.all(img == np.float32([0.11, 0.11, 0.11, 1.0]), axis=2), clear)
+        check(img, ref)
+
+
 def test_constant_volume_and_large_tf(rp):
     """min == max (0/0 -> NaN density index: texel 0) and a TF beyond the LDS stage (1000 texels)."""
     W, H = 40, 30

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Alternating A/B of library builds on the headline bench line (C3, 3 frames in flight, no
-# variants) and the shaded view sweep.  Usage (GPU box): bash tools/ab_bench.sh <tag> <rounds> lib_a lib_b ...
+# variants) and the shaded view sweep.  Usage (GPU box): bash tools/experiments/r01_r02/ab_bench.sh <tag> <rounds> lib_a lib_b ...
 TAG=$1; R=$2; shift 2
 O=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $O
@@ -11,4 +11,4 @@ for r in $(seq 1 $R); do
     python -c "import json; d=json.load(open('$O/b.json')); print('$r', '$L'.ljust(12), 'C3', d['value'], d['ms_per_step'])" | tee -a $O/ab_bench.txt
   done
 done
-AB_CFGS="--shading 1 --ert 1e-5" bash tools/ab_views.sh $TAG "$@" "$@"
+AB_CFGS="--shading 1 --ert 1e-5" bash tools/experiments/r01_r02/ab_views.sh $TAG "$@" "$@"

@@ -3,7 +3,7 @@
 # (make -C volumetric-renderer_amd EXTRA=-DVR_EXPERIMENTS LIBDIR=lib_exp BUILDDIR=build_exp, then
 # VR_AMD_LIB=.../lib_exp/libvr_amd.so); the product library reads no environment (vr_debug.h).
 # Per-view A/B of one build under environment settings (e.g. VR_PIPELINE=0 / 1).
-# Usage (GPU box): bash tools/ab_env.sh <tag> "<cfg args>" "ENV=a" "ENV=b" ...
+# Usage (GPU box): bash tools/experiments/r01_r02/ab_env.sh <tag> "<cfg args>" "ENV=a" "ENV=b" ...
 set -o pipefail
 TAG=$1; CFG=$2; shift 2
 O=$GRAFT_REPO_ROOT/gpurun_out/$TAG

@@ -2,7 +2,7 @@
 # Alternating A/B of library builds on the whole bench line (C3 headline + its default-camera,
 # reference-semantics and skip-empty variants, 4 frames in flight) and serial per-view kernel
 # times (unshaded, shaded + ERT), after the parity suites under the first candidate build.
-# Usage (GPU box): bash tools/ab_full.sh <tag> <rounds> lib lib_b ...
+# Usage (GPU box): bash tools/experiments/r01_r02/ab_full.sh <tag> <rounds> lib lib_b ...
 set -o pipefail
 TAG=$1; R=$2; shift 2
 O=$GRAFT_REPO_ROOT/gpurun_out/$TAG
@@ -31,5 +31,5 @@ PY
   done
 done
 for r in $(seq 1 $R); do
-  bash tools/ab_views.sh $TAG "$@" || exit 1
+  bash tools/experiments/r01_r02/ab_views.sh $TAG "$@" || exit 1
 done

@@ -6,7 +6,7 @@
 # under VR_LDS=1 first (every frame checked against the oracle), then per-view kernel times of
 # each arm (f32 shaded + ERT, f32 reference semantics, u8 1024^3 @ 2048^2).  Each GPU step has
 # its own time limit; chained (the first failure ends the script).
-# Usage: bash tools/ab_lds.sh <tag> "<name>:<env settings>" ...
+# Usage: bash tools/experiments/r01_r02/ab_lds.sh <tag> "<name>:<env settings>" ...
 #   e.g. "gather:VR_LDS=0" "lds:VR_LDS=1" "lds3wg:VR_LDS=1 VR_AMD_LIB=$PWD/volumetric-renderer_amd/lib_b23/libvr_amd.so"
 set -o pipefail
 TAG=${1:-ab_lds}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of experiment builds (make LIBDIR=lib_<name> BUILDDIR=build_<name> EXTRA=...): kernel
 # time of C3 (shaded + ERT) and the reference-semantics frame per build, alternating builds
-# over R rounds.  Usage (GPU box): bash tools/ab_libs.sh <tag> <rounds> lib lib_a lib_b ...
+# over R rounds.  Usage (GPU box): bash tools/experiments/r01_r02/ab_libs.sh <tag> <rounds> lib lib_a lib_b ...
 set -o pipefail
 TAG=$1; R=$2; shift 2
 O=$GRAFT_REPO_ROOT/gpurun_out/$TAG

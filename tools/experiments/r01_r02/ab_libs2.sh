@@ -2,7 +2,7 @@
 # A/B of builds (make LIBDIR=lib_<name> BUILDDIR=build_<name> EXTRA=...) or environment settings,
 # alternating arms over R rounds: kernel ms of C3 (shaded + ERT), C3 reference semantics, the C3
 # default camera and C4 (u8 1024^3 @ 2048^2) per arm, via tools/prof_run.py (20 frames).
-# Usage (GPU box): bash tools/ab_libs2.sh <tag> <rounds> "<name>:<env>" ...
+# Usage (GPU box): bash tools/experiments/r01_r02/ab_libs2.sh <tag> <rounds> "<name>:<env>" ...
 set -o pipefail
 TAG=$1; R=$2; shift 2
 O=gpurun_out/$TAG

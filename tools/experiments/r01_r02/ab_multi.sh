@@ -1,5 +1,5 @@
 # A/B of experiment builds: parity (first variant), C3 bench x2 alternating, unshaded + shaded view sweeps
-# usage: bash tools/dbg/ab_multi.sh <tag> lib lib_a [lib_b ...]
+# usage: bash tools/experiments/r01_r02/ab_multi.sh <tag> lib lib_a [lib_b ...]
 set -o pipefail
 TAG=$1; shift
 O=gpurun_out/$TAG; mkdir -p $O

@@ -1,4 +1,4 @@
-"""Summarise tools/dbg/ab_multi.sh output: python tools/dbg/ab_report.py <dir> lib lib_a ..."""
+"""Summarise tools/experiments/r01_r02/ab_multi.sh output: python tools/experiments/r01_r02/ab_report.py <dir> lib lib_a ..."""
 import glob
 import json
 import os

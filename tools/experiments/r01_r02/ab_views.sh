@@ -1,6 +1,6 @@
 #!/bin/bash
 # Per-view A/B of experiment builds: tools/view_sweep.py (non-shaded, and shaded + ERT) per
-# library.  Usage (GPU box): bash tools/ab_views.sh <tag> lib lib_a ...
+# library.  Usage (GPU box): bash tools/experiments/r01_r02/ab_views.sh <tag> lib lib_a ...
 set -o pipefail
 TAG=$1; shift
 O=$GRAFT_REPO_ROOT/gpurun_out/$TAG

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Frames in flight per 8-bit configuration (C2/C4/C5), alternating settings, past the
 # cold-device ramp (50 / 20 warm-up frames).  Each run has its own time limit; the first
-# failure ends the script.  Usage (GPU box): bash tools/fif_configs.sh <tag> <rounds> "<fifs>"
+# failure ends the script.  Usage (GPU box): bash tools/experiments/r01_r02/fif_configs.sh <tag> <rounds> "<fifs>"
 set -o pipefail
 TAG=${1:-fif_configs}; R=${2:-2}; FIFS=${3:-"3 4 6"}
 O=$GRAFT_REPO_ROOT/gpurun_out/$TAG

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU check of one build: parity tests, bench (C3 + reference-semantics variant), view sweeps.
 # Every GPU step has its own time limit; steps are chained with && (stop at the first failure).
-# Usage (on the box, via gpurun): bash tools/gpu_check.sh <tag> [extra bench args]
+# Usage (on the box, via gpurun): bash tools/experiments/r01_r02/gpu_check.sh <tag> [extra bench args]
 set -o pipefail
 TAG=${1:-check}
 shift || true

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Frames-in-flight throughput over views, shaded (C3) and unshaded, N = 1 and the N = 8 share;
 # every GPU step under its own time limit, chained with &&.
-# Usage (on the box, via gpurun): bash tools/inflight_views.sh <tag> [extra sweep args]
+# Usage (on the box, via gpurun): bash tools/experiments/r01_r02/inflight_views.sh <tag> [extra sweep args]
 set -o pipefail
 TAG=${1:-inflight}
 shift || true

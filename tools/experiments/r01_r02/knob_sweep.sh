@@ -4,7 +4,7 @@
 # VR_AMD_LIB=.../lib_exp/libvr_amd.so); the product library reads no environment (vr_debug.h).
 # Per-view kernel-choice sweep (serial frames, tools/view_sweep.py) over the launch-policy
 # overrides: pipelined / lane-pair (2, 4 lanes per ray) kernels and wavefront shapes.
-# Usage (GPU box): bash tools/knob_sweep.sh <tag> "<view_sweep args>"
+# Usage (GPU box): bash tools/experiments/r01_r02/knob_sweep.sh <tag> "<view_sweep args>"
 TAG=$1; ARGS=$2
 O=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $O

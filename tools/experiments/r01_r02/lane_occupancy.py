@@ -1,6 +1,6 @@
 """Lane occupancy of the march (experiment): lane-steps (the normal counting kernel) against
 64 x each wavefront's longest ray (a -DVR_EXP_WAVE_STEPS=1 build, VR_AMD_LIB_WS), per view.
-GPU box: python tools/dbg/lane_occupancy.py"""
+GPU box: python tools/experiments/r01_r02/lane_occupancy.py"""
 import json
 import os
 import subprocess

@@ -2,7 +2,7 @@
 # Every BASELINE config through bench.py on one GPU (C3 is the default bench line; the rest
 # are reported in DESIGN.md §8).  C4/C5 skip the CPU baseline (the oracle would need minutes
 # per frame).  Each run has its own time limit; chained with &&.
-# Usage: bash tools/measure_configs.sh <tag>
+# Usage: bash tools/experiments/r01_r02/measure_configs.sh <tag>
 set -o pipefail
 TAG=${1:-configs}
 O=$GRAFT_REPO_ROOT/gpurun_out/$TAG

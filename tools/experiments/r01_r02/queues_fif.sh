@@ -1,7 +1,7 @@
 #!/bin/bash
 # C3 bench line (headline + default-camera / reference-semantics / skip-empty variants) per
 # hardware-queue count and frames in flight, alternating.  Each run has its own time limit;
-# the first failure ends the script.  Usage (GPU box): bash tools/queues_fif.sh <tag> <rounds>
+# the first failure ends the script.  Usage (GPU box): bash tools/experiments/r01_r02/queues_fif.sh <tag> <rounds>
 set -o pipefail
 TAG=${1:-queues_fif}; R=${2:-2}
 O=$GRAFT_REPO_ROOT/gpurun_out/$TAG

@@ -1,6 +1,6 @@
 """Where the fixed cost of a short timed region goes (K=20 W=5 vs K=200): one arm per fresh
 process, C3, 3 frames in flight; per-frame end times relative to the start of the timed region.
-  python tools/dbg/ramp.py K W [preburn_ms] [timing]
+  python tools/experiments/r01_r02/ramp.py K W [preburn_ms] [timing]
 preburn_ms > 0: keep the GPU busy with a torch matmul loop that long before the warm-up (clock
 ramp test); timing=1: the library's per-launch HIP event timing on, as bench.py runs it."""
 import json

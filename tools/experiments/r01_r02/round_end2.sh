@@ -3,4 +3,4 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out/round_end
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/round_end/tests.log 2>&1 &&
 bash tools/measure_round.sh round_end &&
-bash tools/measure_configs.sh configs_end
+bash tools/experiments/r01_r02/measure_configs.sh configs_end

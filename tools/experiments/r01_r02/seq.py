@@ -1,4 +1,4 @@
-"""Does what ran before change a variant's time?  python tools/dbg/seq.py <pre> ; pre in
+"""Does what ran before change a variant's time?  python tools/experiments/r01_r02/seq.py <pre> ; pre in
 none | fill1 (one shaded fill frame: builds the difference field) | serial (bench's serial
 variant) | fillpipe (40+20 pipelined fill frames).  Then the default-camera variant as bench
 runs it (K=20 after 40 warm-up frames), twice."""

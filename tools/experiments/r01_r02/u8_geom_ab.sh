@@ -7,4 +7,4 @@ for r in 1 2; do for L in $A $B; do for c in c4 c5; do
   VR_AMD_LIB=$PWD/volumetric-renderer_amd/$L/libvr_amd.so timeout -k 10 300 python bench.py --config $c --no-variants --no-cpu-baseline --steps 30 > $O/b.json 2> $O/b.err || exit 1
   python -c "import json; d=json.load(open('$O/b.json')); print('$r', '$L'.ljust(8), '$c', d['value'], d['ms_per_step'], d['config']['volume_resident_bytes'])" | tee -a $O/out.txt
 done; done; done
-AB_CFGS="--dtype uint8 --n 1024 --size 2048x2048 --shading 0" bash tools/ab_views.sh r02_u8geom $A $B
+AB_CFGS="--dtype uint8 --n 1024 --size 2048x2048 --shading 0" bash tools/experiments/r01_r02/ab_views.sh r02_u8geom $A $B

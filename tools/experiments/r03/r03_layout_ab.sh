@@ -2,7 +2,7 @@
 # Round 3: f32 layout A/B per view: lib (z-pair 8^3 bricks), lib_plain (-DVR_F32_PLAIN=1: one
 # voxel per element, 4 x 8-B loads per sample, half the bytes), lib_778 (-DVR_BRICK_CELLS=7,7,8).
 # tools/view_sweep.py per library, shaded (policy) and unshaded, 4 frames in flight and serial,
-# two alternating rounds.  Usage (GPU box): bash tools/r03_layout_ab.sh <tag>
+# two alternating rounds.  Usage (GPU box): bash tools/experiments/r03/r03_layout_ab.sh <tag>
 set -o pipefail
 TAG=${1:-r03_layout_ab}
 O=$GRAFT_REPO_ROOT/gpurun_out/$TAG
