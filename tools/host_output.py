@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=100)
     ap.add_argument("--shading", type=int, default=1)
+    ap.add_argument("--pinned", type=int, default=0, help="1: a page-locked host frame buffer")
     a = ap.parse_args()
     W, H = 1920, 1080
     rp = vr_amd.OffscreenPass(W, H)
@@ -27,14 +28,19 @@ def main():
     rp.transfer_function_changed(synth.tf2())
     cam = synth.camera("fill").to_vr_camera()
     p = vr_amd.default_params(shading=a.shading, ert_eps=1e-5 if a.shading else 0.0)
-    buf = np.empty((H, W, 4), np.uint8)
+    if a.pinned:
+        import torch
+        buf = torch.empty((H, W, 4), dtype=torch.uint8, pin_memory=True).numpy()
+    else:
+        buf = np.empty((H, W, 4), np.uint8)
     for _ in range(60):
         rp.render(cam, p, vr_amd.OUT_RGBA8, out=buf)
     t0 = time.perf_counter()
     for _ in range(a.frames):
         rp.render(cam, p, vr_amd.OUT_RGBA8, out=buf)
     dt = (time.perf_counter() - t0) / a.frames
-    print(json.dumps(dict(lib=os.environ.get("VR_AMD_LIB", "lib"), ms=round(dt * 1e3, 4),
+    print(json.dumps(dict(lib=os.path.basename(os.path.dirname(os.environ.get("VR_AMD_LIB", "/lib/x"))),
+                          pinned=a.pinned, shading=a.shading, ms=round(dt * 1e3, 4),
                           fps=round(1 / dt, 1))))
 
 

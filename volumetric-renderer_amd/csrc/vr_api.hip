@@ -27,7 +27,9 @@ using namespace vr;
 // vr_render (host output): row bands per frame, each copied to the host while later bands
 // render (kHostBandMinRows rows at least, vr_internal.h).  C3 into pageable host memory, ms
 // per frame, three rounds (profiles/r03/host_bands/): 4 bands 0.589-0.603 shaded, 0.470-0.488
-// unshaded; 8 bands 0.730-0.753 / 0.557-0.560; 16 bands 1.13-1.63 / 0.86-0.90.
+// unshaded; 8 bands 0.730-0.753 / 0.557-0.560; 16 bands 1.13-1.63 / 0.86-0.90.  A page-locked
+// destination changes nothing (4 bands 0.582 against 0.583; 2 bands 0.635-0.655, both
+// kinds; profiles/r03/host_pinned/): the bands' own launches, not the copies, set the time.
 #ifndef VR_HOST_BANDS
 #define VR_HOST_BANDS 4
 #endif
