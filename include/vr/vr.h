@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 5
+#define VR_ABI_VERSION 6
 
 /* ---- status codes (negative errno style) ---- */
 #define VR_OK 0
@@ -242,6 +242,19 @@ uint32_t vr_shard_rows(uint32_t height, uint32_t row_block, uint32_t nranks);
  * (rank-major, vr_shard_rows() rows each); writes the H x W frame to `out_dev`. */
 int vr_assemble_rows(vr_ctx *ctx, const void *gathered_dev, void *out_dev, int out_format,
                      uint32_t row_block, uint32_t nranks, void *stream);
+
+/* ---- zero-copy presentation ----
+ * Import device memory that another API exported as a POSIX file descriptor -- Vulkan:
+ * VK_KHR_external_memory_fd (vkGetMemoryFdKHR on the VkDeviceMemory of a device-local buffer
+ * or linear image; the reference's copy_buffer_to_image, offscreen_pass.cpp:1379-1406, then
+ * copies it into the colour image on the GPU, no host round trip) -- and map `size` bytes at
+ * `offset` of it on the context's device (the lowest device of a vr_create_mask context).
+ * *dev_ptr can be passed to vr_render_device.  On success the import owns `fd`; release the
+ * mapping with vr_release_external_memory before the exporter frees the memory. */
+typedef struct vr_external_memory vr_external_memory;
+int vr_import_memory_fd(vr_ctx *ctx, int fd, uint64_t size, uint64_t offset,
+                        vr_external_memory **mem, void **dev_ptr);
+int vr_release_external_memory(vr_ctx *ctx, vr_external_memory *mem);
 
 /* Count the work of one frame (same camera/params/shard) exactly; synchronous. */
 int vr_count_work(vr_ctx *ctx, const vr_camera *cam, const vr_params *p, uint32_t row_block,

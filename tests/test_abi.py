@@ -58,7 +58,7 @@ def test_product_never_reads_the_environment():
 
 def test_library_loads_and_pure_entry_points():
     L = vr_amd.lib()
-    assert L.vr_abi_version() == 5
+    assert L.vr_abi_version() == 6
     p = vr_amd.default_params()
     assert p.step == pytest.approx(0.005) and p.ray_dist == pytest.approx(1.8)
     assert list(p.clear_color) == pytest.approx([0.11, 0.11, 0.11, 1.0])
@@ -93,7 +93,7 @@ int main(void) { printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(vr_camera), size
                                      vr_amd.vr_params.skip_empty.offset,
                                      vr_amd.vr_params.frames_in_flight.offset,
                                      vr_amd.vr_params.exact_gradient.offset]
-    assert "VR_ABI_VERSION 5" in src
+    assert "VR_ABI_VERSION 6" in src
 
 
 def test_create_without_device_fails_cleanly():

@@ -14,6 +14,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIBDIR = os.path.join(ROOT, "volumetric-renderer_amd", "lib")
 SRC = os.path.join(ROOT, "tests", "shim", "reference_call_shapes.cpp")
 EXE = os.path.join(LIBDIR, "reference_call_shapes")
+EXT_SRC = os.path.join(ROOT, "tests", "shim", "external_memory.cpp")
+EXT_EXE = os.path.join(LIBDIR, "external_memory")
 
 
 def build():
@@ -21,6 +23,15 @@ def build():
                     SRC, "-o", EXE, "-L", LIBDIR, "-lvr_amd", "-Wl,-rpath," + LIBDIR],
                    check=True, capture_output=True, text=True)
     return EXE
+
+
+def build_external():
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-D__HIP_PLATFORM_AMD__",
+                    "-I", os.path.join(ROOT, "include"), "-I", "/opt/rocm/include", EXT_SRC,
+                    "-o", EXT_EXE, "-L", LIBDIR, "-lvr_amd", "-Wl,-rpath," + LIBDIR,
+                    "-L", "/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"],
+                   check=True, capture_output=True, text=True)
+    return EXT_EXE
 
 
 def test_reference_call_shapes_compile_and_link():
@@ -49,3 +60,19 @@ def test_u8_scan_as_float_dataset_is_stored_native(gpu):
     r = subprocess.run([exe, "--u8-dataset"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "narrow=1" in r.stdout and "match=1" in r.stdout
+
+
+def test_external_memory_program_compiles_and_links():
+    assert os.path.exists(build_external())
+
+
+@pytest.mark.gpu
+def test_frame_rendered_into_imported_memory(gpu):
+    """SURVEY.md §8f-3 (zero-copy presentation): a shareable allocation exported as a POSIX fd
+    (the vkGetMemoryFdKHR stand-in) is imported with vr_import_memory_fd, two frames are rendered
+    into it with vr_render_device, and the exporter reads through ITS OWN mapping exactly
+    vr_render's bytes for the same camera, with the bytes around the imported range untouched."""
+    exe = EXT_EXE if os.path.exists(EXT_EXE) else build_external()
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "match=1" in r.stdout and "guard=1" in r.stdout

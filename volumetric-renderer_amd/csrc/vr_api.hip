@@ -1742,6 +1742,61 @@ int vr_assemble_rows(vr_ctx *c, const void *gathered_dev, void *out_dev, int out
     return VR_OK;
 }
 
+// Zero-copy presentation: memory another API exported as a POSIX fd (Vulkan
+// VK_KHR_external_memory_fd), imported on the device vr_render_device writes to.
+struct vr_external_memory {
+    hipExternalMemory_t ext;
+    void *ptr;
+    int device;
+};
+
+int vr_import_memory_fd(vr_ctx *c, int fd, uint64_t size, uint64_t offset,
+                        vr_external_memory **mem, void **dev_ptr)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (!mem || !dev_ptr) return fail(c, VR_EINVAL, "NULL output");
+    *mem = nullptr;
+    *dev_ptr = nullptr;
+    if (fd < 0 || size == 0) return fail(c, VR_EINVAL, "bad fd or size");
+    const int device = is_group(c) ? c->members[0]->device : c->device;
+    HIP_TRY(c, hipSetDevice(device), "hipSetDevice");
+    hipExternalMemoryHandleDesc hd;
+    std::memset(&hd, 0, sizeof hd);
+    hd.type = hipExternalMemoryHandleTypeOpaqueFd;
+    hd.handle.fd = fd;
+    hd.size = offset + size;
+    hipExternalMemory_t ext = nullptr;
+    HIP_TRY(c, hipImportExternalMemory(&ext, &hd), "hipImportExternalMemory");
+    hipExternalMemoryBufferDesc bd;
+    std::memset(&bd, 0, sizeof bd);
+    bd.offset = offset;
+    bd.size = size;
+    void *ptr = nullptr;
+    const hipError_t e = hipExternalMemoryGetMappedBuffer(&ptr, ext, &bd);
+    if (e != hipSuccess) {
+        (void)hipDestroyExternalMemory(ext);
+        return hip_fail(c, e, "hipExternalMemoryGetMappedBuffer");
+    }
+    *mem = new vr_external_memory{ext, ptr, device};
+    *dev_ptr = ptr;
+    return VR_OK;
+}
+
+int vr_release_external_memory(vr_ctx *c, vr_external_memory *m)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (!m) return fail(c, VR_EINVAL, "mem is NULL");
+    HIP_TRY(c, hipSetDevice(m->device), "hipSetDevice");
+    // frames still rendering into the mapping finish first
+    HIP_TRY(c, hipDeviceSynchronize(), "hipDeviceSynchronize");
+    const hipError_t e1 = hipFree(m->ptr);
+    const hipError_t e2 = hipDestroyExternalMemory(m->ext);
+    delete m;
+    if (e1 != hipSuccess) return hip_fail(c, e1, "hipFree(external mapping)");
+    if (e2 != hipSuccess) return hip_fail(c, e2, "hipDestroyExternalMemory");
+    return VR_OK;
+}
+
 int vr_count_work(vr_ctx *c, const vr_camera *cam, const vr_params *p, uint32_t row_block,
                   uint32_t rank, uint32_t nranks, vr_stats *out)
 {

@@ -76,6 +76,7 @@ ABI_SYMBOLS = [
     "vr_set_transfer_function", "vr_set_slicing", "vr_render", "vr_render_device",
     "vr_shard_rows", "vr_assemble_rows", "vr_count_work", "vr_timing_enable",
     "vr_timing_read", "vr_timing_reset", "vr_kernel_name",
+    "vr_import_memory_fd", "vr_release_external_memory",
 ]
 HOST_SYMBOLS = [
     "vr_cam_init", "vr_cam_rotate", "vr_cam_zoom", "vr_cam_position", "vr_cam_view",
@@ -99,7 +100,7 @@ KNOBS = {"pipeline": 1, "pair": 2, "pair_lanes": 3, "grad_field": 4, "lds": 5, "
 KNOB_AUTO = {"pipeline": -1, "pair": -1, "pair_lanes": 0, "grad_field": -1, "lds": 0,
              "u8_layout": -1, "tile_order": 0, "narrow": 1, "alt_geometry": -1}
 
-ABI_VERSION = 5  # include/vr/vr.h VR_ABI_VERSION
+ABI_VERSION = 6  # include/vr/vr.h VR_ABI_VERSION
 _LIB = None
 
 
@@ -160,6 +161,9 @@ def lib() -> C.CDLL:
         "vr_timing_read": (i32, [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
         "vr_timing_reset": (i32, [vp]),
         "vr_kernel_name": (C.c_char_p, [vp, C.POINTER(vr_params)]),
+        "vr_import_memory_fd": (C.c_int, [vp, C.c_int, C.c_uint64, C.c_uint64, C.POINTER(vp),
+                                          C.POINTER(vp)]),
+        "vr_release_external_memory": (C.c_int, [vp, vp]),
         "vr_debug_set_knob": (i32, [vp, i32, i32]),
         "vr_debug_get_knob": (i32, [vp, i32, C.POINTER(i32)]),
         "vr_cam_init": (None, [C.POINTER(vr_orbit_camera)]),
