@@ -68,6 +68,10 @@ def test_library_loads_and_pure_entry_points():
     assert vr_amd.shard_rows(1080, 16, 8) == 144
     assert vr_amd.shard_rows(53, 1, 5) == 11
     assert vr_amd.shard_rows(10, 0, 2) == 0
+    # external-memory import: argument checks come before any HIP call
+    mem, ptr = C.c_void_p(), C.c_void_p()
+    assert L.vr_import_memory_fd(None, 3, 64, 0, C.byref(mem), C.byref(ptr)) == -22
+    assert L.vr_release_external_memory(None, None) == -22
 
 
 def test_struct_layouts_match_header():

@@ -1757,7 +1757,8 @@ int vr_import_memory_fd(vr_ctx *c, int fd, uint64_t size, uint64_t offset,
     if (!mem || !dev_ptr) return fail(c, VR_EINVAL, "NULL output");
     *mem = nullptr;
     *dev_ptr = nullptr;
-    if (fd < 0 || size == 0) return fail(c, VR_EINVAL, "bad fd or size");
+    if (fd < 0 || size == 0 || offset > UINT64_MAX - size)
+        return fail(c, VR_EINVAL, "bad fd, size or offset");
     const int device = is_group(c) ? c->members[0]->device : c->device;
     HIP_TRY(c, hipSetDevice(device), "hipSetDevice");
     hipExternalMemoryHandleDesc hd;
