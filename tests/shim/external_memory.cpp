@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -36,11 +37,14 @@
         }                                                                          \
     } while (0)
 
-int main()
+int main(int argc, char **argv)
 {
     const uint32_t W = 160, H = 120;
     const size_t frame_bytes = (size_t)W * H * 4;
-    vr_ctx *ctx = vr_create(0, W, H);
+    // --device-mask M: a multi-device context (vr_create_mask); frames land on its lowest device
+    const bool group = argc > 2 && std::strcmp(argv[1], "--device-mask") == 0;
+    vr_ctx *ctx = group ? vr_create_mask((uint32_t)std::strtoul(argv[2], nullptr, 0), W, H)
+                        : vr_create(0, W, H);
     if (!ctx) return 2;
     float mm[2];
     VR_CALL(ctx, vr_generate_volume(ctx, 0, VR_DTYPE_F32, 96, 80, 64, 7, &mm[0], &mm[1]));
@@ -116,7 +120,7 @@ int main()
     HIP_OK(hipMemAddressFree(exp_ptr, size));
     HIP_OK(hipMemRelease(handle));
     vr_destroy(ctx);
-    std::printf("external frame %ux%u offset=%zu covered=%u guard=%d match=%d\n", W, H, offset,
-                covered, (int)guard, (int)same);
+    std::printf("external frame %ux%u group=%d offset=%zu covered=%u guard=%d match=%d\n", W, H,
+                (int)group, offset, covered, (int)guard, (int)same);
     return same && guard && covered > 0 ? 0 : 1;
 }

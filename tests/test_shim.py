@@ -67,12 +67,16 @@ def test_external_memory_program_compiles_and_links():
 
 
 @pytest.mark.gpu
-def test_frame_rendered_into_imported_memory(gpu):
+@pytest.mark.parametrize("mask", [None, "0x1"])
+def test_frame_rendered_into_imported_memory(gpu, mask):
     """SURVEY.md §8f-3 (zero-copy presentation): a shareable allocation exported as a POSIX fd
     (the vkGetMemoryFdKHR stand-in) is imported with vr_import_memory_fd, two frames are rendered
     into it with vr_render_device, and the exporter reads through ITS OWN mapping exactly
-    vr_render's bytes for the same camera, with the bytes around the imported range untouched."""
+    vr_render's bytes for the same camera, with the bytes around the imported range untouched.
+    With a device mask the context is a vr_create_mask group, whose frames land on its lowest
+    device."""
     exe = EXT_EXE if os.path.exists(EXT_EXE) else build_external()
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    r = subprocess.run([exe] + (["--device-mask", mask] if mask else []), capture_output=True,
+                       text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "match=1" in r.stdout and "guard=1" in r.stdout
