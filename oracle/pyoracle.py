@@ -119,7 +119,8 @@ class Scene:
                     smax=(1, 1, 1), grad_f16=False):
         """Build from a vr_amd vr_camera / vr_params pair (same meaning as the C ABI).
         grad_f16: restate the device's binary16 difference field (a shaded f32 frame with
-        params.exact_gradient == 0 whose kernel reads the field, vr_amd.reads_half_field)."""
+        params.exact_gradient == 0 whose kernel reads the field: kernel tag F32H in
+        vr_kernel_name)."""
         return cls(vol, vmin, vmax, tf, list(camera.view), list(camera.position), width, height,
                    smin=smin, smax=smax, step=params.step, ray_dist=params.ray_dist,
                    ert_eps=params.ert_eps, shading=params.shading,
