@@ -3,7 +3,8 @@
 Tolerance: float RGBA after blend, before UNORM quantisation,
 RMSE <= 1e-4 over all pixels x 4 channels and max |d| <= 2e-3 (one boundary sample);
 RGBA8 output within 1 LSB.  The kernel performs the oracle's IEEE operations in the same
-order (contraction off, explicit fmaf), so most cases are bit-exact; the tests record that.
+order (contraction off, explicit fmaf), so frames are also bit-exact, and test_parity_float
+asserts that after the tolerance check (as does the randomized sweep, test_gpu_random.py).
 Work counters (rays, samples, shaded samples, steps) must match the oracle exactly.
 """
 import numpy as np
@@ -90,11 +91,15 @@ def test_parity_float(rp, case):
     cam = synth.camera(camname).to_vr_camera()
     p = vr_amd.default_params(shading=shading, ert_eps=ert)
     img = rp.render(cam, p, vr_amd.OUT_RGBA32F)
-    ref, st = oracle_render(vol.astype(np.float32), ds.vmin, ds.vmax, tf, cam, W, H, p, smin, smax)
+    half = "F32H" in rp.kernel_name(p)  # the binary16 difference field: restated by the oracle
+    ref, st = oracle_render(vol.astype(np.float32), ds.vmin, ds.vmax, tf, cam, W, H, p, smin, smax,
+                            grad_f16=half)
     check(img, ref)
-    # RGBA8 target: within 1 LSB of the quantised oracle
+    assert np.array_equal(img, ref.astype(np.float32))  # and bit for bit
+    # RGBA8 target: within 1 LSB of the quantised oracle (equal, as the float frame is)
     img8 = rp.render(cam, p, vr_amd.OUT_RGBA8)
     assert np.abs(img8.astype(int) - vr_amd.unorm8(ref).astype(int)).max() <= 1
+    assert np.array_equal(img8, vr_amd.unorm8(ref))
     # exact work accounting
     cw = rp.count_work(cam, p)
     assert cw == st, (cw, st)
