@@ -814,3 +814,46 @@ def test_half_field_bit_exact(rp, vname):
         assert np.array_equal(exact.view(np.uint32), ref32.view(np.uint32)), (vname, skip)
     with pytest.raises(RuntimeError):
         rp.render(cam, vr_amd.default_params(shading=1, exact_gradient=2))
+
+
+def test_field_precision_switch_orders_other_streams(rp):
+    """Switching vr_params.exact_gradient rebuilds the difference field in place, on the stream
+    of the frame that switches.  Frames on other streams -- the other row bands of a host
+    render of >= 256 rows, frames in flight -- must wait for that rebuild (regression: the
+    rebuild of a field that was valid on entry recorded no build event, and the first frame
+    after a switch read a half-rebuilt field in every other band)."""
+    import torch
+    W, H = 640, 512
+    rp.framebuffer_size_changed(W, H)
+    vol = synth.gaussians_numpy((160, 160, 160), seed=23)
+    ds = synth.dataset(vol)
+    rp.volume_dataset_changed(ds)
+    tf = synth.tf_band(0.15, 0.9)
+    rp.transfer_function_changed(tf)
+    cam = synth.camera("fill").to_vr_camera()
+    ph = vr_amd.default_params(shading=1, ert_eps=1e-5)
+    pe = vr_amd.default_params(shading=1, ert_eps=1e-5, exact_gradient=1)
+    rp.render(cam, ph, vr_amd.OUT_RGBA32F)
+    assert "F32H" in rp.kernel_name(ph), rp.kernel_name(ph)
+    ref = {0: oracle_render(vol, ds.vmin, ds.vmax, tf, cam, W, H, ph, grad_f16=True)[0],
+           1: oracle_render(vol, ds.vmin, ds.vmax, tf, cam, W, H, pe)[0]}
+    assert not np.array_equal(ref[0], ref[1])
+    # host renders in row bands on two streams, switching precision every frame
+    for i in range(4):
+        p = (pe, ph)[i % 2]
+        img = rp.render(cam, p, vr_amd.OUT_RGBA32F)
+        bad = int((img.view(np.uint32) != ref[p.exact_gradient].view(np.uint32)).any(axis=-1).sum())
+        assert bad == 0, f"frame {i} (exact_gradient={p.exact_gradient}): {bad} pixels differ"
+    # frames in flight on three streams, switching precision every frame
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    outs = [torch.empty((H, W), dtype=torch.int32, device="cuda") for _ in range(6)]
+    for i in range(6):
+        p = vr_amd.default_params(shading=1, ert_eps=1e-5, exact_gradient=(i + 1) % 2,
+                                  frames_in_flight=3)
+        rp.render_device(cam, p, outs[i].data_ptr(), vr_amd.OUT_RGBA8, 16, 0, 1,
+                         streams[i % 3].cuda_stream)
+    torch.cuda.synchronize()
+    for i in range(6):
+        got = outs[i].cpu().numpy().view(np.uint8).reshape(H, W, 4)
+        want = vr_amd.unorm8(ref[(i + 1) % 2])
+        assert np.array_equal(got, want), f"in-flight frame {i}"

@@ -715,15 +715,18 @@ int ensure_skip(vr_ctx *c, MarchParams &P, hipStream_t s)
 // density; when that does not fit beside a 2 GiB reserve the kernel forms the differences
 // from the 4-wide stencil instead (exact f32 differences).  half: the binary16 field
 // (vr_params.exact_gradient == 0), the same 24-B elements.  Switching precision rebuilds the
-// field in place after the device has drained (frames in flight may still read it).
-void ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s, bool half)
+// field in place after the device has drained (frames in flight may still read it).  Returns
+// true when it launched a (re)build on `s`: frames on other streams must then wait for it
+// (ensure_derived records the build event).
+bool ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s, bool half)
 {
-    if (!use_grad_field(c, half)) return;
+    bool built = false;
+    if (!use_grad_field(c, half)) return built;
     const int k = half ? field_scale_log2(c->vmin, c->vmax) : 0;
     if (c->grad_valid && (c->grad_half != half || c->grad_scale_log2 != k)) {
         if (hipDeviceSynchronize() != hipSuccess) {
             (void)hipGetLastError();
-            return;
+            return built;
         }
         c->grad_valid = false;
     }
@@ -734,11 +737,12 @@ void ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s, bool half)
         c->grad_bytes = 0;
         c->grad_valid = false;
         size_t free_b = 0, total_b = 0;
-        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < bytes + (2ull << 30)) return;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < bytes + (2ull << 30))
+            return built;
         void *g = nullptr;
         if (hipMalloc(&g, bytes) != hipSuccess) {
             (void)hipGetLastError();
-            return;
+            return built;
         }
         c->grad = static_cast<float *>(g);
         c->grad_bytes = bytes;
@@ -746,13 +750,15 @@ void ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s, bool half)
     if (!c->grad_valid) {
         if (launch_grad_field(static_cast<const float *>(c->bricks), c->grad, c->nx, c->ny, c->nz,
                               half, k, s) != hipSuccess)
-            return;
+            return built;
+        built = true;
         c->grad_valid = true;
         c->grad_half = half;
         c->grad_scale_log2 = k;
     }
     P.grad = c->grad;
     P.grad_half = half ? 1 : 0;
+    return built;
 }
 
 // The derived fields a frame reads (skip-empty classification, gradient field), built on `s`
@@ -760,13 +766,14 @@ void ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s, bool half)
 // waits on the event recorded after the last build (a no-op once it has completed).
 int ensure_derived(vr_ctx *c, const vr_params *p, MarchParams &P, hipStream_t s)
 {
-    const bool r0 = c->range_valid, d0 = c->dist_valid, g0 = c->grad_valid;
+    const bool r0 = c->range_valid, d0 = c->dist_valid;
     if (p->skip_empty) {
         int rc = ensure_skip(c, P, s);
         if (rc) return rc;
     }
-    if (p->shading) ensure_grad(c, P, s, p->exact_gradient == 0);
-    const bool built = (!r0 && c->range_valid) || (!d0 && c->dist_valid) || (!g0 && c->grad_valid);
+    // (a precision switch rebuilds a field that was valid on entry: ask ensure_grad, not the flag)
+    const bool g_built = p->shading && ensure_grad(c, P, s, p->exact_gradient == 0);
+    const bool built = (!r0 && c->range_valid) || (!d0 && c->dist_valid) || g_built;
     if (built) {
         if (!c->built_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->built_ev, hipEventDisableTiming),
                                   "hipEventCreate");
