@@ -857,3 +857,49 @@ def test_field_precision_switch_orders_other_streams(rp):
         got = outs[i].cpu().numpy().view(np.uint8).reshape(H, W, 4)
         want = vr_amd.unorm8(ref[(i + 1) % 2])
         assert np.array_equal(got, want), f"in-flight frame {i}"
+
+
+def test_builds_on_other_streams_are_chained(rp):
+    """Frames in flight whose views need different derived structures: each frame builds what
+    it lacks on its own stream, and a later frame on a third stream must see every earlier
+    build (regression: one build event was re-recorded without waiting for the previous one,
+    so a frame could read an alternative brick copy, or a gradient field, still being built
+    on another stream)."""
+    import torch
+    W, H = 512, 384
+    rp.framebuffer_size_changed(W, H)
+    vol = synth.gaussians_numpy((320, 320, 320), seed=29)
+    ds = synth.dataset(vol)
+    tf = synth.tf_band(0.15, 0.9)
+    obl = vr_amd.make_camera(radius=1.8, rotate=(120.0, 60.0)).to_vr_camera()
+    fill = synth.camera("fill").to_vr_camera()
+    unshaded = vr_amd.default_params(frames_in_flight=3)
+    shaded = vr_amd.default_params(shading=1, ert_eps=1e-5, frames_in_flight=3)
+    shaded_skip = vr_amd.default_params(shading=1, ert_eps=1e-5, skip_empty=1, frames_in_flight=3)
+    unshaded_skip = vr_amd.default_params(skip_empty=1, frames_in_flight=3)
+    sequences = [  # (camera, params) per frame, frame i on stream i
+        # a long build (the oblique copy), a short one (skip ranges), a reader of the first
+        [(obl, unshaded), (fill, unshaded_skip), (obl, unshaded)],
+        [(obl, unshaded), (fill, shaded), (obl, unshaded)],   # alt copy, field, alt copy again
+        [(fill, shaded), (fill, shaded_skip), (obl, unshaded)],  # field, skip ranges over it
+    ]
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    refs = {}
+    for seq in sequences:
+        rp.volume_dataset_changed(ds)  # fresh: every derived structure stale
+        rp.transfer_function_changed(tf)
+        outs = [torch.empty((H, W), dtype=torch.int32, device="cuda") for _ in seq]
+        for i, (cam, p) in enumerate(seq):
+            rp.render_device(cam, p, outs[i].data_ptr(), vr_amd.OUT_RGBA8, 16, 0, 1,
+                             streams[i].cuda_stream)
+        torch.cuda.synchronize()
+        for i, (cam, p) in enumerate(seq):
+            key = (id(cam), p.shading)  # skip-empty frames are bit-identical to the others
+            if key not in refs:
+                rp.render(cam, p)  # serial: which kernel (field precision) this view runs
+                grad16 = "F32H" in rp.kernel_name(p)
+                refs[key] = vr_amd.unorm8(oracle_render(vol, ds.vmin, ds.vmax, tf, cam, W, H, p,
+                                                        grad_f16=grad16)[0])
+            got = outs[i].cpu().numpy().view(np.uint8).reshape(H, W, 4)
+            bad = int((got != refs[key]).any(axis=-1).sum())
+            assert bad == 0, f"sequence {sequences.index(seq)} frame {i}: {bad} pixels differ"

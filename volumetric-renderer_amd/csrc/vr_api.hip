@@ -675,6 +675,16 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     return VR_OK;
 }
 
+// After a build on `s`: frames on other streams wait for it (ensure_derived).
+int record_build(vr_ctx *c, hipStream_t s)
+{
+    if (!c->built_ev)
+        HIP_TRY(c, hipEventCreateWithFlags(&c->built_ev, hipEventDisableTiming), "hipEventCreate");
+    HIP_TRY(c, hipEventRecord(c->built_ev, s), "hipEventRecord(build)");
+    c->built_recorded = true;
+    return VR_OK;
+}
+
 // skip_empty: (re)build the per-brick ranges and the distance field when stale, on `s` ahead of
 // the march that reads them.
 int ensure_skip(vr_ctx *c, MarchParams &P, hipStream_t s)
@@ -761,11 +771,17 @@ bool ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s, bool half)
     return built;
 }
 
-// The derived fields a frame reads (skip-empty classification, gradient field), built on `s`
-// when stale.  A frame on another stream may follow before that build has run: every frame
-// waits on the event recorded after the last build (a no-op once it has completed).
+// The derived fields a frame reads (skip-empty classification, gradient field, alternative
+// brick copies), built on `s` when stale.  A frame on another stream may follow before a build
+// has run, so builds are chained through one event: every frame first waits on the event
+// recorded after the last build (a no-op once it has completed), and a frame that builds
+// records it again after its own builds.  Since that frame's stream already waited on the
+// previous record, the new record also covers every earlier build, on whichever stream it ran
+// (a frame that reads a field built on one stream and builds another on its own, e.g. a
+// shaded skip-empty frame, or a later frame reading both).
 int ensure_derived(vr_ctx *c, const vr_params *p, MarchParams &P, hipStream_t s)
 {
+    if (c->built_recorded) HIP_TRY(c, hipStreamWaitEvent(s, c->built_ev, 0), "hipStreamWaitEvent(build)");
     const bool r0 = c->range_valid, d0 = c->dist_valid;
     if (p->skip_empty) {
         int rc = ensure_skip(c, P, s);
@@ -774,14 +790,7 @@ int ensure_derived(vr_ctx *c, const vr_params *p, MarchParams &P, hipStream_t s)
     // (a precision switch rebuilds a field that was valid on entry: ask ensure_grad, not the flag)
     const bool g_built = p->shading && ensure_grad(c, P, s, p->exact_gradient == 0);
     const bool built = (!r0 && c->range_valid) || (!d0 && c->dist_valid) || g_built;
-    if (built) {
-        if (!c->built_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->built_ev, hipEventDisableTiming),
-                                  "hipEventCreate");
-        HIP_TRY(c, hipEventRecord(c->built_ev, s), "hipEventRecord(build)");
-        c->built_recorded = true;
-    } else if (c->built_recorded) {
-        HIP_TRY(c, hipStreamWaitEvent(s, c->built_ev, 0), "hipStreamWaitEvent(build)");
-    }
+    if (built) return record_build(c, s);
     return VR_OK;
 }
 
@@ -868,12 +877,9 @@ int ensure_alt(vr_ctx *c, int lay, hipStream_t s, bool *ready)
     if (f != hipSuccess) return hip_fail(c, f, "hipFreeAsync(alt staging)");
     a.valid = true;
     *ready = true;
-    // frames on other streams that read the copy wait for this build (ensure_derived)
-    if (!c->built_ev)
-        HIP_TRY(c, hipEventCreateWithFlags(&c->built_ev, hipEventDisableTiming), "hipEventCreate");
-    HIP_TRY(c, hipEventRecord(c->built_ev, s), "hipEventRecord(alt build)");
-    c->built_recorded = true;
-    return VR_OK;
+    // frames on other streams that read the copy wait for this build (ensure_derived; `s`
+    // already waited on the previous build record there)
+    return record_build(c, s);
 }
 
 // The march variant a launch runs, as part of the schedule key: a shaded, unshaded or
