@@ -27,6 +27,12 @@ def oracle_render(vol_f32, vmin, vmax, tf, cam, W, H, params, smin=(0, 0, 0), sm
     return sc.render(row0, row1)
 
 
+def reads_half(rp, p):
+    """The last frame rendered with params p read the binary16 difference field (kernel tag
+    F32H): the oracle must restate that rounding to match it bit for bit."""
+    return "F32H" in rp.kernel_name(p)
+
+
 def compare(img, ref, rows=None):
     if rows is not None:
         img, ref = img[rows], ref[rows]
@@ -36,9 +42,18 @@ def compare(img, ref, rows=None):
     return rmse, mx
 
 
-def check(img, ref, rows=None):
+def check(img, ref, rows=None, exact=True):
+    """The tolerance of SURVEY.md §8c, then (exact) bit for bit: the kernel performs the
+    oracle's IEEE operations in the same order.  exact=False only where ref deliberately
+    differs from what the kernel computes (the exact f32 oracle against a binary16-field
+    frame)."""
     rmse, mx = compare(img, ref, rows)
     assert rmse <= RMSE_TOL and mx <= MAX_TOL, f"rmse {rmse:.3e} max {mx:.3e}"
+    if exact:
+        a = np.asarray(img, np.float32) if rows is None else np.asarray(img, np.float32)[rows]
+        b = np.asarray(ref, np.float32) if rows is None else np.asarray(ref, np.float32)[rows]
+        bad = int((a.view(np.uint32) != b.view(np.uint32)).any(axis=-1).sum())
+        assert bad == 0, f"{bad} pixels differ bitwise (rmse {rmse:.3e} max {mx:.3e})"
     return rmse, mx
 
 
@@ -128,7 +143,7 @@ def test_native_dtypes(rp, np_dtype):
     img = rp.render(cam, p)
     vf = vol.astype(np.float32)  # static_cast<float>, as the reference loader
     assert np.array_equal(rp.read_volume(), vf)
-    ref, _ = oracle_render(vf, ds.vmin, ds.vmax, tf, cam, W, H, p)
+    ref, _ = oracle_render(vf, ds.vmin, ds.vmax, tf, cam, W, H, p, grad_f16=reads_half(rp, p))
     check(img, ref)
 
 
@@ -272,7 +287,8 @@ def test_edge_viewports_and_empty_frames(rp):
             cam = synth.camera(camname).to_vr_camera()
             p = vr_amd.default_params(shading=1)
             img = rp.render(cam, p)
-            ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p)
+            ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p,
+                                   grad_f16=reads_half(rp, p))
             check(img, ref)
     # zero sizes are ignored, as framebuffer_size_changed (offscreen_pass.cpp:237-239)
     rp.framebuffer_size_changed(0, 5)
@@ -305,7 +321,8 @@ def test_near_plane_clips_part_of_the_front_face(rp, radius, rotate):
     for shading in (0, 1):
         p = vr_amd.default_params(shading=shading)
         img = rp.render(cam, p, vr_amd.OUT_RGBA32F)
-        ref, st = oracle_render(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p)
+        ref, st = oracle_render(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p,
+                                grad_f16=reads_half(rp, p))
         assert 0 < st["rays"] < W * H, st
         assert rp.count_work(cam, p) == st
         clear = np.all(ref == np.float32([0.11, 0.11, 0.11, 1.0]), axis=2)
@@ -532,7 +549,7 @@ def test_sparse_views_take_the_stencil_gradient(rp):
             rp.render(cam, pe)
             assert "<float, true, false, false, false," in rp.kernel_name(pe), rp.kernel_name(pe)
         ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p)
-        check(img, ref)
+        check(img, ref, exact=not gf)
         ref16, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p,
                                  grad_f16=gf)
         assert np.array_equal(img.view(np.uint32), ref16.view(np.uint32)), camname
@@ -808,7 +825,7 @@ def test_half_field_bit_exact(rp, vname):
             assert np.array_equal(img.view(np.uint32), ref16.view(np.uint32)), (vname, skip, env)
         assert "F32H" in rp.kernel_name(p), rp.kernel_name(p)
         if mm is None:  # the clamped volume's differences are not the exact ones
-            check(img, ref32)
+            check(img, ref32, exact=False)
         exact = rp.render(cam, vr_amd.default_params(shading=1, ert_eps=1e-5, skip_empty=skip,
                                                      exact_gradient=1), vr_amd.OUT_RGBA32F)
         assert np.array_equal(exact.view(np.uint32), ref32.view(np.uint32)), (vname, skip)
