@@ -249,8 +249,9 @@ int vr_assemble_rows(vr_ctx *ctx, const void *gathered_dev, void *out_dev, int o
  * or linear image; the reference's copy_buffer_to_image, offscreen_pass.cpp:1379-1406, then
  * copies it into the colour image on the GPU, no host round trip) -- and map `size` bytes at
  * `offset` of it on the context's device (the lowest device of a vr_create_mask context).
- * *dev_ptr can be passed to vr_render_device.  On success the import owns `fd`; release the
- * mapping with vr_release_external_memory before the exporter frees the memory. */
+ * *dev_ptr can be passed to vr_render_device.  The caller keeps `fd`: neither call closes it
+ * (measured on ROCm 7.2: the descriptor is still open after the release), so close it after
+ * vr_release_external_memory.  Release the mapping before the exporter frees the memory. */
 typedef struct vr_external_memory vr_external_memory;
 int vr_import_memory_fd(vr_ctx *ctx, int fd, uint64_t size, uint64_t offset,
                         vr_external_memory **mem, void **dev_ptr);

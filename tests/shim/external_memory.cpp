@@ -16,6 +16,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fcntl.h>
+#include <unistd.h>
 #include <vector>
 
 #include "vr/vr.h"
@@ -99,6 +101,8 @@ int main(int argc, char **argv)
     VR_CALL(ctx, vr_render_device(ctx, &cam, &p, frame, VR_OUT_RGBA8, 8, 0, 1, nullptr));
     HIP_OK(hipDeviceSynchronize());
     VR_CALL(ctx, vr_release_external_memory(ctx, mem));
+    // the caller keeps the fd (vr.h): still open after the release
+    const int fd_open = fcntl(fd, F_GETFD) != -1;
 
     // ---- the exporter reads what it was handed (its own mapping) ----
     std::vector<uint8_t> shown(size);
@@ -120,7 +124,9 @@ int main(int argc, char **argv)
     HIP_OK(hipMemAddressFree(exp_ptr, size));
     HIP_OK(hipMemRelease(handle));
     vr_destroy(ctx);
-    std::printf("external frame %ux%u group=%d offset=%zu covered=%u guard=%d match=%d\n", W, H,
-                (int)group, offset, covered, (int)guard, (int)same);
-    return same && guard && covered > 0 ? 0 : 1;
+    std::printf("external frame %ux%u group=%d offset=%zu covered=%u guard=%d match=%d "
+                "fd_open_after_release=%d\n", W, H, (int)group, offset, covered, (int)guard,
+                (int)same, fd_open);
+    if (fd_open) close(fd);
+    return same && guard && fd_open && covered > 0 ? 0 : 1;
 }

@@ -80,3 +80,4 @@ def test_frame_rendered_into_imported_memory(gpu, mask):
                        text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "match=1" in r.stdout and "guard=1" in r.stdout
+    assert "fd_open_after_release=1" in r.stdout  # the caller keeps the fd (vr.h)
