@@ -23,9 +23,11 @@ CAMS = [(1.6, None), (1.6, (40.0, 25.0)), (1.6, (360.0, 0.0)), (2.0, (180.0, 140
         (3.0, None), (1.3, (-120.0, 80.0))]
 
 
-@pytest.fixture(scope="module")
-def rp(gpu):
-    r = vr_amd.OffscreenPass(64, 48)
+@pytest.fixture(scope="module", params=[None, 0x1], ids=["device", "mask"])
+def rp(request, gpu):
+    """A one-device context, and a vr_create_mask context over device 0 (the multi-device
+    path: member contexts, frame workers, the group's own streams)."""
+    r = vr_amd.OffscreenPass(64, 48, device_mask=request.param)
     yield r
     r.close()
 
