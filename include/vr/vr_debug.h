@@ -36,10 +36,11 @@ enum vr_knob {
                                that fit 8/16 bits are stored in that type (same frames); 0:
                                keep f32 storage (next upload)                              */
     VR_KNOB_ALT_GEOMETRY = 9 /* f32 volumes: -1 auto (oblique views read a 7x15x8-cell-brick
-                               copy; sparse views a 15x15x8 z-pair one when shaded, a plain
+                               copy; sparse views the stencil copy when shaded, a plain
                                one-voxel-per-element 15^3 one when not), 0 never, 1 the
                                oblique copy, 2 the z-pair sparse copy, 3 the plain copy,
-                               whenever the launch allows it                               */
+                               4 the stencil copy (29x13x13-cell plain bricks with a 1-below /
+                               2-above apron), whenever the launch allows it               */
 };
 
 /* Set / read one knob of `ctx` (a multi-device context sets it on every device).

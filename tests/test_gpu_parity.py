@@ -742,16 +742,17 @@ def test_non_integer_uploads_stay_f32(rp):
 def test_alt_geometry_copy_bit_identical(rp):
     """f32 volumes keep further copies in alternative brick geometries that oblique views
     (7x15x8 cells, kernel tag F32Alt) and sparse views (15x15x8, F32Wide; or plain one-voxel
-    elements, F32P) read (vr_api.hip want_alt): the frames are byte-identical to the 8^3
+    elements, F32P; or plain with the gradient's apron, F32S) read (vr_api.hip want_alt): the frames are byte-identical to the 8^3
     bricks' -- unshaded and shaded (stencil gradient across every geometry's brick
     boundaries), single stage and pipelined -- the
     launch policy picks the oblique copy for the diagonal view, a sparse one for the
-    reference's default camera (z-pairs shaded, plain unshaded) and neither for the
-    frame-filling view, and a volume change rebuilds them."""
+    reference's default camera (stencil copy shaded, plain unshaded) and neither for the
+    frame-filling view, and a volume change rebuilds them.  (Policy: shaded sparse views read
+    the stencil copy, unshaded ones the plain copy.)"""
     W, H = 160, 120
     rp.framebuffer_size_changed(W, H)
     tf = synth.tf_band(0.15, 0.9)
-    want = {"default": "F32Wide", "diag": "F32Alt", "fill": None}
+    want = {"default": "F32S", "diag": "F32Alt", "fill": None}
     for seed in (31, 32):
         vol = synth.gaussians_numpy((64, 60, 66), seed=seed).astype(np.float32)
         rp.volume_dataset_changed(synth.dataset(vol))
@@ -765,7 +766,7 @@ def test_alt_geometry_copy_bit_identical(rp):
                     p = vr_amd.default_params(shading=shading, ert_eps=1e-5)
                     with rp.knobs(pipeline=pipe, grad_field=0, alt_geometry=0):
                         a = rp.render(c, p, vr_amd.OUT_RGBA32F)
-                    for alt, tag in ((1, "F32Alt"), (2, "F32Wide"), (3, "F32P")):
+                    for alt, tag in ((1, "F32Alt"), (2, "F32Wide"), (3, "F32P"), (4, "F32S")):
                         with rp.knobs(pipeline=pipe, grad_field=0, alt_geometry=alt):
                             b = rp.render(c, p, vr_amd.OUT_RGBA32F)
                             assert tag in rp.kernel_name(p)
@@ -775,9 +776,9 @@ def test_alt_geometry_copy_bit_identical(rp):
                 p = vr_amd.default_params(shading=shading, exact_gradient=1)
                 rp.render(c, p)
                 name = rp.kernel_name(p)
-                picked = next((t for t in ("F32Alt", "F32Wide", "F32P") if t in name), None)
+                picked = next((t for t in ("F32Alt", "F32Wide", "F32P", "F32S") if t in name), None)
                 w = want[camname]
-                if w == "F32Wide" and not shading:
+                if w == "F32S" and not shading:
                     w = "F32P"  # sparse and unshaded: the plain copy
                 assert picked == w, (camname, shading, name)
         ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, synth.camera("default").to_vr_camera(),

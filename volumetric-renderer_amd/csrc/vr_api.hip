@@ -57,7 +57,7 @@ struct vr_ctx {
         void *bricks = nullptr;
         size_t bytes = 0;
         bool valid = false, failed = false;
-    } alt[3];
+    } alt[4];
     uint32_t nx = 1, ny = 1, nz = 1;
     float vmin = 0.0f, vmax = 1.0f;
     // transfer function (decoded, linear float RGBA)
@@ -803,15 +803,17 @@ int ensure_derived(vr_ctx *c, const vr_params *p, MarchParams &P, hipStream_t s)
 // frame-filling, side and top views are 2-4% faster in 8^3 and stay there.  Not for
 // skip-empty, difference-field, lane-group or LDS-staged launches (the 8^3 copy keeps those
 // structures).  Returns the layout code to launch: c->layout, or ST_F32 | kAltFlag / kWideFlag
-// / kPlainF32Flag.  Knob VR_KNOB_ALT_GEOMETRY: 0 never, 1 the oblique copy, 2 the z-pair sparse
-// copy, 3 the plain f32 copy.
+// / kPlainF32Flag / kStencilF32Flag.  Knob VR_KNOB_ALT_GEOMETRY: 0 never, 1 the oblique copy, 2
+// the z-pair sparse copy, 3 the plain f32 copy, 4 the stencil copy.
 // Sparse views read the whole copy from HBM every frame, so unshaded they take the plain f32
 // copy (kPlainF32Flag, 15^3-cell bricks, 1.2x the voxels: 0.65 GB for 512^3 against 1.37 GB of
 // z-pairs); shaded, the stencil gradient's extra loads cost more there than the bytes save.
 // C3 volume, default camera r = 3, 3 frames in flight, ms per frame, two rounds
 // (profiles/r03/plain_copy/): unshaded 0.205 / 0.208 (15x15x8 z-pairs) -> 0.191 / 0.191
 // (plain); shaded 0.256 / 0.260 -> 0.260 / 0.262.  Plain bricks of 15x15x7 or 31x15x7 cells
-// measured 1-2% slower than 15^3.
+// measured 1-2% slower than 15^3.  Shaded, they take the stencil copy (kStencilF32Flag: plain
+// voxels with the gradient's apron, vr_internal.h): 0.260 / 0.261 -> 0.238 / 0.237
+// (profiles/r03/stencil2/); on the diagonal it loses to the oblique copy (0.65 -> 0.70).
 int want_alt(const vr_ctx *c, const vr_params *p, const MarchParams &P)
 {
     if (c->layout != ST_F32 || p->skip_empty || P.lds || P.pair || P.grad) return c->layout;
@@ -819,16 +821,22 @@ int want_alt(const vr_ctx *c, const vr_params *p, const MarchParams &P)
     if (c->knobs.alt >= 0)
         which = c->knobs.alt;
     else if (!c->dense_rows)
-        which = c->axis_align < kAltAlign ? 1 : (c->pixel_span > kAltSpan ? (p->shading ? 2 : 3) : 0);
+        which = c->axis_align < kAltAlign ? 1 : (c->pixel_span > kAltSpan ? (p->shading ? 4 : 3) : 0);
     switch (which) {
         case 1: return ST_F32 | kAltFlag;
         case 2: return ST_F32 | kWideFlag;
         case 3: return ST_F32 | kPlainF32Flag;
+        case 4: return ST_F32 | kStencilF32Flag;
         default: return c->layout;
     }
 }
 
-int alt_index(int layout) { return (layout & kAltFlag) ? 0 : ((layout & kWideFlag) ? 1 : 2); }
+int alt_index(int layout)
+{
+    if (layout & kAltFlag) return 0;
+    if (layout & kWideFlag) return 1;
+    return (layout & kPlainF32Flag) ? 2 : 3;
+}
 
 // Bytes of the copy of the current volume in layout `lay`.
 size_t alt_bytes_for(const vr_ctx *c, int lay)
@@ -1059,7 +1067,7 @@ bool knob_value_ok(int knob, int v)
         case VR_KNOB_PAIR_LANES: return v == 0 || v == 2 || v == 4;
         case VR_KNOB_LDS:
         case VR_KNOB_NARROW: return v == 0 || v == 1;
-        case VR_KNOB_ALT_GEOMETRY: return v >= -1 && v <= 3;
+        case VR_KNOB_ALT_GEOMETRY: return v >= -1 && v <= 4;
         case VR_KNOB_TILE_ORDER: return v >= 0 && v <= 4;
         default: return v >= -1 && v <= 1;
     }

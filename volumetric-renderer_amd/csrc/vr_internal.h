@@ -38,10 +38,13 @@ namespace vr {
 #ifndef VR_BRICK_ALIGN
 #define VR_BRICK_ALIGN 1
 #endif
-template <int X, int Y, int Z>
+// LO = 1 (the stencil copy below): every axis also stores one element below the brick's first
+// cell and one more above, so a cell's gradient taps (x - 1 .. x + 2, per axis) never leave it.
+template <int X, int Y, int Z, int LO = 0>
 struct BrickGeom {
     static constexpr int BX = X, BY = Y, BZ = Z;
-    static constexpr int EX = X + 1, EY = Y + 1, EZ = Z + 1;  // elements per axis
+    static constexpr int Lo = LO;  // apron elements below the first cell
+    static constexpr int EX = X + 1 + 2 * LO, EY = Y + 1 + 2 * LO, EZ = Z + 1 + 2 * LO;  // elements per axis
     static constexpr int Row = EX, Slice = EX * EY;           // element strides of y, z
     static constexpr int Elems = (EX * EY * EZ + VR_BRICK_ALIGN - 1) / VR_BRICK_ALIGN * VR_BRICK_ALIGN;
     __host__ __device__ static constexpr int cells(int a) { return a == 0 ? X : (a == 1 ? Y : Z); }
@@ -180,6 +183,22 @@ using GeomPlainRows = BrickGeom<VR_PLAIN_BRICK_CELLS>;
 struct F32P {
     float v;
 };
+// The stencil copy (kStencilF32Flag, kernel tag F32S): plain f32 voxels in GeomStencil bricks,
+// which store one element below and two above every cell on each axis (32 x 16 x 16 elements
+// for 29 x 13 x 13 cells: 128-B rows, 1.67x the voxels, 0.90 GB for 512^3), so a shaded
+// sample's central-difference taps are constant element offsets inside the brick: its density
+// loads are rows x - 1 .. x + 2 (16 B each) and carry the x differences, y / z taps are 8-B
+// loads, no neighbour-brick selection.  For shaded sparse views: the
+// reference's default camera 0.260 (15x15x8 z-pairs) -> 0.238 ms (profiles/r03/stencil2/;
+// 13^3 cells 0.240).
+constexpr int kStencilF32Flag = 0x200;
+#ifndef VR_STENCIL_BRICK_CELLS
+#define VR_STENCIL_BRICK_CELLS 29, 13, 13
+#endif
+using GeomStencil = BrickGeom<VR_STENCIL_BRICK_CELLS, 1>;
+struct F32S {
+    float v;
+};
 // kernel-side tag type of the f32 8^3-brick volume read with the difference field in binary16
 // (MarchParams::grad_half); kHalfFieldFlag marks that variant in kernel names and schedule keys
 // only (the bricks are the ST_F32 ones)
@@ -206,7 +225,7 @@ inline bool byte_storage(int st)
 }
 inline size_t voxels_per_element(int st)
 {
-    if (st & kPlainF32Flag) return 1;
+    if (st & (kPlainF32Flag | kStencilF32Flag)) return 1;
     return (st & 0xF) == ST_F32 ? kF32VoxelsPerElement : (byte_storage(st) ? 1 : 4);
 }
 inline size_t element_size(int st) { return storage_size(st) * voxels_per_element(st); }
@@ -216,6 +235,7 @@ inline int brick_cells(int st, int a)
     if (st & kAltFlag) return GeomAlt::cells(a);
     if (st & kWideFlag) return GeomWideRows::cells(a);
     if (st & kPlainF32Flag) return GeomPlainRows::cells(a);
+    if (st & kStencilF32Flag) return GeomStencil::cells(a);
     return byte_storage(st) ? GeomByte::cells(a) : GeomWide::cells(a);
 }
 inline size_t brick_elems(int st)
@@ -223,6 +243,7 @@ inline size_t brick_elems(int st)
     if (st & kAltFlag) return GeomAlt::Elems;
     if (st & kWideFlag) return GeomWideRows::Elems;
     if (st & kPlainF32Flag) return GeomPlainRows::Elems;
+    if (st & kStencilF32Flag) return GeomStencil::Elems;
     return byte_storage(st) ? GeomByte::Elems : GeomWide::Elems;
 }
 

@@ -89,6 +89,10 @@ template <>
 struct VoxOf<F32P> {
     using type = float;
 };
+template <>
+struct VoxOf<F32S> {
+    using type = float;
+};
 template <typename VT>
 using Vox = typename VoxOf<VT>::type;
 template <typename VT>
@@ -101,7 +105,20 @@ template <typename VT>
 constexpr bool kZPair = std::is_same<Vox<VT>, float>::value;
 // f32 voxels one per element (the F32P copy, or every f32 volume in VR_F32_PLAIN builds)
 template <typename VT>
-constexpr bool kPlainF32 = std::is_same<VT, F32P>::value || (kZPair<VT> && VR_F32_PLAIN);
+constexpr bool kPlainF32 = std::is_same<VT, F32P>::value || std::is_same<VT, F32S>::value ||
+                          (kZPair<VT> && VR_F32_PLAIN);
+// the stencil copy (GeomStencil: gradient taps inside the brick)
+template <typename VT>
+constexpr bool kStencil = std::is_same<VT, F32S>::value;
+// VR_STENCIL_WIDE = 1 (default): the stencil copy's density loads are 16 B from x - 1 (x - 1 ..
+// x + 2 of each row), so a shaded sample's x differences need no further load.  0: 8-B density
+// loads and one 16-B load per row at shade time (shaded default camera 0.240 -> 0.260 ms,
+// profiles/r03/stencil_copy/)
+#ifndef VR_STENCIL_WIDE
+#define VR_STENCIL_WIDE 1
+#endif
+template <typename VT>
+constexpr bool kStencilWide = kStencil<VT> && VR_STENCIL_WIDE;
 // 8-bit volumes stored one voxel per element (VR_U8_PLAIN, vr_internal.h)
 template <typename VT>
 constexpr bool kPlainByte = sizeof(VT) == 1 && VR_U8_PLAIN && !kIsQuad8<VT>;
@@ -113,7 +130,7 @@ using GeomOf = std::conditional_t<kPlainByte<VT>, GeomByte,
                                   std::conditional_t<std::is_same<VT, F32Alt>::value, GeomAlt,
                                   std::conditional_t<std::is_same<VT, F32Wide>::value, GeomWideRows,
                                   std::conditional_t<std::is_same<VT, F32P>::value, GeomPlainRows,
-                                                     GeomWide>>>>;
+                                  std::conditional_t<kStencil<VT>, GeomStencil, GeomWide>>>>>;
 template <typename VT>
 constexpr int kQuadWords = sizeof(VT) == 1 ? 1 : 2;
 
@@ -126,7 +143,8 @@ __device__ __forceinline__ size_t cell_offset(int pi, int pj, int pk, uint32_t n
     using G = GeomOf<VT>;
     const uint32_t ux = (uint32_t)pi, uy = (uint32_t)pj, uz = (uint32_t)pk;
     const uint32_t bx = ux / G::BX, by = uy / G::BY, bz = uz / G::BZ;
-    const uint32_t l = ((uz - bz * G::BZ) * G::EY + (uy - by * G::BY)) * G::EX + (ux - bx * G::BX);
+    const uint32_t l = ((uz - bz * G::BZ + G::Lo) * G::EY + (uy - by * G::BY + G::Lo)) * G::EX +
+                       (ux - bx * G::BX + G::Lo);
     return (size_t)brick_slot(bx, by, bz, nbx, nby) * (size_t)G::Elems + l;
 }
 
@@ -255,13 +273,25 @@ struct CellRaw<VT, std::enable_if_t<kZPair<VT> && !kPlainF32<VT>>> {
     f4a r0, r1;  // rows y and y + 1: elements x, x + 1 as z-pairs
 };
 template <typename VT>
+struct CellRaw<VT, std::enable_if_t<kStencilWide<VT>>> {
+    f4a q[4];  // rows (y|y+1, z|z+1): elements x - 1 .. x + 2
+};
+template <typename VT>
 struct CellRaw<VT, std::enable_if_t<kPlainByte<VT> && GeomByte::EX == 8>> {
     u4a q0, q1;    // slices z and z + 1: the 16 bytes from the 4-aligned address at or below e
     uint32_t sh;   // e mod 4
 };
 
+// the stencil copy with 16-B density loads keeps each row's x - 1 / x + 2 voxels for the
+// gradient (row r = dy + 2 dz)
+template <typename VT, typename = void>
+struct CellTaps {};
 template <typename VT>
-struct Cell8 {
+struct CellTaps<VT, std::enable_if_t<kStencilWide<VT>>> {
+    float xm[4], xp[4];
+};
+template <typename VT>
+struct Cell8 : CellTaps<VT> {
     float v[8];  // index dx + 2 dy + 4 dz
     // issue the loads of the cell whose low corner element is e (decode() converts them)
     static __device__ __forceinline__ void issue(CellRaw<VT> &w, const char *__restrict__ base,
@@ -270,6 +300,12 @@ struct Cell8 {
         if constexpr (kZPair<VT> && !kPlainF32<VT>) {
             w.r0 = zpair_load2(base, e);
             w.r1 = zpair_load2(base, e + GeomOf<VT>::Row);
+        } else if constexpr (kStencilWide<VT>) {
+            using G = GeomOf<VT>;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                w.q[r] = *reinterpret_cast<const f4a *>(
+                    base + (e - 1 + (size_t)((r & 1) * G::Row + (r >> 1) * G::Slice)) * 4);
         } else if constexpr (kPlainByte<VT> && GeomByte::EX == 8) {
             const size_t a = e & ~(size_t)3;
             w.sh = (uint32_t)e & 3u;
@@ -293,6 +329,14 @@ struct Cell8 {
             v[6] = w.r1.y;
             v[3] = w.r1.z;
             v[7] = w.r1.w;
+        } else if constexpr (kStencilWide<VT>) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                this->xm[r] = w.q[r].x;
+                v[2 * r] = w.q[r].y;
+                v[2 * r + 1] = w.q[r].z;
+                this->xp[r] = w.q[r].w;
+            }
         } else if constexpr (kPlainByte<VT> && GeomByte::EX == 8) {
             const uint32_t q[4] = {__builtin_amdgcn_alignbyte(w.q0.y, w.q0.x, w.sh),
                                    __builtin_amdgcn_alignbyte(w.q0.w, w.q0.z, w.sh),
@@ -310,7 +354,11 @@ struct Cell8 {
     }
     __device__ __forceinline__ void load(const char *__restrict__ base, size_t e)
     {
-        if constexpr (kPlainF32<VT>) {  // rows (y, z), (y+1, z), (y, z+1), (y+1, z+1)
+        if constexpr (kStencilWide<VT>) {
+            CellRaw<VT> w;
+            issue(w, base, e);
+            decode(w);
+        } else if constexpr (kPlainF32<VT>) {  // rows (y, z), (y+1, z), (y, z+1), (y+1, z+1)
             using G = GeomOf<VT>;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -422,7 +470,14 @@ __device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e
     // a tap outside the brick reads the neighbouring brick (constant strides in x-fastest
     // brick order, the neighbour's slot otherwise)
     long dxm, dxp, dym, dyp, dzm, dzp;
-    if constexpr (kGroupShift == 0) {
+    if constexpr (G::Lo == 1) {  // the stencil copy: every tap inside the brick
+        dxm = -1;
+        dxp = 2;
+        dym = -S;
+        dyp = 2 * S;
+        dzm = -S2;
+        dzp = 2 * S2;
+    } else if constexpr (kGroupShift == 0) {
         dxm = lx > 0 ? -1 : (Lx - B);
         dxp = lx < Lx ? 2 : (B - (Lx - 1));
         dym = ly > 0 ? -S : (Ly * S - by_stride);
@@ -453,8 +508,17 @@ __device__ __forceinline__ void gradient(const char *__restrict__ base, size_t e
             for (int dy_ = 0; dy_ < 2; ++dy_) {
                 const int o = 2 * dy_ + 4 * dz_;
                 const long r = dy_ * S + dz_ * S2;
-                Dx[o] = v[o + 1] - ld1(dxm + r);
-                Dx[o + 1] = ld1(dxp + r) - v[o];
+                if constexpr (kStencilWide<VT>) {  // taps kept by the density loads
+                    Dx[o] = v[o + 1] - c.xm[dy_ + 2 * dz_];
+                    Dx[o + 1] = c.xp[dy_ + 2 * dz_] - v[o];
+                } else if constexpr (kStencil<VT>) {  // x - 1 .. x + 2 in one load
+                    const f4a q = *reinterpret_cast<const f4a *>(base + (e - 1 + r) * 4);
+                    Dx[o] = v[o + 1] - q.x;
+                    Dx[o + 1] = q.w - v[o];
+                } else {
+                    Dx[o] = v[o + 1] - ld1(dxm + r);
+                    Dx[o + 1] = ld1(dxp + r) - v[o];
+                }
             }
 #pragma unroll
         for (int dz_ = 0; dz_ < 2; ++dz_) {
@@ -1936,9 +2000,9 @@ __global__ __launch_bounds__(256) void brick_kernel(const SrcT *__restrict__ src
         const uint32_t lx = l % G::EX, lyz = l / G::EX, lyy = lyz % G::EY, lz = lyz / G::EY;
         uint32_t bx, by, bz;
         brick_coords((uint32_t)bidx, nbx, nby, bx, by, bz);
-        const long x = (long)bx * G::BX + lx - kPad;
-        const long y = (long)by * G::BY + lyy - kPad;
-        const long z = (long)bz * G::BZ + lz - kPad;
+        const long x = (long)bx * G::BX + lx - G::Lo - kPad;
+        const long y = (long)by * G::BY + lyy - G::Lo - kPad;
+        const long z = (long)bz * G::BZ + lz - G::Lo - kPad;
         auto at = [&](long xx, long yy, long zz) -> V {
             if (xx < 0 || yy < 0 || zz < 0 || xx >= (long)nx || yy >= (long)ny || zz >= (long)nz)
                 return (V)0;
@@ -2472,6 +2536,7 @@ hipError_t brick_from(const void *src, void *dst, uint32_t nx, uint32_t ny, uint
         case ST_F32 | kAltFlag: hipLaunchKernelGGL((brick_kernel<SrcT, F32Alt>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_F32 | kWideFlag: hipLaunchKernelGGL((brick_kernel<SrcT, F32Wide>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_F32 | kPlainF32Flag: hipLaunchKernelGGL((brick_kernel<SrcT, F32P>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
+        case ST_F32 | kStencilF32Flag: hipLaunchKernelGGL((brick_kernel<SrcT, F32S>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
         default: hipLaunchKernelGGL((brick_kernel<SrcT, float>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
     }
     return hipGetLastError();
@@ -2496,8 +2561,10 @@ hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &
         case ST_F32 | kAltFlag:
         case ST_F32 | kWideFlag:
         case ST_F32 | kPlainF32Flag:
+        case ST_F32 | kStencilF32Flag:
             if (count || p.pair || p.lds || p.skip_empty || p.grad) return hipErrorInvalidValue;
             if (storage & kPlainF32Flag) return launch_march_alt<F32P>(shade, p, stream);
+            if (storage & kStencilF32Flag) return launch_march_alt<F32S>(shade, p, stream);
             return (storage & kAltFlag) ? launch_march_alt<F32Alt>(shade, p, stream)
                                         : launch_march_alt<F32Wide>(shade, p, stream);
         default: return hipErrorInvalidValue;
@@ -2509,11 +2576,11 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
     // demangled names as rocprofv3 reports them (kernel-trace "Kernel_Name"); storage is the
     // layout code (8-bit yz-quads: the Quad8 instantiations)
     static const std::vector<std::string> names = [] {
-        const char *types[11] = {"unsigned char", "signed char", "unsigned short", "short", "float",
+        const char *types[12] = {"unsigned char", "signed char", "unsigned short", "short", "float",
                                  "vr::Quad8<unsigned char>", "vr::Quad8<signed char>", "vr::F32Alt",
-                                 "vr::F32Wide", "vr::F32H", "vr::F32P"};
+                                 "vr::F32Wide", "vr::F32H", "vr::F32P", "vr::F32S"};
         std::vector<std::string> v;
-        for (int t = 0; t < 11; ++t)
+        for (int t = 0; t < 12; ++t)
             for (int k = 0; k < 32; ++k) {
                 std::string n = std::string("void vr::(anonymous namespace)::march_kernel<") + types[t];
                 for (int bit = 4; bit >= 0; --bit) n += (k >> bit) & 1 ? ", true" : ", false";
@@ -2526,7 +2593,8 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
     if (storage & kWideFlag) storage = 8;
     if (storage & kHalfFieldFlag) storage = 9;
     if (storage & kPlainF32Flag) storage = 10;
-    if (storage < 0 || storage > 10) return "march_kernel<?>";
+    if (storage & kStencilF32Flag) storage = 11;
+    if (storage < 0 || storage > 11) return "march_kernel<?>";
     const int k = (shade ? 16 : 0) + (count ? 8 : 0) + (skip ? 4 : 0) + (gf ? 2 : 0) + (pipe ? 1 : 0);
     return names[storage * 32 + k].c_str();
 }
