@@ -240,12 +240,9 @@ __device__ __forceinline__ f2a zpair_load1(const char *__restrict__ base, size_t
     return *reinterpret_cast<const f2a *>(base + e * 8);
 }
 
-#ifndef VR_U8_DWORD
-#define VR_U8_DWORD 0
-#endif
 // Global loads one Cell8::load issues.
 template <typename VT>
-constexpr int kCellLoads = kZPair<VT> ? (kPlainF32<VT> ? 4 : 2) : (kPlainByte<VT> ? (VR_U8_DWORD ? 4 : 2) : 1);
+constexpr int kCellLoads = kZPair<VT> ? (kPlainF32<VT> ? 4 : 2) : (kPlainByte<VT> ? 2 : 1);
 
 // s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt bits [3:0] + [15:14], expcnt and lgkmcnt left at
 // their no-wait maxima).  The pipelined march places it, in code every active lane runs, where
@@ -279,20 +276,10 @@ template <typename VT>
 struct CellRaw<VT, std::enable_if_t<kStencilWide<VT>>> {
     f4a q[4];  // rows (y|y+1, z|z+1): elements x - 1 .. x + 2
 };
-// VR_U8_DWORD = 1: a plain 8-bit sample is 4 byte-aligned dword loads (rows y, y + 1 of slices
-// z, z + 1, each from the cell's own byte: voxels x, x + 1 in its low bytes), 4 B per lane each
-// instead of 2 x 16 B from the 4-aligned address below (the unaligned access mode of gfx9+).
-typedef uint32_t u32u __attribute__((aligned(1)));
 template <typename VT>
-constexpr bool kByteDword = kPlainByte<VT> && GeomByte::EX == 8 && VR_U8_DWORD;
-template <typename VT>
-struct CellRaw<VT, std::enable_if_t<kPlainByte<VT> && GeomByte::EX == 8 && !VR_U8_DWORD>> {
+struct CellRaw<VT, std::enable_if_t<kPlainByte<VT> && GeomByte::EX == 8>> {
     u4a q0, q1;    // slices z and z + 1: the 16 bytes from the 4-aligned address at or below e
     uint32_t sh;   // e mod 4
-};
-template <typename VT>
-struct CellRaw<VT, std::enable_if_t<kByteDword<VT>>> {
-    uint32_t d[4];  // r = dy + 2 dz: the 4 bytes from the cell's element of row y + dy, slice z + dz
 };
 
 // the stencil copy with 16-B density loads keeps each row's x - 1 / x + 2 voxels for the
@@ -319,11 +306,6 @@ struct Cell8 : CellTaps<VT> {
             for (int r = 0; r < 4; ++r)
                 w.q[r] = *reinterpret_cast<const f4a *>(
                     base + (e - 1 + (size_t)((r & 1) * G::Row + (r >> 1) * G::Slice)) * 4);
-        } else if constexpr (kByteDword<VT>) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                w.d[r] = *reinterpret_cast<const u32u *>(
-                    base + e + (size_t)((r & 1) * GeomByte::Row + (r >> 1) * GeomByte::Slice));
         } else if constexpr (kPlainByte<VT> && GeomByte::EX == 8) {
             const size_t a = e & ~(size_t)3;
             w.sh = (uint32_t)e & 3u;
@@ -355,12 +337,6 @@ struct Cell8 : CellTaps<VT> {
                 v[2 * r + 1] = w.q[r].z;
                 this->xp[r] = w.q[r].w;
             }
-        } else if constexpr (kByteDword<VT>) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                v[2 * r] = byte_value<VT>(w.d[r], 0);
-                v[2 * r + 1] = byte_value<VT>(w.d[r], 1);
-            }
         } else if constexpr (kPlainByte<VT> && GeomByte::EX == 8) {
             const uint32_t q[4] = {__builtin_amdgcn_alignbyte(w.q0.y, w.q0.x, w.sh),
                                    __builtin_amdgcn_alignbyte(w.q0.w, w.q0.z, w.sh),
@@ -378,7 +354,7 @@ struct Cell8 : CellTaps<VT> {
     }
     __device__ __forceinline__ void load(const char *__restrict__ base, size_t e)
     {
-        if constexpr (kStencilWide<VT> || kByteDword<VT>) {
+        if constexpr (kStencilWide<VT>) {
             CellRaw<VT> w;
             issue(w, base, e);
             decode(w);
