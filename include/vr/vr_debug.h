@@ -39,7 +39,7 @@ enum vr_knob {
                                copy; sparse views the stencil copy when shaded, a plain
                                one-voxel-per-element 15^3 one when not), 0 never, 1 the
                                oblique copy, 2 the z-pair sparse copy, 3 the plain copy,
-                               4 the stencil copy (29x13x13-cell plain bricks with a 1-below /
+                               4 the stencil copy (29^3-cell plain bricks with a 1-below /
                                2-above apron), whenever the launch allows it               */
 };
 

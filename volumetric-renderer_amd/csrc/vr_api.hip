@@ -812,8 +812,8 @@ int ensure_derived(vr_ctx *c, const vr_params *p, MarchParams &P, hipStream_t s)
 // (profiles/r03/plain_copy/): unshaded 0.205 / 0.208 (15x15x8 z-pairs) -> 0.191 / 0.191
 // (plain); shaded 0.256 / 0.260 -> 0.260 / 0.262.  Plain bricks of 15x15x7 or 31x15x7 cells
 // measured 1-2% slower than 15^3.  Shaded, they take the stencil copy (kStencilF32Flag: plain
-// voxels with the gradient's apron, vr_internal.h): 0.260 / 0.261 -> 0.238 / 0.237
-// (profiles/r03/stencil2/); on the diagonal it loses to the oblique copy (0.65 -> 0.70).
+// voxels with the gradient's apron, vr_internal.h): 0.260 / 0.261 -> 0.232 / 0.230
+// (profiles/r03/stencil2/ .. stencil4/); on the diagonal it loses to the oblique copy.
 int want_alt(const vr_ctx *c, const vr_params *p, const MarchParams &P)
 {
     if (c->layout != ST_F32 || p->skip_empty || P.lds || P.pair || P.grad) return c->layout;

@@ -184,16 +184,16 @@ struct F32P {
     float v;
 };
 // The stencil copy (kStencilF32Flag, kernel tag F32S): plain f32 voxels in GeomStencil bricks,
-// which store one element below and two above every cell on each axis (32 x 16 x 16 elements
-// for 29 x 13 x 13 cells: 128-B rows, 1.67x the voxels, 0.90 GB for 512^3), so a shaded
+// which store one element below and two above every cell on each axis (32^3 elements for 29^3
+// cells: 128-B rows, 1.34x the voxels, 0.76 GB for 512^3), so a shaded
 // sample's central-difference taps are constant element offsets inside the brick: its density
 // loads are rows x - 1 .. x + 2 (16 B each) and carry the x differences, y / z taps are 8-B
 // loads, no neighbour-brick selection.  For shaded sparse views: the
-// reference's default camera 0.260 (15x15x8 z-pairs) -> 0.238 ms (profiles/r03/stencil2/;
-// 13^3 cells 0.240).
+// reference's default camera 0.260 (15x15x8 z-pairs) -> 0.231 ms (profiles/r03/stencil2/ ..
+// stencil4/: 13^3 cells 0.240, 29x13x13 0.236, 29x13x29 / 29x13x61 / 29^3 0.231).
 constexpr int kStencilF32Flag = 0x200;
 #ifndef VR_STENCIL_BRICK_CELLS
-#define VR_STENCIL_BRICK_CELLS 29, 13, 13
+#define VR_STENCIL_BRICK_CELLS 29, 29, 29
 #endif
 using GeomStencil = BrickGeom<VR_STENCIL_BRICK_CELLS, 1>;
 struct F32S {
