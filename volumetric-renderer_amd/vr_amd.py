@@ -600,7 +600,7 @@ class DistFrames:
             pass
 
 
-KERNEL_SOURCES = ("csrc/vr_kernels.hip", "csrc/vr_internal.h", "csrc/vr_exact_math.h")
+KERNEL_SOURCES = ("csrc/vr_kernels.hip", "csrc/vr_internal.h", "csrc/vr_exact_math.h", "Makefile")
 
 
 def kernel_source_hash() -> str:
