@@ -50,6 +50,19 @@ static void glm_perspective_rh_no(float fovy, float aspect, float zn, float zf, 
     m[3 * 4 + 2] = -(2.0f * zf * zn) / (zf - zn);
 }
 
+/* glm::perspectiveRH_ZO: the form GLM_FORCE_DEPTH_ZERO_TO_ONE selects (conformance variant
+ * OR_CONF_CLIP_ZO: the define at offscreen_pass.cpp:3 taking effect after all). */
+static void glm_perspective_rh_zo(float fovy, float aspect, float zn, float zf, float *m)
+{
+    memset(m, 0, 16 * sizeof(float));
+    float th = tanf(fovy / 2.0f);
+    m[0 * 4 + 0] = 1.0f / (aspect * th);
+    m[1 * 4 + 1] = 1.0f / th;
+    m[2 * 4 + 2] = zf / (zn - zf);
+    m[2 * 4 + 3] = -1.0f;
+    m[3 * 4 + 2] = -(zf * zn) / (zf - zn);
+}
+
 /* coordinate_conversion = rotate(I, radians(90), x) * scale(I, (-1,1,1)), glm float math
  * (offscreen_pass.cpp:1159-1162). */
 static void coordinate_conversion(float *m)
@@ -125,7 +138,73 @@ static int inverse4d(const double *m, double *inv)
 typedef struct ray_frame {
     double inv[16];
     int ok;
+    /* OR_CONF_RASTER: window coordinates of the cube's 24 vertices in 2^-8 pixel units, their
+     * clip w, which of the 12 triangles face the camera, twice their signed window area */
+    int raster, raster_bad;
+    int64_t sx[24], sy[24];
+    float w[24];
+    int front[12];
+    int64_t area[12];
 } ray_frame;
+
+/* The cube of offscreen_pass.cpp:55-90 as faces: 4 vertices each in the table's order (tex =
+ * position + 0.5), indexed {0,1,2, 0,2,3} per face (:87-89).  Face f: axis, side of the
+ * constant coordinate, and the (u, v) axes walked by its 4 vertices. */
+static const int CUBE_FACE[6][2] = {{2, +1}, {1, -1}, {0, +1}, {1, +1}, {0, -1}, {2, -1}};
+static const float CUBE_VERT[24][3] = {
+    {-0.5f, -0.5f, 0.5f}, {0.5f, -0.5f, 0.5f}, {0.5f, 0.5f, 0.5f}, {-0.5f, 0.5f, 0.5f},
+    {-0.5f, -0.5f, -0.5f}, {0.5f, -0.5f, -0.5f}, {0.5f, -0.5f, 0.5f}, {-0.5f, -0.5f, 0.5f},
+    {0.5f, -0.5f, -0.5f}, {0.5f, 0.5f, -0.5f}, {0.5f, 0.5f, 0.5f}, {0.5f, -0.5f, 0.5f},
+    {0.5f, 0.5f, -0.5f}, {-0.5f, 0.5f, -0.5f}, {-0.5f, 0.5f, 0.5f}, {0.5f, 0.5f, 0.5f},
+    {-0.5f, 0.5f, -0.5f}, {-0.5f, -0.5f, -0.5f}, {-0.5f, -0.5f, 0.5f}, {-0.5f, 0.5f, 0.5f},
+    {-0.5f, 0.5f, -0.5f}, {0.5f, 0.5f, -0.5f}, {0.5f, -0.5f, -0.5f}, {-0.5f, -0.5f, -0.5f},
+};
+static inline int cube_index(int t, int k)
+{
+    static const int q[6] = {0, 1, 2, 0, 2, 3};
+    return (t / 2) * 4 + q[(t % 2) * 3 + k];
+}
+
+static void make_raster(const or_scene *s, const float *pv, ray_frame *f)
+{
+    f->raster = 1;
+    f->raster_bad = 0;
+    const float W = (float)s->width, H = (float)s->height;
+    float cz[24];
+    for (int v = 0; v < 24; ++v) {
+        /* volume.vert:23 gl_Position = (proj * view) * vec4(in_position, 1): glm mat * vec */
+        float c[4];
+        for (int r = 0; r < 4; ++r) {
+            float acc = pv[0 * 4 + r] * CUBE_VERT[v][0];
+            acc = acc + pv[1 * 4 + r] * CUBE_VERT[v][1];
+            acc = acc + pv[2 * 4 + r] * CUBE_VERT[v][2];
+            acc = acc + pv[3 * 4 + r];
+            c[r] = acc;
+        }
+        f->w[v] = c[3];
+        cz[v] = c[2];
+        /* viewport (0, 0, W, H): xf = W/2 * xd + W/2 (Vulkan "Controlling the Viewport"),
+         * snapped to the 2^-8 sub-pixel grid */
+        const float xf = (W * 0.5f) * (c[0] / c[3]) + W * 0.5f;
+        const float yf = (H * 0.5f) * (c[1] / c[3]) + H * 0.5f;
+        f->sx[v] = llrintf(xf * 256.0f);
+        f->sy[v] = llrintf(yf * 256.0f);
+    }
+    for (int t = 0; t < 12; ++t) {
+        const int face = t / 2, ax = CUBE_FACE[face][0], side = CUBE_FACE[face][1];
+        /* back-face cull (offscreen_pass.cpp:680-681); the object-space facing test equals the
+         * window-area sign for every non-degenerate triangle */
+        f->front[t] = (float)side * s->cam_pos[ax] > 0.5f;
+        const int a = cube_index(t, 0), b = cube_index(t, 1), c = cube_index(t, 2);
+        f->area[t] = (f->sx[b] - f->sx[a]) * (f->sy[c] - f->sy[a]) -
+                     (f->sy[b] - f->sy[a]) * (f->sx[c] - f->sx[a]);
+        if (f->front[t])
+            for (int k = 0; k < 3; ++k) {
+                const int v = cube_index(t, k);
+                if (!(f->w[v] > 0.0f) || cz[v] < 0.0f || cz[v] > f->w[v]) f->raster_bad = 1;
+            }
+    }
+}
 
 static void make_ray_frame(const or_scene *s, ray_frame *f)
 {
@@ -134,13 +213,87 @@ static void make_ray_frame(const or_scene *s, ray_frame *f)
     float zf = s->zfar > 0.0f ? s->zfar : 10.0f;
     float aspect = (float)s->width / (float)s->height;
     float persp[16], conv[16], proj[16], pv[16];
-    glm_perspective_rh_no(fovy, aspect, zn, zf, persp);
+    if (s->conf_flags & OR_CONF_CLIP_ZO)
+        glm_perspective_rh_zo(fovy, aspect, zn, zf, persp);
+    else
+        glm_perspective_rh_no(fovy, aspect, zn, zf, persp);
     coordinate_conversion(conv);
     glm_mul(persp, conv, proj);
     glm_mul(proj, s->view, pv);
     double pvd[16];
     for (int i = 0; i < 16; ++i) pvd[i] = (double)pv[i];
     f->ok = inverse4d(pvd, f->inv);
+    f->raster = 0;
+    f->raster_bad = 0;
+    if (s->conf_flags & OR_CONF_RASTER) make_raster(s, pv, f);
+}
+
+/* volume.frag:23 ray_dir = normalize(in_frag_position - camera_position) */
+static void ray_direction(const or_scene *s, const float frag[3], float dir[3])
+{
+    float vx = frag[0] - s->cam_pos[0];
+    float vy = frag[1] - s->cam_pos[1];
+    float vz = frag[2] - s->cam_pos[2];
+    float len2 = vx * vx + vy * vy + vz * vz;
+    if (s->conf_flags & OR_CONF_GPU_MATH) {
+        const float rs = (float)(1.0 / sqrt((double)len2)); /* correctly rounded rsqrt */
+        dir[0] = vx * rs;
+        dir[1] = vy * rs;
+        dir[2] = vz * rs;
+        return;
+    }
+    float len = sqrtf(len2);
+    dir[0] = vx / len;
+    dir[1] = vy / len;
+    dir[2] = vz / len;
+}
+
+/* OR_CONF_RASTER: the front triangle covering the pixel centre (exact integer edge functions
+ * on the snapped grid; a sample exactly on an edge belongs to the triangle for which that edge
+ * is a "top-left" one, so a shared edge is covered once) and its perspective-correct
+ * attributes, f = sum(l_k f_k / w_k) / sum(l_k / w_k) in float. */
+static int pixel_ray_raster(const or_scene *s, const ray_frame *f, int px, int py, float tex[3],
+                            float frag[3], float dir[3])
+{
+    const int64_t X = (int64_t)px * 256 + 128, Y = (int64_t)py * 256 + 128;
+    for (int t = 0; t < 12; ++t) {
+        if (!f->front[t] || f->area[t] == 0) continue;
+        int v[3] = {cube_index(t, 0), cube_index(t, 1), cube_index(t, 2)};
+        int64_t area = f->area[t];
+        if (area < 0) {
+            const int tmp = v[1];
+            v[1] = v[2];
+            v[2] = tmp;
+            area = -area;
+        }
+        int64_t e[3];
+        int inside = 1;
+        for (int k = 0; k < 3 && inside; ++k) {
+            const int a = v[(k + 1) % 3], b = v[(k + 2) % 3]; /* the edge opposite vertex k */
+            const int64_t dx = f->sx[b] - f->sx[a], dy = f->sy[b] - f->sy[a];
+            e[k] = dx * (Y - f->sy[a]) - dy * (X - f->sx[a]);
+            if (e[k] < 0 || (e[k] == 0 && !(dy < 0 || (dy == 0 && dx > 0)))) inside = 0;
+        }
+        if (!inside) continue;
+        float a[3], sum = 0.0f;
+        for (int k = 0; k < 3; ++k) {
+            a[k] = ((float)e[k] / (float)area) / f->w[v[k]];
+            sum = sum + a[k];
+        }
+        for (int c = 0; c < 3; ++c) {
+            float fp = a[0] * CUBE_VERT[v[0]][c];
+            fp = fp + a[1] * CUBE_VERT[v[1]][c];
+            fp = fp + a[2] * CUBE_VERT[v[2]][c];
+            float tc = a[0] * (CUBE_VERT[v[0]][c] + 0.5f);
+            tc = tc + a[1] * (CUBE_VERT[v[1]][c] + 0.5f);
+            tc = tc + a[2] * (CUBE_VERT[v[2]][c] + 0.5f);
+            frag[c] = fp / sum;
+            tex[c] = tc / sum;
+        }
+        ray_direction(s, frag, dir);
+        return 1;
+    }
+    return 0;
 }
 
 /* Ray entry of one pixel: the cube's camera-facing face hit by the pixel-centre ray,
@@ -149,6 +302,7 @@ static void make_ray_frame(const or_scene *s, ray_frame *f)
 static int pixel_ray(const or_scene *s, const ray_frame *f, int px, int py, float tex[3],
                      float frag[3], float dir[3])
 {
+    if (f->raster) return pixel_ray_raster(s, f, px, py, tex, frag, dir);
     if (!f->ok) return 0;
     const double *m = f->inv;
     double x = ((double)px + 0.5) / (double)s->width * 2.0 - 1.0;
@@ -191,14 +345,7 @@ static int pixel_ray(const or_scene *s, const ray_frame *f, int px, int py, floa
     }
     frag[axis] = d[axis] > 0.0 ? -0.5f : 0.5f;
     tex[axis] = d[axis] > 0.0 ? 0.0f : 1.0f;
-    /* volume.frag:23  ray_dir = normalize(in_frag_position - camera_position) */
-    float vx = frag[0] - s->cam_pos[0];
-    float vy = frag[1] - s->cam_pos[1];
-    float vz = frag[2] - s->cam_pos[2];
-    float len = sqrtf(vx * vx + vy * vy + vz * vz);
-    dir[0] = vx / len;
-    dir[1] = vy / len;
-    dir[2] = vz / len;
+    ray_direction(s, frag, dir);
     return 1;
 }
 
@@ -325,6 +472,21 @@ static inline float grad_cell_f16(const vsrc *v, int nx, int ny, int nz, int i, 
 }
 
 /* Normalised coordinate -> texel space: u = s*N - 0.5 (texel i's centre at (i+0.5)/N). */
+/* Conformance variant conf_weight_bits = b > 0: u on the 2^-b grid (subTexelPrecisionBits),
+ * round to nearest even, so floor(u) and frac(u) come from the quantised coordinate. */
+static inline float quantise_u(float u, int bits)
+{
+    return bits > 0 ? ldexpf(rintf(ldexpf(u, bits)), -bits) : u;
+}
+
+static inline void texel_coord_q(float p, int n, int bits, int *i, float *a)
+{
+    float u = quantise_u(p * (float)n - 0.5f, bits);
+    float f = floorf(u);
+    *a = u - f;
+    *i = (int)f;
+}
+
 static inline void texel_coord(float p, int n, int *i, float *a)
 {
     float u = p * (float)n - 0.5f;
@@ -370,6 +532,19 @@ void or_tf_decode(const uint32_t *tf, int n, float *lut)
 
 /* 1D LINEAR filter, CLAMP_TO_EDGE (offscreen_pass.cpp:1125-1150).  The clamp of u to
  * [-1, n] keeps the float->int conversion defined for t = +-inf/NaN (min == max). */
+static inline void tf_lookup_q(const float *lut, int n, float t, int bits, float out[4])
+{
+    float u = t * (float)n - 0.5f;
+    u = fminf(fmaxf(u, -1.0f), (float)n);
+    u = quantise_u(u, bits);
+    float f = floorf(u);
+    float w = u - f;
+    int i0 = (int)f, i1 = i0 + 1;
+    i0 = i0 < 0 ? 0 : (i0 > n - 1 ? n - 1 : i0);
+    i1 = i1 < 0 ? 0 : (i1 > n - 1 ? n - 1 : i1);
+    for (int c = 0; c < 4; ++c) out[c] = lerpf(lut[i0 * 4 + c], lut[i1 * 4 + c], w);
+}
+
 static inline void tf_lookup(const float *lut, int n, float t, float out[4])
 {
     float u = t * (float)n - 0.5f;
@@ -407,8 +582,11 @@ static float powi(float x, int p)
     return r;
 }
 
-static void march_pixel(const or_scene *s, const ray_frame *f, const float *lut, int px,
-                        int py, float *out, or_stats *st)
+/* conf = 0: the oracle (conformance fields ignored, the baseline's hot path unchanged);
+ * conf = 1: the conformance variants of s->conf_weight_bits / s->conf_flags. */
+static inline __attribute__((always_inline)) void
+march_pixel_impl(const or_scene *s, const ray_frame *f, const float *lut, int px, int py,
+                 float *out, or_stats *st, const int conf)
 {
     float tex[3], frag[3], dir[3];
     if (!pixel_ray(s, f, px, py, tex, frag, dir)) {
@@ -432,19 +610,24 @@ static void march_pixel(const or_scene *s, const ray_frame *f, const float *lut,
             p1 > s->smin[1] && p2 > s->smin[2]) {
             int i, j, k;
             float ax, ay, az;
-            texel_coord(p0, nx, &i, &ax);
-            texel_coord(p1, ny, &j, &ay);
-            texel_coord(p2, nz, &k, &az);
+            const int qb = conf ? s->conf_weight_bits : 0;
+            texel_coord_q(p0, nx, qb, &i, &ax);
+            texel_coord_q(p1, ny, qb, &j, &ay);
+            texel_coord_q(p2, nz, qb, &k, &az);
             const float d = tri_cell(&src, nx, ny, nz, i, j, k, ax, ay, az); /* :41 */
-            const float t = (d - s->vmin) / range;                              /* :42 */
+            const float t = (conf && (s->conf_flags & OR_CONF_GPU_MATH))
+                                ? (d - s->vmin) * (float)(1.0 / (double)range)
+                                : (d - s->vmin) / range; /* :42 */
             float sc[4];
-            tf_lookup(lut, s->tf_n, t, sc); /* :43 */
+            tf_lookup_q(lut, s->tf_n, t, qb, sc); /* :43 */
             st->samples++;
             if (s->shading && sc[3] > 0.0f) {
                 /* extension: central differences one texel apart, same weights (grad_cell) */
                 float gx, gy, gz;
                 if (s->grad_f16) {
-                    const float sc = ldexpf(1.0f, or_field_scale_log2(s->vmin, s->vmax));
+                    const float sc = ldexpf(1.0f, s->grad_range_set
+                                                      ? or_field_scale_log2(s->grad_range[0], s->grad_range[1])
+                                                      : or_field_scale_log2(s->vmin, s->vmax));
                     gx = grad_cell_f16(&src, nx, ny, nz, i, j, k, ax, ay, az, 0, sc);
                     gy = grad_cell_f16(&src, nx, ny, nz, i, j, k, ax, ay, az, 1, sc);
                     gz = grad_cell_f16(&src, nx, ny, nz, i, j, k, ax, ay, az, 2, sc);
@@ -467,17 +650,29 @@ static void march_pixel(const or_scene *s, const ray_frame *f, const float *lut,
                 }
             }
             /* volume.frag:44-45  C.rgb += T * (s.a * s.rgb);  T *= 1 - s.a */
-            cr = cr + (sc[0] * sc[3]) * T;
-            cg = cg + (sc[1] * sc[3]) * T;
-            cb = cb + (sc[2] * sc[3]) * T;
+            if (conf && (s->conf_flags & OR_CONF_FMA)) {
+                cr = fmaf(sc[0] * sc[3], T, cr);
+                cg = fmaf(sc[1] * sc[3], T, cg);
+                cb = fmaf(sc[2] * sc[3], T, cb);
+            } else {
+                cr = cr + (sc[0] * sc[3]) * T;
+                cg = cg + (sc[1] * sc[3]) * T;
+                cb = cb + (sc[2] * sc[3]) * T;
+            }
             T = T * (1.0f - sc[3]);
             if (T == 0.0f) break; /* exact: later samples add (rgb*a)*0 */
             if (T < s->ert_eps) break;
         }
         /* volume.frag:47  ray_pos += ray_dir * step_size */
-        p0 = p0 + dir[0] * step;
-        p1 = p1 + dir[1] * step;
-        p2 = p2 + dir[2] * step;
+        if (conf && (s->conf_flags & OR_CONF_FMA)) {
+            p0 = fmaf(dir[0], step, p0);
+            p1 = fmaf(dir[1], step, p1);
+            p2 = fmaf(dir[2], step, p2);
+        } else {
+            p0 = p0 + dir[0] * step;
+            p1 = p1 + dir[1] * step;
+            p2 = p2 + dir[2] * step;
+        }
     }
     /* volume.frag:50 alpha = 1 - T; blend SRC_ALPHA / ONE_MINUS_SRC_ALPHA over clear */
     const float A = 1.0f - T;
@@ -486,6 +681,15 @@ static void march_pixel(const or_scene *s, const ray_frame *f, const float *lut,
     out[1] = cg * A + s->clear[1] * omA;
     out[2] = cb * A + s->clear[2] * omA;
     out[3] = A * A + s->clear[3] * omA;
+}
+
+static void march_pixel(const or_scene *s, const ray_frame *f, const float *lut, int px,
+                        int py, float *out, or_stats *st)
+{
+    if (s->conf_flags == 0 && s->conf_weight_bits == 0)
+        march_pixel_impl(s, f, lut, px, py, out, st, 0);
+    else
+        march_pixel_impl(s, f, lut, px, py, out, st, 1);
 }
 
 int or_render_rows(const or_scene *s, float *out, int row0, int row1, int nthreads,
@@ -497,6 +701,7 @@ int or_render_rows(const or_scene *s, float *out, int row0, int row1, int nthrea
     if (row1 > s->height) row1 = s->height;
     ray_frame f;
     make_ray_frame(s, &f);
+    if (f.raster_bad) return -95; /* OR_CONF_RASTER needs no near/far clipping */
     float *lut = (float *)malloc((size_t)s->tf_n * 4 * sizeof(float));
     if (!lut) return -12;
     or_tf_decode(s->tf, s->tf_n, lut);
@@ -532,6 +737,7 @@ int or_render_row_list(const or_scene *s, float *out, const int32_t *rows, int n
         return -22;
     ray_frame f;
     make_ray_frame(s, &f);
+    if (f.raster_bad) return -95; /* OR_CONF_RASTER needs no near/far clipping */
     float *lut = (float *)malloc((size_t)s->tf_n * 4 * sizeof(float));
     if (!lut) return -12;
     or_tf_decode(s->tf, s->tf_n, lut);

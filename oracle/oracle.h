@@ -92,7 +92,38 @@ typedef struct or_scene {
      * frame that reads the field): every central difference D becomes round_f16(D * 2^k),
      * k = or_field_scale_log2(vmin, vmax); 0 = exact f32 differences */
     int32_t grad_f16;
+    /* Conformance study (tools/conformance_gap.py).  Each field restates one
+     * implementation-defined freedom a conformant Vulkan run of the reference may take; all
+     * are 0 (off) by default, and the product kernel's parity target is that default.
+     * conf_weight_bits: 0 = exact float filter weights; b > 0 = the texel coordinate
+     *   u = s*N - 0.5 of the 3D and 1D LINEAR filters rounded to a multiple of 2^-b
+     *   (subTexelPrecisionBits; spec minimum 4), round to nearest, before floor/frac. */
+    int32_t conf_weight_bits;
+    int32_t conf_flags; /* OR_CONF_* below */
+    /* grad_f16: the range the device takes the field's scale from -- the stored data's own
+     * min/max (vr_api.hip data_range), not vmin/vmax, which may be a narrower display window.
+     * grad_range_set == 0: use vmin/vmax (equal to the data range for every Dataset). */
+    int32_t grad_range_set;
+    float grad_range[2];
 } or_scene;
+
+/* FMA contraction the SPIR-V permits (volume_frag.spv carries no NoContraction decoration,
+ * tests/test_spirv_facts.py): ray_pos = fma(ray_dir, step, ray_pos) (volume.frag:47) and
+ * C.rgb = fma(rgb*a, T, C.rgb) (volume.frag:44). */
+#define OR_CONF_FMA 1
+/* glm's [0, 1] clip form: perspectiveRH_ZO instead of _NO (offscreen_pass.cpp:3,1166), i.e.
+ * GLM_FORCE_DEPTH_ZERO_TO_ONE in effect; moves the effective near plane 0.198 -> 0.1. */
+#define OR_CONF_CLIP_ZO 2
+/* Entry attributes (in_tex_coords, in_frag_position) from a rasteriser model instead of the
+ * exact double ray/box intersection: float clip positions ((proj*view)*v, volume.vert:23),
+ * window coordinates snapped to 2^-8 pixel (subPixelPrecisionBits = 8), exact integer edge
+ * functions, float perspective-correct barycentrics ("Basic Polygon Rasterization").  Needs
+ * every front-facing vertex inside 0 <= z <= w (no near clipping); returns -95 otherwise. */
+#define OR_CONF_RASTER 4
+/* GPU shader arithmetic at its permitted precision: the density quotient as d * rcp(range)
+ * and normalize() as v * rsqrt(dot(v, v)) with correctly rounded rcp/rsqrt (GLSL's OpFDiv
+ * allows 2.5 ulp, inversesqrt 2 ulp; this is the common 1-instruction code generation). */
+#define OR_CONF_GPU_MATH 8
 
 typedef struct or_stats {
     uint64_t rays, samples, shaded_samples, steps;

@@ -35,7 +35,13 @@ class or_scene(C.Structure):
         ("ka", C.c_float), ("kd", C.c_float), ("ks", C.c_float), ("spec_power", C.c_int32),
         ("vol_u8", C.POINTER(C.c_uint8)),
         ("grad_f16", C.c_int32),
+        ("conf_weight_bits", C.c_int32), ("conf_flags", C.c_int32),
+        ("grad_range_set", C.c_int32), ("grad_range", C.c_float * 2),
     ]
+
+
+# conformance-study variants (oracle.h OR_CONF_*; tools/conformance_gap.py)
+CONF_FMA, CONF_CLIP_ZO, CONF_RASTER, CONF_GPU_MATH = 1, 2, 4, 8
 
 
 class or_stats(C.Structure):
@@ -81,7 +87,8 @@ class Scene:
     def __init__(self, vol, vmin, vmax, tf, view, cam_pos, width, height, smin=(0, 0, 0),
                  smax=(1, 1, 1), step=0.005, ray_dist=1.8, ert_eps=0.0, shading=0,
                  clear=(0.11, 0.11, 0.11, 1.0), ka=0.3, kd=0.7, ks=0.25, spec_power=16,
-                 fovy_deg=40.0, znear=0.1, zfar=10.0, grad_f16=False):
+                 fovy_deg=40.0, znear=0.1, zfar=10.0, grad_f16=False, conf_weight_bits=0,
+                 conf_flags=0):
         # (nz, ny, nx); u8 volumes are kept as u8 (float(v) is exact: same samples, 1/4 the
         # host memory of a float copy, e.g. C5's 2048^3)
         if np.asarray(vol).dtype == np.uint8:
@@ -112,7 +119,19 @@ class Scene:
             s.clear[i] = float(clear[i])
         s.ka, s.kd, s.ks, s.spec_power = ka, kd, ks, int(spec_power)
         s.grad_f16 = 1 if grad_f16 else 0
+        if grad_f16:  # the device scales the binary16 field by the stored data's own range
+            lo, hi = (float(np.min(self.vol)), float(np.max(self.vol))) if self.vol.size else (0.0, 0.0)
+            s.grad_range_set = 1
+            s.grad_range[0], s.grad_range[1] = lo, hi
+        s.conf_weight_bits = int(conf_weight_bits)
+        s.conf_flags = int(conf_flags)
         self.s = s
+
+    def conformance(self, weight_bits=0, flags=0):
+        """Switch the conformance-study variant (oracle.h OR_CONF_*); (0, 0) is the oracle."""
+        self.s.conf_weight_bits = int(weight_bits)
+        self.s.conf_flags = int(flags)
+        return self
 
     @classmethod
     def from_params(cls, vol, vmin, vmax, tf, camera, width, height, params, smin=(0, 0, 0),

@@ -197,7 +197,8 @@ def _glib():
     return lib
 
 
-@pytest.mark.parametrize("members,inflight,nframes", [(2, 3, 7), (3, 2, 5), (3, 1, 3), (1, 2, 3)])
+@pytest.mark.parametrize("members,inflight,nframes",
+                         [(2, 3, 7), (3, 2, 5), (3, 1, 3), (1, 2, 3), (8, 3, 6), (8, 1, 3)])
 def test_group_schedule_one_process(members, inflight, nframes):
     """A multi-device context (vr_create_mask) in ONE process: vr_frame_workers.h issues every
     frame on N members -- member 0 on the calling thread, the others on worker threads -- each
@@ -224,6 +225,8 @@ def test_group_schedule_one_process(members, inflight, nframes):
     delays = rng.uniform(0.0, 0.01, size=(members, nframes, 4))
 
     def op_fn(_user, m, op, slot, frame):
+        if op >= 4:  # OP_ABORT / OP_ISSUE hooks: nothing fails here
+            return 0
         t0 = time.monotonic_ns()
         try:
             time.sleep(delays[m, frame, op])
@@ -284,3 +287,67 @@ def test_group_schedule_reports_member_errors():
     assert lib.vr_group_host_synchronize(g) == -5
     lib.vr_group_host_destroy(g)
     assert not lib.vr_group_host_create(0, 2, cb, None)
+
+
+class _Rendezvous:
+    """A collective with real matching, standing in for ncclGather: member m's gather of frame f
+    returns only once every member posted frame f, or fails once the group is aborted (the
+    stand-in for ncclCommAbort ending pending collectives)."""
+
+    def __init__(self, members):
+        self.members = members
+        self.cond = threading.Condition()
+        self.posted = {}
+        self.aborted = False
+        self.abort_calls = []
+
+    def gather(self, m, frame):
+        with self.cond:
+            self.posted.setdefault(frame, set()).add(m)
+            self.cond.notify_all()
+            ok = self.cond.wait_for(
+                lambda: self.aborted or len(self.posted[frame]) == self.members, timeout=60)
+            assert ok, "collective hung (no abort)"
+            return -5 if len(self.posted[frame]) < self.members else 0
+
+    def abort(self, m):
+        with self.cond:
+            self.abort_calls.append(m)
+            self.aborted = True
+            self.cond.notify_all()
+
+
+@pytest.mark.parametrize("members,fail_member,fail_frame", [(3, 2, 1), (8, 5, 2), (8, 0, 1)])
+def test_group_member_issue_failure_aborts_collectives(members, fail_member, fail_frame):
+    """a member whose issue fails never posts its gather, so its peers' gathers of
+    that frame can never match and would block their streams forever.  The frame workers'
+    settle() aborts every communicator (OP_ABORT, ncclCommAbort in vr_dist.cpp) before any
+    stream is synchronised: synchronize returns the member's error in bounded time, and the
+    context refuses further frames."""
+    lib = _glib()
+    rv = _Rendezvous(members)
+
+    def op_fn(_u, m, op, _slot, frame):
+        if op == 5:  # OP_ISSUE: the failing member's enqueue of frame fail_frame fails
+            return -5 if (m == fail_member and frame == fail_frame) else 0
+        if op == 4:
+            rv.abort(m)
+            return 0
+        if op == 1:
+            return rv.gather(m, frame)
+        return 0
+
+    cb = GCB(op_fn)
+    g = lib.vr_group_host_create(members, 2, cb, None)
+    t0 = time.monotonic()
+    rcs = [lib.vr_group_host_frame(g) for _ in range(4)]
+    rc = lib.vr_group_host_synchronize(g)
+    assert time.monotonic() - t0 < 30
+    assert rc == -5
+    assert sorted(rv.abort_calls) == list(range(members))  # every communicator, once
+    if fail_member == 0:  # member 0's issue fails on the caller's thread: reported at once
+        assert rcs[fail_frame] == -5
+    assert lib.vr_group_host_frame(g) != 0  # aborted: no further frames
+    assert lib.vr_group_host_synchronize(g) == -5
+    assert sorted(rv.abort_calls) == list(range(members))  # abort ran once only
+    lib.vr_group_host_destroy(g)

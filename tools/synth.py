@@ -169,6 +169,8 @@ CAMERAS = {
     "fill_oblique": dict(radius=1.6, rotate=(40.0, 25.0)),
     # the diagonal view of the view sweeps (tools/view_sweep.py): rays cross brick rows and slabs
     "diag": dict(radius=2.0, rotate=(180.0, 140.0)),
+    # the near plane (0.198 in glm's [-1, 1] clip form) cuts the cube's front face
+    "near": dict(radius=0.65, rotate=None),
 }
 
 

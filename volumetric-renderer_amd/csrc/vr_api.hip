@@ -78,7 +78,11 @@ struct vr_ctx {
     size_t grad_bytes = 0;
     bool grad_valid = false;
     bool grad_half = false;      // the field's precision (vr_params.exact_gradient == 0: binary16)
-    int grad_scale_log2 = 0;     // and its scale (field_scale_log2 of the volume's min/max)
+    int grad_scale_log2 = 0;     // and its scale (field_scale_log2 of the data's own range)
+    // f32 storage: the stored voxels' min and max, zero border included (measured on the bricks
+    // at upload): the binary16 field's scale comes from these, never from the caller's
+    // vmin/vmax, which may be a display window narrower than the data
+    float data_lo = 0.0f, data_hi = 1.0f;
     // adaptive tile order (tile_order 4): per launch geometry, the last launch's per-tile
     // durations and the workgroup -> tile permutation built from them
     // Keyed by the launch stream too: frames in flight on different streams each own their
@@ -394,6 +398,35 @@ int set_bricks(vr_ctx *c, int storage, uint32_t nx, uint32_t ny, uint32_t nz, vo
     c->bricks = p;
     c->brick_bytes = bytes;
     *out = p;
+    return VR_OK;
+}
+
+// f32 storage: min and max over every stored element of the bricks (z-pairs duplicate voxels,
+// the apron and the border hold zeros), i.e. [min(data, 0), max(data, 0)] -- exactly the
+// bound field_scale_log2 needs for the central differences, zero border included.
+// Synchronous on `s` (uploads are).
+int data_range(vr_ctx *c, hipStream_t s)
+{
+    c->data_lo = 0.0f;
+    c->data_hi = 0.0f;
+    if (c->storage != ST_F32) return VR_OK;
+    uint32_t *mm = reinterpret_cast<uint32_t *>(c->counters);  // scratch: 2 words
+    const uint32_t init[2] = {0xFFFFFFFFu, 0u};
+    HIP_TRY(c, hipMemcpyAsync(mm, init, sizeof init, hipMemcpyHostToDevice, s), "hipMemcpy(range)");
+    HIP_TRY(c, launch_minmax(ST_F32, c->bricks, c->brick_bytes / sizeof(float),
+                             reinterpret_cast<float *>(mm), s),
+            "data range kernel");
+    uint32_t h[2];
+    HIP_TRY(c, hipMemcpyAsync(h, mm, sizeof h, hipMemcpyDeviceToHost, s), "hipMemcpy(range)");
+    HIP_TRY(c, hipStreamSynchronize(s), "data range sync");
+    auto unorder = [](uint32_t o) {
+        const uint32_t u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
+        float f;
+        std::memcpy(&f, &u, 4);
+        return f;
+    };
+    c->data_lo = unorder(h[0]);
+    c->data_hi = unorder(h[1]);
     return VR_OK;
 }
 
@@ -732,7 +765,7 @@ bool ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s, bool half)
 {
     bool built = false;
     if (!use_grad_field(c, half)) return built;
-    const int k = half ? field_scale_log2(c->vmin, c->vmax) : 0;
+    const int k = half ? field_scale_log2(c->data_lo, c->data_hi) : 0;
     if (c->grad_valid && (c->grad_half != half || c->grad_scale_log2 != k)) {
         if (hipDeviceSynchronize() != hipSuccess) {
             (void)hipGetLastError();
@@ -1023,6 +1056,8 @@ int replicate_volume(vr_ctx *c)
             d->nz = src->nz;
             d->vmin = src->vmin;
             d->vmax = src->vmax;
+            d->data_lo = src->data_lo;
+            d->data_hi = src->data_hi;
             d->range_valid = d->dist_valid = d->grad_valid = false;
         }
     }
@@ -1358,7 +1393,7 @@ int vr_set_volume_device(vr_ctx *c, const void *data_dev, int dtype, uint32_t nx
     c->vmin = vmin;  // offscreen_pass.cpp:265-266
     c->vmax = vmax;
     c->range_valid = c->dist_valid = false;
-    return VR_OK;
+    return data_range(c, s);
 }
 
 int vr_set_volume(vr_ctx *c, const void *data, int dtype, uint32_t nx, uint32_t ny, uint32_t nz,
@@ -1484,7 +1519,7 @@ int vr_generate_volume(vr_ctx *c, int kind, int dtype, uint32_t nx, uint32_t ny,
     c->range_valid = c->dist_valid = false;
     if (vmin_out) *vmin_out = c->vmin;
     if (vmax_out) *vmax_out = c->vmax;
-    return VR_OK;
+    return data_range(c, nullptr);
 }
 
 uint64_t vr_volume_bytes(const vr_ctx *c)
@@ -1641,14 +1676,15 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
     vr_ctx::TileSched *ts =
         tile_sched(c, P, stream, tile_kernel_key(P, p->shading != 0, layout));
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (c->timing) {
+    const bool timing = c->timing;  // read once: the pair is recorded and queued together
+    if (timing) {
         e0 = pooled_event(c);
         e1 = pooled_event(c);
         if (!e0 || !e1) return fail(c, VR_EIO, "hipEventCreate failed");
         HIP_TRY(c, hipEventRecord(e0, s), "hipEventRecord");
     }
     HIP_TRY(c, launch_march(layout, p->shading != 0, false, P, s), "march kernel launch");
-    if (c->timing) {
+    if (timing) {
         HIP_TRY(c, hipEventRecord(e1, s), "hipEventRecord");
         c->ev_pending.emplace_back(e0, e1);
     }
@@ -1859,6 +1895,9 @@ int vr_count_work(vr_ctx *c, const vr_camera *cam, const vr_params *p, uint32_t 
 int vr_timing_enable(vr_ctx *c, int enable)
 {
     if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    // the members' frame workers may be inside vr_render_device: drain them first
+    if (is_group(c))
+        if (int rc = group_idle(c)) return rc;
     for (vr_ctx *m : c->members) vr_timing_enable(m, enable);
     c->timing = enable != 0;
     return VR_OK;
@@ -1946,6 +1985,8 @@ int vr_debug_set_knob(vr_ctx *c, int knob, int value)
     int *k = knob_slot(c, knob);
     if (!k) return fail(c, VR_EINVAL, "unknown knob");
     if (!knob_value_ok(knob, value)) return fail(c, VR_EINVAL, "knob value out of range");
+    if (is_group(c))  // no member may be inside a frame while its knobs change
+        if (int rc = group_idle(c)) return rc;
     *k = value;
     for (vr_ctx *m : c->members) vr_debug_set_knob(m, knob, value);
     return VR_OK;

@@ -43,6 +43,7 @@ struct Rccl {
     ncclResult_t (*gather)(const void *, void *, size_t, ncclDataType_t, int, ncclComm_t,
                            hipStream_t) = nullptr;
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
     const char *(*error_string)(ncclResult_t) = nullptr;
 };
 
@@ -68,8 +69,9 @@ Rccl load_rccl()
         !bind(h, "ncclCommInitRank", r.comm_init_rank) || !bind(h, "ncclGather", r.gather) ||
         !bind(h, "ncclCommInitAll", r.comm_init_all) ||
         !bind(h, "ncclCommDestroy", r.comm_destroy) ||
+        !bind(h, "ncclCommAbort", r.comm_abort) ||
         !bind(h, "ncclGetErrorString", r.error_string)) {
-        r.err = "librccl.so.1 lacks ncclGather/ncclCommInitRank/ncclCommInitAll/...";
+        r.err = "librccl.so.1 lacks ncclGather/ncclCommInitRank/ncclCommInitAll/ncclCommAbort/...";
         return r;
     }
     r.ok = true;
@@ -585,29 +587,46 @@ Group *group_create(const std::vector<vr_ctx *> &members, std::string *err)
     return g.release();
 }
 
+// A member failed: its peers' gathers of the failed frame (and of every later frame the workers
+// had queued) can never be matched.  Abort every communicator so those collectives end instead
+// of holding the streams forever (FrameWorkers::settle calls this once, after the enqueues
+// drained, before any stream is synchronised).  The context is unusable afterwards.
+void abort_comms(Group *g)
+{
+    for (size_t m = 0; m < g->comms.size(); ++m)
+        if (g->comms[m]) {
+            hipSetDevice(g->devices[m]);
+            rccl().comm_abort(g->comms[m]);
+            g->comms[m] = nullptr;
+        }
+    if (!g->devices.empty()) hipSetDevice(g->devices[0]);
+}
+
 int group_drain(Group *g, std::string *err)
 {
     if (!g->workers) return VR_OK;
-    return g->workers->drain(err) == 0 ? VR_OK : VR_EIO;
+    return g->workers->settle([g] { abort_comms(g); }, err) == 0 ? VR_OK : VR_EIO;
 }
 
 int group_synchronize(Group *g, std::string *err)
 {
-    if (int rc = group_drain(g, err)) return rc;
+    // a member's failure aborts the communicators here, before the waits below
+    const int failed = group_drain(g, err);
+    std::string sync_err;
     for (vr_dist *d : g->dists)
-        if (vr_dist_synchronize(d) != VR_OK) {
-            *err = d->err;
-            return VR_EIO;
-        }
+        if (vr_dist_synchronize(d) != VR_OK && sync_err.empty()) sync_err = d->err;
     for (size_t m = 1; m < g->own.size(); ++m)
         if (g->own[m]) {
             hipSetDevice(g->devices[m]);
-            if (hipStreamSynchronize(g->own[m]) != hipSuccess) {
-                *err = "hipStreamSynchronize";
-                return VR_EIO;
-            }
+            if (hipStreamSynchronize(g->own[m]) != hipSuccess && sync_err.empty())
+                sync_err = "hipStreamSynchronize";
         }
     hipSetDevice(g->devices[0]);
+    if (failed) return failed;
+    if (!sync_err.empty()) {
+        *err = sync_err;
+        return VR_EIO;
+    }
     return VR_OK;
 }
 
@@ -641,7 +660,13 @@ int group_render(Group *g, const vr_camera *cam, const vr_params *p, void *out_d
     j.p = *p;
     j.out = out_dev;
     j.stream = stream;
-    const int rc = g->workers->issue(j, err);
+    int rc = g->workers->issue(j, err);
+    if (rc != 0 && !g->workers->aborted()) {
+        // member 0 or a worker failed: end the unmatched collectives now, so the
+        // caller's stream and vr_destroy cannot wait on them forever
+        std::string m;
+        g->workers->settle([g] { abort_comms(g); }, &m);
+    }
     return rc == 0 ? VR_OK : (rc < 0 ? rc : VR_EIO);
 }
 

@@ -16,6 +16,13 @@
 // Errors are sticky per worker: the first failing issue is reported by the next issue() or
 // drain(), with its message, and the worker skips its later jobs (the frame stream on that
 // member is broken; the context must be destroyed).
+//
+// A failed member breaks the collective: its peers have already issued (or will issue) their
+// gathers of that frame, which can never be matched, so their streams would wait forever.
+// settle(abort) is the one place that resolves this for both executors: it drains the
+// enqueues, and if any member (member 0 included) failed it calls abort() once -- the HIP
+// executor aborts every communicator (ncclCommAbort), which ends the pending collectives --
+// before the caller synchronises any stream.  After that every issue() fails.
 #pragma once
 
 #include <atomic>
@@ -71,6 +78,11 @@ class FrameWorkers {
     // here.  A failure already recorded on a worker is returned first.
     int issue(const Job &job, std::string *msg)
     {
+        if (aborted_) {
+            if (msg) *msg = "a device member failed and the frame collectives were aborted: "
+                            "destroy the context (" + first_msg_ + ")";
+            return first_rc_ ? first_rc_ : -5;
+        }
         if (int rc = sticky(msg)) return rc;
         for (auto &w : workers_) {
             {
@@ -79,8 +91,40 @@ class FrameWorkers {
             }
             w->cv.notify_one();
         }
-        return issue_(0, job, msg);
+        const int rc = issue_(0, job, msg);
+        if (rc && !failed0_) {
+            failed0_ = rc;
+            failed0_msg_ = "device member 0: " + (msg ? *msg : std::string());
+        }
+        return rc;
     }
+
+    // Drains the enqueues; if any member failed (now or before), calls abort() once and
+    // returns that member's error (message in *msg), else 0.  Call before synchronising the
+    // members' streams.
+    int settle(const std::function<void()> &abort, std::string *msg)
+    {
+        std::string m;
+        int rc = drain(&m);
+        if (!rc && failed0_) {
+            rc = failed0_;
+            m = failed0_msg_;
+        }
+        if (!rc && aborted_) {
+            rc = first_rc_;
+            m = first_msg_;
+        }
+        if (rc && !aborted_) {
+            aborted_ = true;
+            first_rc_ = rc;
+            first_msg_ = m;
+            if (abort) abort();
+        }
+        if (rc && msg) *msg = m;
+        return rc;
+    }
+
+    bool aborted() const { return aborted_; }
 
     // Waits until every member has issued every frame posted so far; the first worker error.
     int drain(std::string *msg)
@@ -140,6 +184,11 @@ class FrameWorkers {
 
     IssueFn issue_;
     std::vector<std::unique_ptr<Worker>> workers_;
+    // member 0's failure (it runs on the caller's thread) and the abort state; touched only
+    // by the caller's thread (issue / settle)
+    int failed0_ = 0, first_rc_ = 0;
+    bool aborted_ = false;
+    std::string failed0_msg_, first_msg_;
 };
 
 }  // namespace sched

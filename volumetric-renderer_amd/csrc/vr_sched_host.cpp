@@ -96,7 +96,7 @@ struct HostStream {
 };
 
 typedef int (*vr_sched_op_fn)(void *user, int op, int slot, uint64_t frame);
-enum { OP_RENDER = 0, OP_GATHER = 1, OP_ASSEMBLE = 2, OP_CONSUME = 3 };
+enum { OP_RENDER = 0, OP_GATHER = 1, OP_ASSEMBLE = 2, OP_CONSUME = 3, OP_ABORT = 4, OP_ISSUE = 5 };
 
 struct HostExec {
     using Stream = HostStream *;
@@ -256,12 +256,20 @@ static int group_member_op(void *user, int op, int slot, uint64_t frame)
     return t->g->fn(t->g->user, t->member, op, slot, frame);
 }
 
+// Stand-in for ncclCommAbort on every member's communicator.
+static void group_abort(vr_group_host *g)
+{
+    for (int m = 0; m < (int)g->members.size(); ++m) g->fn(g->user, m, OP_ABORT, -1, 0);
+}
+
 // One frame on member m (rank m of the members): the schedule, plus (member 0) the caller's
-// consume of the assembled frame.
+// consume of the assembled frame.  fn(OP_ISSUE) first, synchronously on the issuing thread:
+// non-zero fails this member's issue (as a vr_dist_render enqueue error would).
 static int group_member_frame(vr_group_host *g, int m)
 {
     vr_sched_host *h = g->members[m];
     const uint64_t frame = h->sched.frame;
+    if (int rc = g->fn(g->user, m, OP_ISSUE, -1, frame)) return rc;
     int rc = h->sched.issue(h->x, h->caller, nullptr);
     if (rc || m != 0) return rc;
     return h->x.call(h->caller, OP_CONSUME, (int)(frame % h->sched.slots.size()), frame);
@@ -295,15 +303,23 @@ int vr_group_host_frame(vr_group_host *g)
 {
     if (!g) return -22;
     std::string msg;
-    return g->workers->issue(0, &msg);
+    const int rc = g->workers->issue(0, &msg);
+    if (rc && !g->workers->aborted()) {  // as vr_dist.cpp group_render: end the collectives now
+        std::string m;
+        g->workers->settle([g] { group_abort(g); }, &m);
+    }
+    return rc;
 }
 
 // Waits until every member has issued and run every op so far; the first failure, else 0.
+// A member whose issue failed aborts the group first (FrameWorkers::settle, as vr_dist.cpp's
+// group_synchronize): fn(user, m, OP_ABORT, -1, 0) for every member -- ncclCommAbort on each
+// communicator there -- so peers blocked in that frame's collective return instead of hanging.
 int vr_group_host_synchronize(vr_group_host *g)
 {
     if (!g) return -22;
     std::string msg;
-    int rc = g->workers->drain(&msg);
+    int rc = g->workers->settle([g] { group_abort(g); }, &msg);
     for (auto *m : g->members) {
         const int r = m->sync();
         if (r && !rc) rc = r;
