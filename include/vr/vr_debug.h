@@ -8,7 +8,7 @@
  * vr_params.exact_gradient is 0 (the field then holds binary16 differences, the stencil exact
  * ones); the GPU tests use them to render each variant and compare.  The library never reads the process environment, except in
  * experiment builds (`make EXTRA=-DVR_EXPERIMENTS`), where vr_create() seeds the knobs from
- * VR_PIPELINE, VR_PAIR, VR_PAIR_LANES, VR_NO_GRAD_FIELD / VR_GRAD_FIELD_ALWAYS, VR_LDS,
+ * VR_PIPELINE, VR_PAIR, VR_PAIR_LANES, VR_NO_GRAD_FIELD / VR_GRAD_FIELD_ALWAYS,
  * VR_U8_LAYOUT and VR_TILE_ORDER_DEFAULT (the names the round-1/2 A/B scripts under tools/
  * set).
  */
@@ -27,8 +27,7 @@ enum vr_knob {
     VR_KNOB_PAIR_LANES = 3, /* 0 auto, 2 or 4 lanes per ray                                 */
     VR_KNOB_GRAD_FIELD = 4, /* -1 auto (dense-row views), 0 stencil gradient, 1 the f32
                                difference field on every view                               */
-    VR_KNOB_LDS = 5,        /* 0 (default) off; 1 keep a linear copy at the next volume
-                               upload and launch the LDS-staged march (march_lds_kernel)   */
+    /* 5: retired (the LDS-staged march, measured 1.6-2.7x slower: tools/experiments/r04_pruned/) */
     VR_KNOB_U8_LAYOUT = 6,  /* -1 auto, 0 plain 7x8x8 bricks, 1 yz-quads (next upload)      */
     VR_KNOB_TILE_ORDER = 7, /* tile order used when vr_params.tile_order == 0: 0 auto (4),
                                1..4 as vr_params.tile_order                                */
@@ -38,9 +37,9 @@ enum vr_knob {
     VR_KNOB_ALT_GEOMETRY = 9 /* f32 volumes: -1 auto (oblique views read a 7x15x8-cell-brick
                                copy; sparse views the stencil copy when shaded, a plain
                                one-voxel-per-element 15^3 one when not), 0 never, 1 the
-                               oblique copy, 2 the z-pair sparse copy, 3 the plain copy,
-                               4 the stencil copy (29^3-cell plain bricks with a 1-below /
-                               2-above apron), whenever the launch allows it               */
+                               oblique copy, 3 the plain copy, 4 the stencil copy (29^3-cell
+                               plain bricks with a 1-below / 2-above apron), whenever the
+                               launch allows it (2, the retired z-pair sparse copy: EINVAL) */
 };
 
 /* Set / read one knob of `ctx` (a multi-device context sets it on every device).

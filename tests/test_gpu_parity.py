@@ -584,43 +584,6 @@ def test_kernel_variants_bit_identical(rp, shading):
     check(imgs[0], ref)
 
 
-@pytest.mark.parametrize("np_dtype", [np.float32, np.uint8, np.int16])
-def test_lds_staged_kernel_bit_identical(rp, np_dtype):
-    """The opt-in LDS-staged march (knob lds = 1 at upload and render: per-stage voxel boxes
-    DMA'd into LDS from a zero-padded linear copy) renders the bricked gather's bytes, shaded
-    and unshaded; without the knob no linear copy is kept."""
-    W, H = 88, 70
-    rp.framebuffer_size_changed(W, H)
-    vol = synth.gaussians_numpy((37, 30, 43), seed=23)
-    if np_dtype != np.float32:
-        info = np.iinfo(np_dtype)
-        vol = np.clip(np.rint(vol / vol.max() * info.max), info.min, info.max).astype(np_dtype)
-    else:
-        vol = vol.astype(np.float32)
-    tf = synth.tf_band(0.1, 0.9)
-    base_bytes = None
-    for lds in (0, 1):
-        rp.set_knob("lds", lds)
-        rp.volume_dataset_changed(synth.dataset(vol))
-        rp.transfer_function_changed(tf)
-        imgs = []
-        for shading in (0, 1):
-            for camname in ("rotA", "fill_oblique"):
-                cam = synth.camera(camname).to_vr_camera()
-                imgs.append(rp.render(cam, vr_amd.default_params(shading=shading, ert_eps=1e-4,
-                                                                 exact_gradient=1),
-                                      vr_amd.OUT_RGBA32F))
-        if base_bytes is None:
-            base_bytes = imgs
-            assert "lds" not in rp.kernel_name(vr_amd.default_params()), "no linear copy without the knob"
-        else:
-            assert "lds" in rp.kernel_name(vr_amd.default_params())
-            for a, b in zip(base_bytes, imgs):
-                assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), np_dtype
-    rp.set_knob("lds", 0)
-    rp.volume_dataset_changed(synth.dataset(vol))  # later tests: no linear copy
-
-
 def test_frames_in_flight_on_streams_are_identical(rp):
     """Frames rendered back to back on 3 streams (frames_in_flight = 3, own output buffer per
     stream, adaptive tile order per stream) equal the serial frame byte for byte.  Right
@@ -741,8 +704,8 @@ def test_non_integer_uploads_stay_f32(rp):
 
 def test_alt_geometry_copy_bit_identical(rp):
     """f32 volumes keep further copies in alternative brick geometries that oblique views
-    (7x15x8 cells, kernel tag F32Alt) and sparse views (15x15x8, F32Wide; or plain one-voxel
-    elements, F32P; or plain with the gradient's apron, F32S) read (vr_api.hip want_alt): the frames are byte-identical to the 8^3
+    (7x15x8 cells, kernel tag F32Alt) and sparse views (plain one-voxel elements, F32P; or
+    plain with the gradient's apron, F32S) read (vr_api.hip want_alt): the frames are byte-identical to the 8^3
     bricks' -- unshaded and shaded (stencil gradient across every geometry's brick
     boundaries), single stage and pipelined -- the
     launch policy picks the oblique copy for the diagonal view, a sparse one for the
@@ -766,7 +729,7 @@ def test_alt_geometry_copy_bit_identical(rp):
                     p = vr_amd.default_params(shading=shading, ert_eps=1e-5)
                     with rp.knobs(pipeline=pipe, grad_field=0, alt_geometry=0):
                         a = rp.render(c, p, vr_amd.OUT_RGBA32F)
-                    for alt, tag in ((1, "F32Alt"), (2, "F32Wide"), (3, "F32P"), (4, "F32S")):
+                    for alt, tag in ((1, "F32Alt"), (3, "F32P"), (4, "F32S")):
                         with rp.knobs(pipeline=pipe, grad_field=0, alt_geometry=alt):
                             b = rp.render(c, p, vr_amd.OUT_RGBA32F)
                             assert tag in rp.kernel_name(p)
@@ -776,7 +739,7 @@ def test_alt_geometry_copy_bit_identical(rp):
                 p = vr_amd.default_params(shading=shading, exact_gradient=1)
                 rp.render(c, p)
                 name = rp.kernel_name(p)
-                picked = next((t for t in ("F32Alt", "F32Wide", "F32P", "F32S") if t in name), None)
+                picked = next((t for t in ("F32Alt", "F32P", "F32S") if t in name), None)
                 w = want[camname]
                 if w == "F32S" and not shading:
                     w = "F32P"  # sparse and unshaded: the plain copy

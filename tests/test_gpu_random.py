@@ -103,9 +103,8 @@ def test_random_scene_matches_oracle(rp, seed):
 
 
 def test_random_sweep_covered_the_layouts():
-    """Runs after the sweep: the scenes reached every f32 brick copy the launch policy picks (the
-    z-pair sparse copy F32Wide is knob-only: test_alt_geometry_copy_bit_identical), the binary16
-    field and the
+    """Runs after the sweep: the scenes reached every f32 brick copy the launch policy picks, the
+    binary16 field and the
     8-bit yz-quads (plain 8-bit bricks start at 2^25 voxels, past the oracle's budget here:
     test_byte_layouts_plain_and_quad_identical renders them)."""
     names = "\n".join(f"{k}: {len(v)}" for k, v in sorted(KERNELS.items()))

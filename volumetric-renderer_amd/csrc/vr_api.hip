@@ -41,9 +41,6 @@ struct vr_ctx {
     // volume (bricked, native storage type)
     void *bricks = nullptr;
     size_t brick_bytes = 0;
-    // the same voxels zero-padded and linear (march_lds_kernel's LDS staging source)
-    void *lin = nullptr;
-    size_t lin_bytes = 0;
     int storage = ST_F32;
     int layout = ST_F32;  // brick layout code (storage | kQuadFlag for 8-bit yz-quads)
     // the last frame's view (view_dense_rows): image x along the bricks' rows, dense sampling
@@ -51,13 +48,13 @@ struct vr_ctx {
     double pixel_span = 0.0;  // voxels per pixel step at the volume centre (view_dense_rows)
     double axis_align = 1.0;  // largest |component| of the centre ray's unit direction
     // f32 volumes: further resident copies in the alternative geometries (kAltFlag for
-    // oblique views, kWideFlag for sparse ones), each built lazily on the first frame that wants
-    // it after a volume change
+    // oblique views, the plain and stencil copies for sparse ones), each built lazily on the
+    // first frame that wants it after a volume change
     struct AltCopy {
         void *bricks = nullptr;
         size_t bytes = 0;
         bool valid = false, failed = false;
-    } alt[4];
+    } alt[3];
     uint32_t nx = 1, ny = 1, nz = 1;
     float vmin = 0.0f, vmax = 1.0f;
     // transfer function (decoded, linear float RGBA)
@@ -123,7 +120,7 @@ struct vr_ctx {
     // launch-policy overrides for tests and A/B experiments (include/vr/vr_debug.h); the
     // product path never reads the process environment
     struct Knobs {
-        int pipeline = -1, pair = -1, pair_lanes = 0, grad_field = -1, lds = 0, u8_layout = -1,
+        int pipeline = -1, pair = -1, pair_lanes = 0, grad_field = -1, u8_layout = -1,
             tile_order = 0, narrow = 1, alt = -1;
     } knobs;
     // multi-device context (vr_create_mask): one member context per device of the mask, the
@@ -430,39 +427,6 @@ int data_range(vr_ctx *c, hipStream_t s)
     return VR_OK;
 }
 
-// The zero-padded linear copy (MarchParams::lin) of a linear device source, on `s`.
-int set_lin(vr_ctx *c, int storage, int src_dtype, const void *src, uint32_t nx, uint32_t ny,
-            uint32_t nz, hipStream_t s)
-{
-    // only for the opt-in LDS-staged kernel (knob VR_KNOB_LDS = 1 at upload): it measured slower
-    // than the bricked gather (profiles/r02/lds_staging), and the copy costs memory and an
-    // upload pass
-    if (c->knobs.lds != 1) {
-        if (c->lin) hipFree(c->lin);
-        c->lin = nullptr;
-        c->lin_bytes = 0;
-        return VR_OK;
-    }
-    const size_t bytes = lin_elems(nx, ny, nz) * storage_size(storage);
-    if (!c->lin || c->lin_bytes != bytes) {
-        if (c->lin) hipFree(c->lin);
-        c->lin = nullptr;
-        c->lin_bytes = 0;
-        HIP_TRY(c, hipMalloc(&c->lin, bytes), "hipMalloc(linear volume)");
-        c->lin_bytes = bytes;
-    }
-    HIP_TRY(c, launch_pad_from_linear(src_dtype, src, c->lin, nx, ny, nz, storage, s), "pad kernel");
-    return VR_OK;
-}
-
-// LDS-staged march (march_lds_kernel): only with knob VR_KNOB_LDS = 1; needs the linear copy,
-// the TF in LDS and no empty-space skipping (that variant keeps the bricked kernels).
-bool use_lds(const vr_ctx *c, const vr_params *p)
-{
-    if (!c->lin || p->skip_empty || c->tf_n > 256) return false;
-    return c->knobs.lds == 1;
-}
-
 int upload_tf(vr_ctx *c, const uint32_t *tf, uint32_t n)
 {
     // entry i + 1 = texel i as {c_i, c_(i+1) - c_i} (0 for the last), entries 0 and n + 1 the
@@ -700,11 +664,6 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     c->dense_rows = view_dense_rows(P.inv, c->width, c->nx, c->ny, c->nz, &c->pixel_span,
                                     &c->axis_align);
     P.pipelined = use_pipeline(p->shading != 0, P.tiles_x * P.tiles_y, c);
-    P.lin = c->lin;
-    P.lpx = lin_pitch_x(c->nx);
-    P.lpy = c->ny + 2 * kPad;
-    P.lpz = c->nz + 2 * kPad;
-    P.lds = use_lds(c, p) ? 1 : 0;
     return VR_OK;
 }
 
@@ -849,7 +808,7 @@ int ensure_derived(vr_ctx *c, const vr_params *p, MarchParams &P, hipStream_t s)
 // (profiles/r03/stencil2/ .. stencil4/); on the diagonal it loses to the oblique copy.
 int want_alt(const vr_ctx *c, const vr_params *p, const MarchParams &P)
 {
-    if (c->layout != ST_F32 || p->skip_empty || P.lds || P.pair || P.grad) return c->layout;
+    if (c->layout != ST_F32 || p->skip_empty || P.pair || P.grad) return c->layout;
     int which = 0;
     if (c->knobs.alt >= 0)
         which = c->knobs.alt;
@@ -857,7 +816,6 @@ int want_alt(const vr_ctx *c, const vr_params *p, const MarchParams &P)
         which = c->axis_align < kAltAlign ? 1 : (c->pixel_span > kAltSpan ? (p->shading ? 4 : 3) : 0);
     switch (which) {
         case 1: return ST_F32 | kAltFlag;
-        case 2: return ST_F32 | kWideFlag;
         case 3: return ST_F32 | kPlainF32Flag;
         case 4: return ST_F32 | kStencilF32Flag;
         default: return c->layout;
@@ -867,8 +825,7 @@ int want_alt(const vr_ctx *c, const vr_params *p, const MarchParams &P)
 int alt_index(int layout)
 {
     if (layout & kAltFlag) return 0;
-    if (layout & kWideFlag) return 1;
-    return (layout & kPlainF32Flag) ? 2 : 3;
+    return (layout & kPlainF32Flag) ? 1 : 2;
 }
 
 // Bytes of the copy of the current volume in layout `lay`.
@@ -1033,20 +990,6 @@ int replicate_volume(vr_ctx *c)
         hipError_t e = hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking);
         if (e == hipSuccess)
             e = hipMemcpyPeerAsync(dst, d->device, src->bricks, src->device, src->brick_bytes, st[k]);
-        if (e == hipSuccess && src->lin) {  // the LDS-staged kernel's linear copy (knob lds)
-            if (d->lin && d->lin_bytes != src->lin_bytes) {
-                hipFree(d->lin);
-                d->lin = nullptr;
-            }
-            if (!d->lin) e = hipMalloc(&d->lin, src->lin_bytes);
-            d->lin_bytes = src->lin_bytes;
-            if (e == hipSuccess)
-                e = hipMemcpyPeerAsync(d->lin, d->device, src->lin, src->device, src->lin_bytes, st[k]);
-        } else if (e == hipSuccess && d->lin) {
-            hipFree(d->lin);
-            d->lin = nullptr;
-            d->lin_bytes = 0;
-        }
         if (e != hipSuccess) rc = hip_fail(c, e, "replicate volume (peer copy)");
         if (rc == VR_OK) {
             d->storage = src->storage;
@@ -1087,7 +1030,6 @@ int *knob_slot(vr_ctx *c, int knob)
         case VR_KNOB_PAIR: return &c->knobs.pair;
         case VR_KNOB_PAIR_LANES: return &c->knobs.pair_lanes;
         case VR_KNOB_GRAD_FIELD: return &c->knobs.grad_field;
-        case VR_KNOB_LDS: return &c->knobs.lds;
         case VR_KNOB_U8_LAYOUT: return &c->knobs.u8_layout;
         case VR_KNOB_TILE_ORDER: return &c->knobs.tile_order;
         case VR_KNOB_NARROW: return &c->knobs.narrow;
@@ -1100,9 +1042,8 @@ bool knob_value_ok(int knob, int v)
 {
     switch (knob) {
         case VR_KNOB_PAIR_LANES: return v == 0 || v == 2 || v == 4;
-        case VR_KNOB_LDS:
         case VR_KNOB_NARROW: return v == 0 || v == 1;
-        case VR_KNOB_ALT_GEOMETRY: return v >= -1 && v <= 4;
+        case VR_KNOB_ALT_GEOMETRY: return v >= -1 && v <= 4 && v != 2;
         case VR_KNOB_TILE_ORDER: return v >= 0 && v <= 4;
         default: return v >= -1 && v <= 1;
     }
@@ -1117,7 +1058,6 @@ void knobs_from_env(vr_ctx *c)
     };
     flag("VR_PIPELINE", c->knobs.pipeline);
     flag("VR_PAIR", c->knobs.pair);
-    flag("VR_LDS", c->knobs.lds);
     if (const char *e = std::getenv("VR_PAIR_LANES")) c->knobs.pair_lanes = e[0] == '4' ? 4 : 2;
     if (std::getenv("VR_NO_GRAD_FIELD")) c->knobs.grad_field = 0;
     if (std::getenv("VR_GRAD_FIELD_ALWAYS")) c->knobs.grad_field = 1;
@@ -1295,7 +1235,6 @@ void vr_destroy(vr_ctx *c)
     for (auto e : c->ev_pool) hipEventDestroy(e);
     if (c->built_ev) hipEventDestroy(c->built_ev);
     if (c->bricks) hipFree(c->bricks);
-    if (c->lin) hipFree(c->lin);
     if (c->tf) hipFree(c->tf);
     if (c->tf_nz) hipFree(c->tf_nz);
     if (c->brick_range) hipFree(c->brick_range);
@@ -1382,8 +1321,6 @@ int vr_set_volume_device(vr_ctx *c, const void *data_dev, int dtype, uint32_t nx
     rc = set_bricks(c, lay, nx, ny, nz, &dst);
     if (rc) return rc;
     HIP_TRY(c, launch_brick_from_linear(dtype, data_dev, dst, nx, ny, nz, lay, s), "brick kernel");
-    rc = set_lin(c, st, dtype, data_dev, nx, ny, nz, s);
-    if (rc) return rc;
     HIP_TRY(c, hipStreamSynchronize(s), "brick kernel sync");
     c->storage = st;
     c->layout = lay;
@@ -1497,7 +1434,6 @@ int vr_generate_volume(vr_ctx *c, int kind, int dtype, uint32_t nx, uint32_t ny,
     if (rc == VR_OK) {
         e = launch_brick_from_linear(src_dtype, lin, dst, nx, ny, nz, lay, nullptr);
         if (e != hipSuccess) rc = hip_fail(c, e, "brick generated volume");
-        if (rc == VR_OK) rc = set_lin(c, st, src_dtype, lin, nx, ny, nz, nullptr);
         if (rc == VR_OK && (e = hipDeviceSynchronize()) != hipSuccess)
             rc = hip_fail(c, e, "brick generated volume");
     }
@@ -1652,7 +1588,7 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
     hipStream_t s = static_cast<hipStream_t>(stream);
     rc = ensure_derived(c, p, P, s);
     if (rc) return rc;
-    if (!P.lds && use_pair(c, P, p)) {  // L lanes per ray on 16 x (16 / L) tiles (march_pair_kernel)
+    if (use_pair(c, P, p)) {  // L lanes per ray on 16 x (16 / L) tiles (march_pair_kernel)
         // 4 lanes below kPairQuadMaxWaves (N = 8 C3 share: 0.151 -> 0.144 ms), else 2
         P.pair = P.tiles_x * P.tiles_y * (kThreadsPerTile / 64) < kPairQuadMaxWaves ? 4 : 2;
         if (c->knobs.pair_lanes == 2 || c->knobs.pair_lanes == 4) P.pair = c->knobs.pair_lanes;
@@ -1966,7 +1902,6 @@ const char *vr_kernel_name(const vr_ctx *c, const vr_params *p)
     const uint32_t tiles = ((c->width + 15) / 16) * ((c->height + kMarchRows - 1) / kMarchRows);
     const bool pipe = use_pipeline(p && p->shading, tiles, c) &&
                       !(p && p->skip_empty) && c->tf_n <= 256;
-    if (p && use_lds(c, p)) return march_lds_kernel_name(c->storage, p->shading != 0);
     int layout = c->layout;
     if (p && !gf) {  // want_alt for the full frame of the last view, once its copy exists
         MarchParams P;

@@ -146,29 +146,21 @@ template <typename T>
 struct Quad8 {
     T v;
 };
-// Alternative f32 geometries: further resident copies of an f32 volume in bricks whose z-pair
+// Alternative f32 geometry: a further resident copy of an f32 volume in bricks whose z-pair
 // rows never straddle a 128-B line, for the views where a wavefront's lanes sit on different
 // brick rows and every straddled line is another L1 miss:
 //   kAltFlag  (F32Alt):  7 x 15 x 8 cells (8-element, 64-B rows; 8704-B bricks, 68 lines), for
-//                        oblique views (diagonal: 0.81 -> 0.68 ms per C3 frame);
-//   kWideFlag (F32Wide): 15 x 15 x 8 cells (16-element, 128-B rows; 18432-B bricks), for sparse
-//                        axis-aligned views (the reference's default camera: 0.34 -> 0.28 ms).
-// The frame-filling, side and top views stay in 8^3 bricks (2-4% faster there).
+//                        oblique views (diagonal: 0.81 -> 0.68 ms per C3 frame).
+// The frame-filling, side and top views stay in 8^3 bricks (2-4% faster there).  (A 15 x 15 x 8
+// z-pair copy for sparse views, superseded by the plain and stencil copies below, is kept as a
+// patch: tools/experiments/r04_pruned/.)
 constexpr int kAltFlag = 0x20;
-constexpr int kWideFlag = 0x40;
 #ifndef VR_ALT_BRICK_CELLS
 #define VR_ALT_BRICK_CELLS 7, 15, 8
 #endif
-#ifndef VR_WIDE_BRICK_CELLS
-#define VR_WIDE_BRICK_CELLS 15, 15, 8
-#endif
 using GeomAlt = BrickGeom<VR_ALT_BRICK_CELLS>;
-using GeomWideRows = BrickGeom<VR_WIDE_BRICK_CELLS>;
-// kernel-side tag types of f32 voxels in the kAltFlag / kWideFlag layouts
+// kernel-side tag type of f32 voxels in the kAltFlag layout
 struct F32Alt {
-    float v;
-};
-struct F32Wide {
     float v;
 };
 // A plain f32 copy (kPlainF32Flag, kernel tag F32P): one voxel per 4-B element, no z-pair
@@ -233,7 +225,6 @@ inline size_t element_size(int st) { return storage_size(st) * voxels_per_elemen
 inline int brick_cells(int st, int a)
 {
     if (st & kAltFlag) return GeomAlt::cells(a);
-    if (st & kWideFlag) return GeomWideRows::cells(a);
     if (st & kPlainF32Flag) return GeomPlainRows::cells(a);
     if (st & kStencilF32Flag) return GeomStencil::cells(a);
     return byte_storage(st) ? GeomByte::cells(a) : GeomWide::cells(a);
@@ -241,7 +232,6 @@ inline int brick_cells(int st, int a)
 inline size_t brick_elems(int st)
 {
     if (st & kAltFlag) return GeomAlt::Elems;
-    if (st & kWideFlag) return GeomWideRows::Elems;
     if (st & kPlainF32Flag) return GeomPlainRows::Elems;
     if (st & kStencilF32Flag) return GeomStencil::Elems;
     return byte_storage(st) ? GeomByte::Elems : GeomWide::Elems;
@@ -309,26 +299,12 @@ struct MarchParams {
     // 2^k (field_scale_log2; the shading normalises the gradient, so the scale cancels)
     int32_t grad_half;
     float inv_range;        // RN(1 / range) (div_fast)
-    // LDS-staged march (march_lds_kernel): the volume as a LINEAR x-fastest array of the
-    // storage type with kPad zero voxels on every side (padded index = logical + 2), row pitch
-    // lpx (a multiple of 4 voxels, so LDS-DMA chunks are aligned), lpy rows per slice
-    const void *lin;
-    uint32_t lpx, lpy, lpz;
-    int32_t lds;            // launch march_lds_kernel
 };
-
-// Padded linear layout of MarchParams::lin for an nx x ny x nz volume.
-inline uint32_t lin_pitch_x(uint32_t nx) { return (nx + 2 * kPad + 3) / 4 * 4; }
-inline size_t lin_elems(uint32_t nx, uint32_t ny, uint32_t nz)
-{
-    return (size_t)lin_pitch_x(nx) * (ny + 2 * kPad) * (nz + 2 * kPad);
-}
 
 // Launchers (vr_kernels.hip).  All asynchronous on `stream`.
 hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &p,
                         hipStream_t stream);
 const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bool gf, bool pipe);
-const char *march_lds_kernel_name(int storage, bool shade);
 // Wavefront count below which a launch uses the pipelined kernel (see build_params).
 constexpr uint32_t kPipelineMaxWaves = 24576;  // between N = 2 (16 K) and N = 1 (33 K) at 1080p
 constexpr size_t kPipelineMinBytes = 4ull << 30;  // large volumes: always pipelined
@@ -371,9 +347,6 @@ constexpr uint32_t kPairMaxWaves = 24576;
 constexpr uint32_t kPairQuadMaxWaves = 6144;  // below: 4 lanes per ray
 hipError_t launch_brick_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,
                                     uint32_t ny, uint32_t nz, int storage, hipStream_t stream);
-// Linear source (any NRRD element type) -> the zero-padded linear layout of MarchParams::lin.
-hipError_t launch_pad_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,
-                                  uint32_t ny, uint32_t nz, int storage, hipStream_t stream);
 // Bricked volume -> linear x-fastest voxels of the storage type, slices [z0, z0 + cz).
 hipError_t launch_unbrick(int storage, const void *bricks, void *dst, uint32_t nx, uint32_t ny,
                           uint32_t z0, uint32_t cz, hipStream_t stream);

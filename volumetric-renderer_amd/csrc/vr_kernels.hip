@@ -78,10 +78,6 @@ struct VoxOf<F32Alt> {
     using type = float;
 };
 template <>
-struct VoxOf<F32Wide> {
-    using type = float;
-};
-template <>
 struct VoxOf<F32H> {
     using type = float;
 };
@@ -128,9 +124,8 @@ constexpr int kElemBytes = kZPair<VT> ? (kPlainF32<VT> ? 4 : 8)
 template <typename VT>
 using GeomOf = std::conditional_t<kPlainByte<VT>, GeomByte,
                                   std::conditional_t<std::is_same<VT, F32Alt>::value, GeomAlt,
-                                  std::conditional_t<std::is_same<VT, F32Wide>::value, GeomWideRows,
                                   std::conditional_t<std::is_same<VT, F32P>::value, GeomPlainRows,
-                                  std::conditional_t<kStencil<VT>, GeomStencil, GeomWide>>>>>;
+                                  std::conditional_t<kStencil<VT>, GeomStencil, GeomWide>>>>;
 template <typename VT>
 constexpr int kQuadWords = sizeof(VT) == 1 ? 1 : 2;
 
@@ -238,22 +233,6 @@ __device__ __forceinline__ f4a zpair_load2(const char *__restrict__ base, size_t
 __device__ __forceinline__ f2a zpair_load1(const char *__restrict__ base, size_t e)
 {
     return *reinterpret_cast<const f2a *>(base + e * 8);
-}
-
-// Global loads one Cell8::load issues.
-template <typename VT>
-constexpr int kCellLoads = kZPair<VT> ? (kPlainF32<VT> ? 4 : 2) : (kPlainByte<VT> ? 2 : 1);
-
-// s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt bits [3:0] + [15:14], expcnt and lgkmcnt left at
-// their no-wait maxima).  The pipelined march places it, in code every active lane runs, where
-// the stage about to be consumed must have landed and the next stage's N loads may stay in
-// flight: the compiler's own wait insertion then knows at the loop latch that the consumed
-// stage's registers are free, instead of draining every load at the loop head.
-template <int N>
-__device__ __forceinline__ void wait_vmcnt()
-{
-    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
-    __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
 // The 8 voxels of the cell whose low corner element is e:
@@ -937,14 +916,8 @@ __device__ unsigned int g_wg_count;
 #ifndef VR_SKIP_MIN_WAVES
 #define VR_SKIP_MIN_WAVES 1
 #endif
-#ifndef VR_PIPE_DEPTH
-#define VR_PIPE_DEPTH 2  // samples of a ray in flight in the PIPE kernels (2 or 3)
-#endif
 #ifndef VR_DEFER_SHADE
 #define VR_DEFER_SHADE 1  // pipelined + difference field: shade a sample one sample later
-#endif
-#ifndef VR_PIPE_UNIFORM
-#define VR_PIPE_UNIFORM 0  // 1: the pipelined march as a wave-uniform loop (measured slower)
 #endif
 #ifndef VR_PIPE_MIN_WAVES
 #define VR_PIPE_MIN_WAVES 1
@@ -1039,12 +1012,6 @@ __device__ __forceinline__ void phong(const MarchParams &P, float gx, float gy_,
     }
 }
 
-#ifndef VR_EXP_WAVE_STEPS
-#define VR_EXP_WAVE_STEPS 0
-#endif
-#ifndef VR_EXP_NO_GRAD_LOADS
-#define VR_EXP_NO_GRAD_LOADS 0  // experiment builds: time without the difference-field loads
-#endif
 // Gradient Phong extension for one sample with alpha > 0 (s: TF colour in/out): gradient from
 // the difference field (GF) or the stencil, scaled to normalised coordinates, headlight
 // ndl = |n . dir|, rgb' = rgb (ka + kd ndl) + ks ndl^p.  The oracle's march_pixel, same order.
@@ -1056,11 +1023,7 @@ __device__ __forceinline__ void shade_sample(const MarchParams &P, const char *_
                                              float4 &s)
 {
     float gx, gy_, gz;
-    if constexpr (GF && VR_EXP_NO_GRAD_LOADS) {  // timing experiment only: wrong gradient
-        gx = c.v[1] - c.v[0];
-        gy_ = c.v[2] - c.v[0];
-        gz = c.v[4] - c.v[0];
-    } else if constexpr (GF) {  // f32: precomputed difference field
+    if constexpr (GF) {  // f32: precomputed difference field
         grad_field<PACKED, kHalfField<VT>>(reinterpret_cast<const char *>(P.grad), ce, ax, ay, az,
                                            gx, gy_, gz);
     } else {
@@ -1220,51 +1183,9 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
             p1 = p1 + d1 * P.step;
             p2 = p2 + d2 * P.step;
         };
-#if VR_PIPE_DEPTH == 3
-        // three stages in rotation: the loads of samples k+1 and k+2 in flight while sample k
-        // is consumed (a stage is consumed only if every earlier one was in bounds and the ray
-        // has not terminated, as in the two-stage form)
-        Stage A, B, C;
-        int k = 0;
-        prep(A, k);
-        advance();
-        prep(B, ++k);
-        while (A.ok) {
-            advance();
-            prep(C, ++k);
-            if (consume(A) || !B.ok) break;
-            advance();
-            prep(A, ++k);
-            if (consume(B) || !C.ok) break;
-            advance();
-            prep(B, ++k);
-            if (consume(C)) break;
-        }
-#else
         Stage A, B;
         int k = 0;
         prep(A, k);
-#if VR_PIPE_UNIFORM
-        // Ping-pong with a wave-uniform loop: a lane whose ray has ended stops compositing
-        // (`run`) and loads a dummy cell, but the loop, the loads and the two waits below are
-        // uniform, so on every path the wait before a consume leaves exactly the next stage's
-        // loads outstanding.  (With a per-lane `break` between the halves -- or loads under a
-        // per-lane branch -- the CFG had a path on which the consumed stage's loads were not
-        // known to have landed, and the compiler drained every load: one sample in flight.)
-        bool run = A.ok;
-        while (__any(run)) {
-            advance();
-            prep(B, ++k, run);
-            wait_vmcnt<kCellLoads<VT>>();  // A landed; B's loads stay in flight
-            if (run && (consume(A) || !B.ok)) run = false;
-            // no exit here: a second loop exit would give the loop head a path with B's loads
-            // outstanding (one dummy half-iteration per wave instead)
-            advance();
-            prep(A, ++k, run);
-            wait_vmcnt<kCellLoads<VT>>();  // B landed; A's loads stay in flight
-            if (run && (consume(B) || !A.ok)) run = false;
-        }
-#else
         while (A.ok) {  // ping-pong: no register copies between the two stages
             advance();
             prep(B, ++k);
@@ -1273,9 +1194,7 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
             prep(A, ++k);
             if (consume(B)) break;
         }
-#endif
         finish();  // deferred shading: the sample still held when the ray left the volume
-#endif
     } else
     for (int it = 0; it < nsteps; ++it) {
         const bool interior = (unsigned)(it - 1) < (unsigned)kin;  // it in [1, kin]
@@ -1377,17 +1296,7 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
         const unsigned long long rays = wave_sum(covered ? 1ull : 0ull);
         const unsigned long long sm = wave_sum(n_samples);
         const unsigned long long sh = wave_sum(n_shaded);
-#if VR_EXP_WAVE_STEPS  // experiment builds: steps = 64 x the wave's longest ray (lane occupancy)
-        unsigned long long mx = n_steps;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const unsigned long long t = __shfl_xor(mx, o, 64);
-            mx = t > mx ? t : mx;
-        }
-        const unsigned long long st = 64ull * mx;
-#else
         const unsigned long long st = wave_sum(n_steps);
-#endif
         const unsigned long long sk = wave_sum(n_skipped);
         if (lane == 0) {
             atomicAdd(&P.counters[0], rays);
@@ -1578,365 +1487,6 @@ __global__ __launch_bounds__(kThreads) void march_pair_kernel(const MarchParams 
     }
 }
 
-// ---- LDS-staged march (north_star: "hot bricks staged in LDS") --------------------------------
-// The tile's 256 rays advance in lock step by step index.  Per STAGE of S steps the workgroup
-// computes the box of voxels its live rays' trilinear footprints (and, shaded, the gradient
-// stencil) can touch in steps [k0, k0 + S), loads that box from the zero-padded LINEAR volume
-// (MarchParams::lin) into LDS with LDS-DMA (global_load_lds: coalesced rows, no VGPRs), and
-// every ray takes its S samples from LDS: the per-sample gather leaves the texture-data path
-// (TA/TD) for ds_read.  Two staging buffers: stage s + 1's box is predicted from the rays'
-// current positions and its DMA issued before stage s is marched, so the load overlaps the
-// march; one workgroup barrier per stage.  Same positions, predicates, voxels and operation
-// order as march_kernel: frames are bit-identical.  S adapts: halved while a box would not
-// fit, doubled while it fills less than a third of a buffer; a stage whose single-step box
-// still does not fit (rays far apart: zoomed-out views of big volumes) reads the linear volume
-// directly.
-#ifndef VR_LDS_BUF_BYTES
-#define VR_LDS_BUF_BYTES 16128  // x 2 + 8 KiB TF + 256 B = 40704 B: 4 workgroups (16 waves) per CU
-#endif
-#ifndef VR_LDS_S0
-#define VR_LDS_S0 8
-#endif
-#ifndef VR_LDS_SMAX
-#define VR_LDS_SMAX 64
-#endif
-#ifndef VR_LDS_MIN_WAVES
-#define VR_LDS_MIN_WAVES 4
-#endif
-constexpr int kLdsBufBytes = VR_LDS_BUF_BYTES;
-
-// LDS-DMA chunk per lane: 16 B (4 f32) or 4 B (4 x 8-bit, 2 x 16-bit); the box's x extent is a
-// whole number of chunks, aligned in the padded volume (row pitch lpx is a multiple of 4).
-template <typename T>
-struct LdsChunk {
-    static constexpr int kBytes = sizeof(T) == 4 ? 16 : 4;
-    static constexpr int kVox = kBytes / (int)sizeof(T);
-};
-
-template <typename T, typename IdxT>
-__device__ __forceinline__ float vox_f(const T *base, IdxT i)
-{
-    return (float)base[i];
-}
-
-// Ray state of the LDS march.
-struct LaneRay {
-    float p0, p1, p2, d0, d1, d2;
-    float T, cr, cg, cb;
-    int kin, nsteps;
-    bool alive;
-};
-
-// Steps [k0, k0 + S) of one ray, voxels from `base` (the staged box or, for a stage that does
-// not fit, the linear volume) with box origin (ox, oy, oz) in padded coordinates and row /
-// slice pitches py, pz.  Branch-free per step (as march_kernel's PIPE path): the predicates
-// set `alive` and `slab`, the voxel reads are unconditional (the box origin for a lane without
-// a sample, whose alpha is then 0: it composites +0 and leaves T), so the loop's trip count is
-// wave-uniform and only the shading of visible samples branches.
-template <typename T, bool SHADE, typename IdxT>
-__device__ __forceinline__ void lds_steps(const MarchParams &P, LaneRay &R, const float4 *s_tf,
-                                          const T *base, int ox, int oy, int oz, IdxT py,
-                                          IdxT pz, int k0, int S)
-{
-    for (int j = 0; j < S; ++j) {
-        if (!__any(R.alive)) break;
-        const int k = k0 + j;
-        // predicates as bitwise ops (no short-circuit branches)
-        const bool interior = (unsigned)(k - 1) < (unsigned)R.kin;  // k in [1, kin]
-        // volume.frag:31-37: the step bound, then the break if any component > 1 or < 0
-        const bool oob = (R.p0 > 1.0f) | (R.p1 > 1.0f) | (R.p2 > 1.0f) | (R.p0 < 0.0f) |
-                         (R.p1 < 0.0f) | (R.p2 < 0.0f);
-        R.alive = R.alive & (k < R.nsteps) & (interior | !oob);
-        // volume.frag:39-40 (strict)
-        const bool inslab = (R.p0 < P.smax[0]) & (R.p1 < P.smax[1]) & (R.p2 < P.smax[2]) &
-                            (R.p0 > P.smin[0]) & (R.p1 > P.smin[1]) & (R.p2 > P.smin[2]);
-        const bool slab = R.alive & (interior | inslab);
-        int i, jj, kk;
-        float ax, ay, az;
-        texel_coord(R.p0, P.fnx, i, ax);
-        texel_coord(R.p1, P.fny, jj, ay);
-        texel_coord(R.p2, P.fnz, kk, az);
-        const IdxT e0 = ((IdxT)(kk + kPad - oz)) * pz + (IdxT)(jj + kPad - oy) * py +
-                        (IdxT)(i + kPad - ox);
-        const IdxT e = slab ? e0 : (IdxT)0;
-        const float v0 = vox_f(base, e), v1 = vox_f(base, e + 1);
-        const float v2 = vox_f(base, e + py), v3 = vox_f(base, e + py + 1);
-        const float v4 = vox_f(base, e + pz), v5 = vox_f(base, e + pz + 1);
-        const float v6 = vox_f(base, e + pz + py), v7 = vox_f(base, e + pz + py + 1);
-        const float d = tri8(v0, v1, v2, v3, v4, v5, v6, v7, ax, ay, az);  // volume.frag:41
-        float4 sm = tf_lookup(s_tf, P.tf_n, P.tf_nf, div_by_range(d - P.vmin, P));  // :42-43
-        if (!slab) sm.w = 0.0f;
-        if (SHADE && sm.w > 0.0f) {
-            // central differences D_a(c) = v(c + e_a) - v(c - e_a) over the cell's corners
-            // (the oracle's grad_cell; march_kernel's stencil path, same operations)
-            const float v[8] = {v0, v1, v2, v3, v4, v5, v6, v7};
-            float Dx[8], Dy[8], Dz[8];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {  // rows (dy, dz) = (c & 1, c >> 1)
-                const IdxT r = e + (IdxT)(c & 1) * py + (IdxT)(c >> 1) * pz;
-                const int o = 2 * (c & 1) + 4 * (c >> 1);
-                Dx[o] = v[o + 1] - vox_f(base, r - 1);
-                Dx[o + 1] = vox_f(base, r + 2) - v[o];
-            }
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {  // columns (dx, dz) = (c & 1, c >> 1)
-                const IdxT r = e + (IdxT)(c & 1) + (IdxT)(c >> 1) * pz;
-                const int o = (c & 1) + 4 * (c >> 1);
-                Dy[o] = v[o + 2] - vox_f(base, r - py);
-                Dy[o + 2] = vox_f(base, r + 2 * py) - v[o];
-            }
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {  // columns (dx, dy) = (c & 1, c >> 1)
-                const IdxT r = e + (IdxT)(c & 1) + (IdxT)(c >> 1) * py;
-                const int o = (c & 1) + 2 * (c >> 1);
-                Dz[o] = v[o + 4] - vox_f(base, r - pz);
-                Dz[o + 4] = vox_f(base, r + 2 * pz) - v[o];
-            }
-            float gx, gy, gz;
-            grad_filter<true>(Dx, Dy, Dz, ax, ay, az, gx, gy, gz);
-            phong(P, gx, gy, gz, R.d0, R.d1, R.d2, sm);
-        }
-        // volume.frag:44-45 (a lane without a sample adds +0 and keeps T)
-        R.cr = R.cr + (sm.x * sm.w) * R.T;
-        R.cg = R.cg + (sm.y * sm.w) * R.T;
-        R.cb = R.cb + (sm.z * sm.w) * R.T;
-        R.T = R.T * (1.0f - sm.w);
-        if (R.T == 0.0f || R.T < P.ert_eps) R.alive = false;
-        // volume.frag:47
-        R.p0 = R.p0 + R.d0 * P.step;
-        R.p1 = R.p1 + R.d1 * P.step;
-        R.p2 = R.p2 + R.d2 * P.step;
-    }
-}
-
-// Packed 16-bit min over the wavefront (v_pk_min_u16 + DPP row shifts / broadcasts): each
-// 32-bit value holds two u16 keys, both minimised at once.
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b)
-{
-    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
-                                                                   __builtin_bit_cast(u16x2, b)));
-}
-__device__ __forceinline__ uint32_t wave_pk_min_u16(uint32_t v)
-{
-    constexpr int id = -1;  // 0xFFFF,0xFFFF: the identity where a DPP source lane is invalid
-    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x111, 0xf, 0xf, false));
-    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x112, 0xf, 0xf, false));
-    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x114, 0xf, 0xf, false));
-    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x118, 0xf, 0xf, false));
-    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x142, 0xa, 0xf, false));
-    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x143, 0xc, 0xf, false));
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-
-// LDS-DMA of one chunk per lane to the wave-uniform LDS byte address `lds` + lane * CB, issued
-// from inline asm: hipcc then keeps it out of its own s_waitcnt bookkeeping (with the builtin
-// it drains vmcnt(0) before every LDS read of the TF, which would retire the next stage's
-// prefetch at the first step of the current one); the kernel waits vmcnt(0) itself before the
-// barrier that publishes the buffer.  M0 written and restored in the same statement.
-__device__ __forceinline__ uint32_t lds_addr(const char *p)
-{
-    return (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)(size_t)(const __attribute__((address_space(3))) char *)p);
-}
-template <int CB>
-__device__ __forceinline__ void glds(const void *g, uint32_t lds)
-{
-    uint32_t keep;
-    if constexpr (CB == 16)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
-    else
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
-}
-
-// A stage's box in padded voxel coordinates: origin, extents (x in whole chunks).
-struct LdsBox {
-    int ox, oy, oz, Lx, Ly, Lz, nchunk;
-    bool empty;
-};
-
-template <typename T, bool SHADE>
-__global__ __launch_bounds__(kThreadsPerTile, VR_LDS_MIN_WAVES) void march_lds_kernel(const MarchParams P)
-{
-    constexpr int CB = LdsChunk<T>::kBytes, CV = LdsChunk<T>::kVox;
-    constexpr int kBufChunks = kLdsBufBytes / CB;
-    constexpr int kBufBytes = kBufChunks * CB;
-    constexpr int kTfBytes = kTfLut * 16, kRedBytes = 256;
-    // one LDS array (a second __shared__ object next to LDS-DMA staging can make hipcc drain
-    // vmcnt before every ds_read): TF pairs | reduction slots [2 rounds][4 waves][3] | 2 boxes
-    __shared__ __attribute__((aligned(16))) char smem[kTfBytes + kRedBytes + 2 * kBufBytes];
-    float4 *s_tf = reinterpret_cast<float4 *>(smem);
-    uint32_t *s_red = reinterpret_cast<uint32_t *>(smem + kTfBytes);
-    char *s_buf = smem + kTfBytes + kRedBytes;
-
-    const int tid = threadIdx.x;
-    uint32_t tile_x, tile_y;
-    if (!block_tile(P, tile_x, tile_y)) return;
-    const long long wg_start = wall_clock64();
-    for (int i = tid; i < 2 * (P.tf_n + 2); i += (int)kThreadsPerTile) s_tf[i] = P.tf[i];  // tf_n <= 256
-
-    const uint32_t wave = tid >> 6, lane = tid & 63;
-    const uint32_t ws = P.wave_w_shift, ww = 1u << ws, wh = 64u >> ws;
-    const uint32_t wpr = kTile >> ws;
-    const uint32_t px = tile_x * kTile + (wave % wpr) * ww + (lane & (ww - 1));
-    const uint32_t ly = tile_y * kMarchRows + (wave / wpr) * wh + (lane >> ws);
-    bool active = px < P.W && ly < P.local_rows;
-    const uint32_t blk = ly / P.row_block;
-    const uint32_t gy = (blk * P.nranks + P.rank) * P.row_block + (ly - blk * P.row_block);
-    active = active && gy < P.H;
-    float tex[3] = {0.f, 0.f, 0.f}, dir[3] = {0.f, 0.f, 0.f};
-    const bool covered = active && pixel_ray(P, px, gy, tex, dir);
-
-    LaneRay R;
-    R.p0 = tex[0];
-    R.p1 = tex[1];
-    R.p2 = tex[2];
-    R.d0 = dir[0];
-    R.d1 = dir[1];
-    R.d2 = dir[2];
-    R.T = 1.0f;
-    R.cr = R.cg = R.cb = 0.0f;
-    R.nsteps = covered ? P.nsteps : 0;
-    R.kin = (covered && P.slab_default) ? interior_steps(tex, dir, P.step, R.nsteps) : 0;
-    R.alive = covered && R.nsteps > 0;
-
-    const float fn[3] = {P.fnx, P.fny, P.fnz};
-    const int hi_cap[3] = {(int)P.nx + 3, (int)P.ny + 3, (int)P.nz + 3};  // padded [0, N + 3]
-    const T *lin = static_cast<const T *>(P.lin);
-    int rnd = 0;
-
-    // The box of voxels steps [k0 + a, k0 + a + n) of the live rays can read, predicted from
-    // their positions at step k0 (p_k = p_k0 + (k - k0) s, each float add off by <= 2^-24 for
-    // |p| < 2), clamped to [0, 1] (the bounds test breaks outside), texel coordinates
-    // p N - 0.5 with a margin for their float rounding; cells floor(u) .. floor(u) + 1, the
-    // gradient's stencil one more each side.  One workgroup barrier: it also orders every
-    // wave's earlier LDS reads and DMA waits before whatever follows it.
-    auto reduce_box = [&](int k0, int a, int n, LdsBox &B) {
-        uint32_t key[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-        const int first = k0 + a, last = min(k0 + a + n, R.nsteps) - 1;
-        if (R.alive && first <= last) {
-            const float pp[3] = {R.p0, R.p1, R.p2}, dd[3] = {R.d0, R.d1, R.d2};
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                const double sd = (double)(dd[c] * P.step);
-                const double q0 = (double)pp[c] + (double)(first - k0) * sd;
-                const double q1 = (double)pp[c] + (double)(last - k0) * sd;
-                const double m = (double)(last - k0 + 1) * 0x1p-23;
-                const double u0 = fmax(fmin(q0, q1) - m, 0.0), u1 = fmin(fmax(q0, q1) + m, 1.0);
-                const double cm = 1e-3 + (double)fn[c] * 0x1p-21;
-                int l = (int)floor(u0 * (double)fn[c] - 0.5 - cm) + kPad - (SHADE ? 1 : 0);
-                int h = (int)floor(u1 * (double)fn[c] - 0.5 + cm) + 1 + kPad + (SHADE ? 1 : 0);
-                l = max(l, 0);
-                h = min(h, hi_cap[c]);
-                if (l <= h) key[c] = (uint32_t)l | ((uint32_t)(0xFFFF - h) << 16);
-            }
-        }
-        uint32_t *slot = s_red + (rnd & 1) * 16 + wave * 4;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const uint32_t w = wave_pk_min_u16(key[c]);
-            if (lane == 0) slot[c] = w;
-        }
-        __syncthreads();
-        const uint32_t *r = s_red + (rnd & 1) * 16;
-        int lo[3], hi[3];
-        bool empty = false;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const uint32_t w = __builtin_amdgcn_readfirstlane(
-                pk_min_u16(pk_min_u16(r[c], r[4 + c]), pk_min_u16(r[8 + c], r[12 + c])));
-            lo[c] = (int)(w & 0xFFFFu);
-            hi[c] = 0xFFFF - (int)(w >> 16);
-            empty = empty || lo[c] > hi[c];
-        }
-        ++rnd;
-        B.empty = empty;
-        B.ox = lo[0] & ~(CV - 1);
-        const int ncx = (hi[0] - B.ox) / CV + 1;
-        B.Lx = ncx * CV;
-        B.oy = lo[1];
-        B.oz = lo[2];
-        B.Ly = hi[1] - lo[1] + 1;
-        B.Lz = hi[2] - lo[2] + 1;
-        B.nchunk = empty ? 0 : ncx * B.Ly * B.Lz;
-    };
-    // LDS-DMA of box B into buffer `buf`: chunk c = (z, y, cx) row-major -> byte c * CB, so a
-    // wave's 64 chunks land contiguously (LDS-DMA writes wave base + lane * CB).
-    auto stage = [&](const LdsBox &B, char *buf) {
-        const int ncx = B.Lx / CV;
-        const uint64_t mx = ((1ull << 40) + (uint64_t)ncx - 1) / (uint64_t)ncx;
-        const uint64_t my = ((1ull << 40) + (uint64_t)B.Ly - 1) / (uint64_t)B.Ly;
-        for (int c0 = (int)wave * 64; c0 < B.nchunk; c0 += 256) {
-            const int c = c0 + (int)lane;
-            if (c < B.nchunk) {
-                const uint32_t r = (uint32_t)(((uint64_t)c * mx) >> 40);
-                const uint32_t cx = (uint32_t)c - r * (uint32_t)ncx;
-                const uint32_t z = (uint32_t)(((uint64_t)r * my) >> 40);
-                const uint32_t y = r - z * (uint32_t)B.Ly;
-                const T *g = lin + (((size_t)(B.oz + (int)z) * P.lpy + (size_t)(B.oy + (int)y)) * P.lpx +
-                                    (size_t)B.ox + (size_t)cx * CV);
-                glds<CB>(g, lds_addr(buf + (size_t)c0 * CB));
-            }
-        }
-    };
-
-    // prologue: stage 0's box (halving S until it fits or S = 1)
-    int S = VR_LDS_S0, k0 = 0, b = 0;
-    LdsBox cur, nxt;
-    for (;;) {
-        reduce_box(0, 0, S, cur);
-        if (cur.empty || cur.nchunk <= kBufChunks || S == 1) break;
-        S >>= 1;
-    }
-    if (!cur.empty && cur.nchunk <= kBufChunks) stage(cur, s_buf);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    while (!cur.empty) {
-        // stage s + 1: predict its box, issue its DMA into the other buffer (free: every wave
-        // finished stage s - 1, which read it, before the reduction's barrier), then march
-        // stage s, whose DMA every wave waited for before that same barrier
-        int S2 = (cur.nchunk * 3 < kBufChunks && S < VR_LDS_SMAX) ? 2 * S : S;
-        for (;;) {
-            reduce_box(k0, S, S2, nxt);
-            if (nxt.empty || nxt.nchunk <= kBufChunks || S2 == 1) break;
-            S2 >>= 1;
-        }
-        if (!nxt.empty && nxt.nchunk <= kBufChunks) stage(nxt, s_buf + (b ^ 1) * kBufBytes);
-        if (cur.nchunk <= kBufChunks)
-            lds_steps<T, SHADE, int>(P, R, s_tf, reinterpret_cast<const T *>(s_buf + b * kBufBytes),
-                                     cur.ox, cur.oy, cur.oz, cur.Lx, cur.Lx * cur.Ly, k0, S);
-        else  // one step's footprint does not fit: this stage reads the linear volume
-            lds_steps<T, SHADE, long long>(P, R, s_tf, lin, 0, 0, 0, (long long)P.lpx,
-                                           (long long)P.lpx * P.lpy, k0, S);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        k0 += S;
-        S = S2;
-        cur = nxt;
-        b ^= 1;
-    }
-
-    if (P.tile_cost) {  // adaptive order: this tile's duration for the next launch
-        if (tid == 0)
-            P.tile_cost[tile_y * P.tiles_x + tile_x] =
-                (uint32_t)min(wall_clock64() - wg_start, 0x7FFFFFFFLL);
-    }
-    if (!active) return;
-    const float A = 1.0f - R.T;  // volume.frag:50 + blend (offscreen_pass.cpp:715-725)
-    const float omA = 1.0f - A;
-    const float o0 = R.cr * A + P.clear[0] * omA;
-    const float o1 = R.cg * A + P.clear[1] * omA;
-    const float o2 = R.cb * A + P.clear[2] * omA;
-    const float o3 = A * A + P.clear[3] * omA;
-    const size_t idx = (size_t)ly * P.W + px;
-    if (P.out_format == 0) {
-        static_cast<uint32_t *>(P.out)[idx] =
-            unorm8(o0) | (unorm8(o1) << 8) | (unorm8(o2) << 16) | (unorm8(o3) << 24);
-    } else {
-        static_cast<float4 *>(P.out)[idx] = make_float4(o0, o1, o2, o3);
-    }
-}
-
 // ---- adaptive tile order --------------------------------------------------------------------
 
 // One workgroup per XCD x over its tile list (the tiles of the super-tiles s = x (mod 8), as
@@ -2052,26 +1602,6 @@ __global__ __launch_bounds__(256) void brick_kernel(const SrcT *__restrict__ src
             q.v[3] = at(x, y + 1, z + 1);
             reinterpret_cast<Quad *>(dst)[g] = q;
         }
-    }
-}
-
-// ---- volume ingest: linear -> zero-padded linear (march_lds_kernel's staging source) ----------
-template <typename SrcT, typename DstT>
-__global__ __launch_bounds__(256) void pad_kernel(const SrcT *__restrict__ src,
-                                                  DstT *__restrict__ dst, uint32_t nx,
-                                                  uint32_t ny, uint32_t nz, uint32_t lpx,
-                                                  uint32_t lpy, size_t total)
-{
-    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
-         g += (size_t)gridDim.x * blockDim.x) {
-        const uint32_t px = (uint32_t)(g % lpx);
-        const size_t r = g / lpx;
-        const uint32_t py = (uint32_t)(r % lpy), pz = (uint32_t)(r / lpy);
-        const long x = (long)px - kPad, y = (long)py - kPad, z = (long)pz - kPad;
-        DstT v = (DstT)0;
-        if (x >= 0 && y >= 0 && z >= 0 && x < (long)nx && y < (long)ny && z < (long)nz)
-            v = (DstT)src[(size_t)x + (size_t)nx * ((size_t)y + (size_t)ny * (size_t)z)];
-        dst[g] = v;
     }
 }
 
@@ -2432,25 +1962,9 @@ hipError_t launch_pair_t(const MarchParams &p, hipStream_t stream)
     return hipGetLastError();
 }
 
-template <typename VT, bool SHADE>
-hipError_t launch_lds_t(const MarchParams &p, hipStream_t stream)
-{
-    const uint32_t nblocks = p.tile_perm ? p.nperm
-                             : p.tile_order >= 3 ? ((p.supers_total + 7) / 8) * 8 * kSuper * kSuper
-                                                 : p.tiles_x * p.tiles_y;
-    if (p.tiles_x * p.tiles_y == 0) return hipSuccess;
-    hipLaunchKernelGGL((march_lds_kernel<VT, SHADE>), dim3(nblocks), dim3(kThreadsPerTile), 0,
-                       stream, p);
-    return hipGetLastError();
-}
-
 template <typename VT>
 hipError_t launch_march_vt(bool shade, bool count, const MarchParams &p, hipStream_t s)
 {
-    if (p.lds && !count) {  // host: no skip-empty, tf_n <= kTfLds, lin present
-        if (shade) return launch_lds_t<Vox<VT>, true>(p, s);
-        return launch_lds_t<Vox<VT>, false>(p, s);
-    }
     if (p.pair) {  // host: not counting, no skip-empty, tf_n <= kTfLds, 16x8 tiles
         if (!shade) return launch_pair_t<VT, false, false>(p, s);
         if constexpr (kZPair<VT>)
@@ -2562,7 +2076,6 @@ hipError_t brick_from(const void *src, void *dst, uint32_t nx, uint32_t ny, uint
         case ST_U16: hipLaunchKernelGGL((brick_kernel<SrcT, uint16_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (uint16_t *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_I16: hipLaunchKernelGGL((brick_kernel<SrcT, int16_t>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (int16_t *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_F32 | kAltFlag: hipLaunchKernelGGL((brick_kernel<SrcT, F32Alt>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
-        case ST_F32 | kWideFlag: hipLaunchKernelGGL((brick_kernel<SrcT, F32Wide>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_F32 | kPlainF32Flag: hipLaunchKernelGGL((brick_kernel<SrcT, F32P>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
         case ST_F32 | kStencilF32Flag: hipLaunchKernelGGL((brick_kernel<SrcT, F32S>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
         default: hipLaunchKernelGGL((brick_kernel<SrcT, float>), dim3(grid_bricks(total)), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, nbx, nby, total); break;
@@ -2583,18 +2096,16 @@ hipError_t launch_march(int storage, bool shade, bool count, const MarchParams &
         case ST_U16: return launch_march_vt<uint16_t>(shade, count, p, stream);
         case ST_I16: return launch_march_vt<int16_t>(shade, count, p, stream);
         case ST_F32:
-            if (shade && p.grad && p.grad_half && !p.lds)
+            if (shade && p.grad && p.grad_half)
                 return launch_march_half_field<F32H>(count, p, stream);
             return launch_march_vt<float>(shade, count, p, stream);
         case ST_F32 | kAltFlag:
-        case ST_F32 | kWideFlag:
         case ST_F32 | kPlainF32Flag:
         case ST_F32 | kStencilF32Flag:
-            if (count || p.pair || p.lds || p.skip_empty || p.grad) return hipErrorInvalidValue;
+            if (count || p.pair || p.skip_empty || p.grad) return hipErrorInvalidValue;
             if (storage & kPlainF32Flag) return launch_march_alt<F32P>(shade, p, stream);
             if (storage & kStencilF32Flag) return launch_march_alt<F32S>(shade, p, stream);
-            return (storage & kAltFlag) ? launch_march_alt<F32Alt>(shade, p, stream)
-                                        : launch_march_alt<F32Wide>(shade, p, stream);
+            return launch_march_alt<F32Alt>(shade, p, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -2604,11 +2115,11 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
     // demangled names as rocprofv3 reports them (kernel-trace "Kernel_Name"); storage is the
     // layout code (8-bit yz-quads: the Quad8 instantiations)
     static const std::vector<std::string> names = [] {
-        const char *types[12] = {"unsigned char", "signed char", "unsigned short", "short", "float",
+        const char *types[11] = {"unsigned char", "signed char", "unsigned short", "short", "float",
                                  "vr::Quad8<unsigned char>", "vr::Quad8<signed char>", "vr::F32Alt",
-                                 "vr::F32Wide", "vr::F32H", "vr::F32P", "vr::F32S"};
+                                 "vr::F32H", "vr::F32P", "vr::F32S"};
         std::vector<std::string> v;
-        for (int t = 0; t < 12; ++t)
+        for (int t = 0; t < 11; ++t)
             for (int k = 0; k < 32; ++k) {
                 std::string n = std::string("void vr::(anonymous namespace)::march_kernel<") + types[t];
                 for (int bit = 4; bit >= 0; --bit) n += (k >> bit) & 1 ? ", true" : ", false";
@@ -2618,29 +2129,12 @@ const char *march_kernel_name(int storage, bool shade, bool count, bool skip, bo
     }();
     if (storage & kQuadFlag) storage = 5 + (storage & 0xF);
     if (storage & kAltFlag) storage = 7;
-    if (storage & kWideFlag) storage = 8;
-    if (storage & kHalfFieldFlag) storage = 9;
-    if (storage & kPlainF32Flag) storage = 10;
-    if (storage & kStencilF32Flag) storage = 11;
-    if (storage < 0 || storage > 11) return "march_kernel<?>";
+    if (storage & kHalfFieldFlag) storage = 8;
+    if (storage & kPlainF32Flag) storage = 9;
+    if (storage & kStencilF32Flag) storage = 10;
+    if (storage < 0 || storage > 10) return "march_kernel<?>";
     const int k = (shade ? 16 : 0) + (count ? 8 : 0) + (skip ? 4 : 0) + (gf ? 2 : 0) + (pipe ? 1 : 0);
     return names[storage * 32 + k].c_str();
-}
-
-const char *march_lds_kernel_name(int storage, bool shade)
-{
-    static const std::vector<std::string> names = [] {
-        const char *types[5] = {"unsigned char", "signed char", "unsigned short", "short", "float"};
-        std::vector<std::string> v;
-        for (int t = 0; t < 5; ++t)
-            for (int sh = 0; sh < 2; ++sh)
-                v.push_back(std::string("void vr::(anonymous namespace)::march_lds_kernel<") + types[t] +
-                            (sh ? ", true" : ", false") + ">(vr::MarchParams)");
-        return v;
-    }();
-    storage &= 0xF;  // the voxel type: the LDS kernel reads the linear copy
-    if (storage < 0 || storage > 4) return "march_lds_kernel<?>";
-    return names[storage * 2 + (shade ? 1 : 0)].c_str();
 }
 
 hipError_t launch_unbrick(int storage, const void *bricks, void *dst, uint32_t nx, uint32_t ny,
@@ -2656,42 +2150,6 @@ hipError_t launch_unbrick(int storage, const void *bricks, void *dst, uint32_t n
         default: hipLaunchKernelGGL((unbrick_kernel<float>), dim3(g), dim3(256), 0, s, (const float *)bricks, (float *)dst, nx, ny, bx, by, z0, n); break;
     }
     return hipGetLastError();
-}
-
-template <typename SrcT>
-hipError_t pad_from(const void *src, void *dst, uint32_t nx, uint32_t ny, uint32_t nz,
-                    int storage, hipStream_t s)
-{
-    const uint32_t lpx = lin_pitch_x(nx), lpy = ny + 2 * kPad;
-    const size_t total = lin_elems(nx, ny, nz);
-    const SrcT *sp = static_cast<const SrcT *>(src);
-    const unsigned g = grid_for(total);
-    switch (storage) {
-        case ST_U8: hipLaunchKernelGGL((pad_kernel<SrcT, uint8_t>), dim3(g), dim3(256), 0, s, sp, (uint8_t *)dst, nx, ny, nz, lpx, lpy, total); break;
-        case ST_I8: hipLaunchKernelGGL((pad_kernel<SrcT, int8_t>), dim3(g), dim3(256), 0, s, sp, (int8_t *)dst, nx, ny, nz, lpx, lpy, total); break;
-        case ST_U16: hipLaunchKernelGGL((pad_kernel<SrcT, uint16_t>), dim3(g), dim3(256), 0, s, sp, (uint16_t *)dst, nx, ny, nz, lpx, lpy, total); break;
-        case ST_I16: hipLaunchKernelGGL((pad_kernel<SrcT, int16_t>), dim3(g), dim3(256), 0, s, sp, (int16_t *)dst, nx, ny, nz, lpx, lpy, total); break;
-        default: hipLaunchKernelGGL((pad_kernel<SrcT, float>), dim3(g), dim3(256), 0, s, sp, (float *)dst, nx, ny, nz, lpx, lpy, total); break;
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_pad_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,
-                                  uint32_t ny, uint32_t nz, int storage, hipStream_t s)
-{
-    switch (src_dtype) {  // enum vr_dtype
-        case 1: return pad_from<int8_t>(src, dst, nx, ny, nz, storage, s);
-        case 2: return pad_from<uint8_t>(src, dst, nx, ny, nz, storage, s);
-        case 3: return pad_from<int16_t>(src, dst, nx, ny, nz, storage, s);
-        case 4: return pad_from<uint16_t>(src, dst, nx, ny, nz, storage, s);
-        case 5: return pad_from<int32_t>(src, dst, nx, ny, nz, storage, s);
-        case 6: return pad_from<uint32_t>(src, dst, nx, ny, nz, storage, s);
-        case 7: return pad_from<int64_t>(src, dst, nx, ny, nz, storage, s);
-        case 8: return pad_from<uint64_t>(src, dst, nx, ny, nz, storage, s);
-        case 9: return pad_from<float>(src, dst, nx, ny, nz, storage, s);
-        case 10: return pad_from<double>(src, dst, nx, ny, nz, storage, s);
-        default: return hipErrorInvalidValue;
-    }
 }
 
 hipError_t launch_brick_from_linear(int src_dtype, const void *src, void *dst, uint32_t nx,

@@ -95,9 +95,9 @@ DIST_SYMBOLS = [
 DIST_ID_BYTES = 128  # include/vr/vr_dist.h VR_DIST_ID_BYTES
 DEBUG_SYMBOLS = ["vr_debug_set_knob", "vr_debug_get_knob"]
 # include/vr/vr_debug.h enum vr_knob (launch-policy overrides: speed only, never results)
-KNOBS = {"pipeline": 1, "pair": 2, "pair_lanes": 3, "grad_field": 4, "lds": 5, "u8_layout": 6,
+KNOBS = {"pipeline": 1, "pair": 2, "pair_lanes": 3, "grad_field": 4, "u8_layout": 6,
          "tile_order": 7, "narrow": 8, "alt_geometry": 9}
-KNOB_AUTO = {"pipeline": -1, "pair": -1, "pair_lanes": 0, "grad_field": -1, "lds": 0,
+KNOB_AUTO = {"pipeline": -1, "pair": -1, "pair_lanes": 0, "grad_field": -1,
              "u8_layout": -1, "tile_order": 0, "narrow": 1, "alt_geometry": -1}
 
 ABI_VERSION = 6  # include/vr/vr.h VR_ABI_VERSION
