@@ -295,6 +295,20 @@ def run_variant(rp, cfg, steps, warmup, rank, world, inflight, row_block=8, grou
                      render_span_ms=None if np.isnan(float(v[3])) else round(float(v[3]), 4),
                      gather_span_ms=None if np.isnan(float(v[4])) else round(float(v[4]), 4))
                 for v in (t.cpu() for t in per_rank)]
+    if group:
+        # one process drives every device: one entry per device of the context, from its own
+        # HIP events (vr_debug_timing_member), so a slow frame names its straggler
+        loop = round((t1 - t0) / steps * 1e3, 4)
+        per_rank = []
+        for m in range(bin(rp.device_mask).count("1")):
+            t = rp.timing_member(m)
+            n = max(t["frames"], 1)
+            per_rank.append(dict(rank=m, device=t["device"], loop_ms_per_frame=loop,
+                                 kernel_ms=round(t["kernel_ms"] / n, 4),
+                                 render_span_ms=round(t["render_ms"] / n, 4),
+                                 gather_span_ms=round(t["gather_ms"] / n, 4),
+                                 assemble_span_ms=round(t["assemble_ms"] / n, 4) if m == 0 else None,
+                                 frames=t["frames"]))
     check = None
     if world > 1 and rank == 0:
         # the assembled frame must equal this device's single-rank render of the whole frame
@@ -305,7 +319,9 @@ def run_variant(rp, cfg, steps, warmup, rank, world, inflight, row_block=8, grou
         check = bool(torch.equal(full[:H], pipe.last.frame))
     return dict(secs=float(el.item()), kms=kms / max(nl, 1), frame=frame_stats, mine=my_stats,
                 shard_px=sr * W, check=check, per_rank=per_rank, warmup_frames=warmup,
-                last_frame=pipe.last.frame if group else None)
+                last_frame=pipe.last.frame if group else None,
+                last_frame_ptr=slots[0].shard.data_ptr() if slots else pipe.last.frame.data_ptr(),
+                keep=slots)
 
 
 def host_cores():
@@ -600,6 +616,46 @@ def main():
                  "bit-identical to the f32 oracle",
             warmup_frames=V["warmup_frames"])
 
+    if not args.no_variants and args.config == "c3" and world == 1 and not group:
+        # A camera crossing view classes: after frames of the fill view (the
+        # difference field), the reference's default camera needs the stencil copy (~0.76 GB for
+        # 512^3).  Built lazily, inside its first frame; or ahead by vr_prepare.  Serial frames,
+        # host-timed, derived structures freed before each arm (budget 0, then unlimited).
+        fcam = synth.camera(cfg["cam"]).to_vr_camera()
+        dcam = synth.camera("default").to_vr_camera()
+        vp = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"])
+
+        def fresh_fill():
+            rp.set_memory_budget(0)
+            rp.set_memory_budget(2 ** 64 - 1)
+            for _ in range(3):
+                rp.render_device(fcam, vp, R["last_frame_ptr"], vr_amd.OUT_RGBA8, 8, 0, 1)
+            torch.cuda.synchronize()
+
+        def one_frame(cam):
+            t0 = time.perf_counter()
+            rp.render_device(cam, vp, R["last_frame_ptr"], vr_amd.OUT_RGBA8, 8, 0, 1)
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) * 1e3
+
+        fresh_fill()
+        lazy = one_frame(dcam)
+        built = rp.memory_report()
+        steady = sorted(one_frame(dcam) for _ in range(20))[10]
+        fresh_fill()
+        t0 = time.perf_counter()
+        rp.prepare(dcam, vp)
+        prep = (time.perf_counter() - t0) * 1e3
+        prepared = one_frame(dcam)
+        variants["view_switch"] = dict(
+            path="fill view (r = 1.6, difference field) -> the reference's default camera (stencil copy)",
+            first_frame_lazy_ms=round(lazy, 3), first_frame_after_prepare_ms=round(prepared, 3),
+            prepare_ms=round(prep, 3), steady_serial_frame_ms=round(steady, 3),
+            derived_bytes_after_switch=built["derived_bytes"],
+            stencil_copy_bytes=built["stencil_copy_bytes"], field_bytes=built["field_bytes"],
+            note="host-timed serial frames around vr_render_device; vr_prepare builds the copy "
+                 "outside the frame (vr.h ABI 7)")
+
     if not args.no_variants and world == 1 and not group:
         # PCIe-inclusive: vr_render into (pageable) host memory, the drop-in record() path.
         # The frame's RGBA8 bytes cross PCIe inside the timed region; row bands copy while
@@ -638,6 +694,9 @@ def main():
         if group:
             parallelism = (f"image 8-row blocks cyclic x{n_gpus} devices in one process "
                            "(vr_create_mask) + RCCL ncclGather (ncclCommInitAll), stream-ordered")
+            if n_gpus > 1:
+                parallelism += ("; NOTE: the vr_create_mask path with >= 2 devices had not run on "
+                                "hardware before this run (frame_check verifies its frame)")
         elif world > 1:
             parallelism = f"image 8-row blocks cyclic x{world} processes" + (
                 " + gloo host-staged gather (rehearsal, ranks share devices)" if BACKEND != "nccl"

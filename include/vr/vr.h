@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 6
+#define VR_ABI_VERSION 7
 
 /* ---- status codes (negative errno style) ---- */
 #define VR_OK 0
@@ -238,6 +238,19 @@ int vr_render_device(vr_ctx *ctx, const vr_camera *cam, const vr_params *p, void
                      void *stream);
 /* Rows each rank writes for (H, row_block, nranks): ceil(ceil(H/row_block)/nranks)*row_block. */
 uint32_t vr_shard_rows(uint32_t height, uint32_t row_block, uint32_t nranks);
+/* Weighted row shares (ABI 7): block b of a frame split over nranks goes, per period of
+ * first_weight + (nranks - 1) * other_weight blocks, to rank 0 for the period's first
+ * first_weight blocks and to rank r > 0 for the other_weight blocks after first_weight +
+ * (r - 1) * other_weight.  (1, 1), the default, is block b -> rank b % nranks.  A lighter rank 0
+ * (e.g. 7, 8) leaves it time for receiving the other shards and assembling the frame.  Applies
+ * to vr_render_device with nranks > 1, vr_assemble_rows, vr_count_work and every frame of a
+ * vr_create_mask context (whose pipelines are rebuilt); every rank of one frame must use the
+ * same weights.  Frames are byte-identical for every choice.  Weights in [1, 64]. */
+int vr_set_row_share(vr_ctx *ctx, uint32_t first_weight, uint32_t other_weight);
+int vr_get_row_share(const vr_ctx *ctx, uint32_t *first_weight, uint32_t *other_weight);
+/* vr_shard_rows under the context's row share: the rows every rank's shard buffer holds (the
+ * largest share; ranks with fewer blocks leave their last rows unwritten). */
+uint32_t vr_shard_rows_ctx(const vr_ctx *ctx, uint32_t height, uint32_t row_block, uint32_t nranks);
 /* Rank-0 assembly after the gather: `gathered_dev` holds nranks shards back to back
  * (rank-major, vr_shard_rows() rows each); writes the H x W frame to `out_dev`. */
 int vr_assemble_rows(vr_ctx *ctx, const void *gathered_dev, void *out_dev, int out_format,
@@ -256,6 +269,36 @@ typedef struct vr_external_memory vr_external_memory;
 int vr_import_memory_fd(vr_ctx *ctx, int fd, uint64_t size, uint64_t offset,
                         vr_external_memory **mem, void **dev_ptr);
 int vr_release_external_memory(vr_ctx *ctx, vr_external_memory *mem);
+
+/* ---- derived structures and their memory (ABI 7) ----
+ * Beside the bricked volume the library may build, per device, structures that speed particular
+ * views up without changing a pixel: the difference field of shaded f32 dense-row views (3x the
+ * bricks; binary16 unless vr_params.exact_gradient), a 7x15x8-brick copy for oblique f32 views,
+ * a plain copy for unshaded sparse ones, a stencil copy for shaded sparse ones, and the
+ * skip-empty classification.  Each is built on the first frame that wants it (1-5 ms for 512^3,
+ * inside that frame) unless vr_prepare built it first.
+ * vr_set_memory_budget caps their total bytes on each device (the bricks never count): a
+ * structure that would not fit is not built, and its frames read the bricks instead (the same
+ * pixels; with the binary16 field absent a shaded frame forms exact f32 differences, i.e. the
+ * exact_gradient = 1 pixels).  An alternative copy may evict the others to fit.  0 keeps only
+ * the bricks; UINT64_MAX (the default) builds whatever fits beside a 2 GiB free-memory reserve.
+ * Lowering the budget waits for the device and frees the structures.
+ * vr_memory_report: the bytes each structure takes now on the (first) device.
+ * vr_prepare: builds everything a frame with this camera and params would read, synchronously,
+ * so that the next such frame builds nothing (e.g. before a camera move crosses view classes). */
+typedef struct vr_memory_info {
+    uint64_t volume_bytes;        /* the bricked volume (vr_volume_bytes)              */
+    uint64_t field_bytes;         /* difference field                                  */
+    uint64_t oblique_copy_bytes;  /* 7x15x8-cell z-pair copy (oblique views)           */
+    uint64_t plain_copy_bytes;    /* plain 15^3-cell copy (unshaded sparse views)      */
+    uint64_t stencil_copy_bytes;  /* 29^3-cell stencil copy (shaded sparse views)      */
+    uint64_t skip_bytes;          /* skip-empty brick ranges + distance field          */
+    uint64_t derived_bytes;       /* the sum of the five above: what the budget caps   */
+    uint64_t budget_bytes;        /* the budget in force (UINT64_MAX: default policy)  */
+} vr_memory_info;
+int vr_set_memory_budget(vr_ctx *ctx, uint64_t bytes);
+int vr_memory_report(const vr_ctx *ctx, vr_memory_info *out);
+int vr_prepare(vr_ctx *ctx, const vr_camera *cam, const vr_params *p);
 
 /* Count the work of one frame (same camera/params/shard) exactly; synchronous. */
 int vr_count_work(vr_ctx *ctx, const vr_camera *cam, const vr_params *p, uint32_t row_block,

@@ -42,6 +42,23 @@ enum vr_knob {
                                launch allows it (2, the retired z-pair sparse copy: EINVAL) */
 };
 
+/* Per-device timing of a context (ABI 7), so that a multi-GPU frame that runs slow names its
+ * straggler.  With vr_timing_enable on, summed since vr_timing_reset, for member m of a
+ * vr_create_mask context (member 0 = the lowest device, which also assembles; a one-device
+ * context has member 0 only, kernel time alone):
+ *   kernel_ms    its ray-march kernels (HIP events around each launch)
+ *   render_ms    its render step on its slot streams (the march plus the tile-order kernel)
+ *   gather_ms    its ncclGather on its communication stream (member 0: receiving every shard)
+ *   assemble_ms  member 0: the de-interleave of the gathered shards into the frame
+ *   frames       frames timed on that member
+ * (vr_timing_read on a multi-device context sums kernel_ms over the devices.) */
+typedef struct vr_member_timing {
+    int32_t device;
+    uint64_t frames;
+    double kernel_ms, render_ms, gather_ms, assemble_ms;
+} vr_member_timing;
+int vr_debug_timing_member(vr_ctx *ctx, int member, vr_member_timing *out);
+
 /* Set / read one knob of `ctx` (a multi-device context sets it on every device).
  * VR_EINVAL for an unknown knob or an out-of-range value. */
 int vr_debug_set_knob(vr_ctx *ctx, int knob, int value);

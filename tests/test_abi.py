@@ -58,7 +58,7 @@ def test_product_never_reads_the_environment():
 
 def test_library_loads_and_pure_entry_points():
     L = vr_amd.lib()
-    assert L.vr_abi_version() == 6
+    assert L.vr_abi_version() == 7
     p = vr_amd.default_params()
     assert p.step == pytest.approx(0.005) and p.ray_dist == pytest.approx(1.8)
     assert list(p.clear_color) == pytest.approx([0.11, 0.11, 0.11, 1.0])
@@ -72,6 +72,12 @@ def test_library_loads_and_pure_entry_points():
     mem, ptr = C.c_void_p(), C.c_void_p()
     assert L.vr_import_memory_fd(None, 3, 64, 0, C.byref(mem), C.byref(ptr)) == -22
     assert L.vr_release_external_memory(None, None) == -22
+    # ABI 7 entry points: argument checks before any HIP call
+    assert L.vr_set_row_share(None, 1, 1) == -22
+    assert L.vr_set_memory_budget(None, 0) == -22
+    assert L.vr_memory_report(None, None) == -22
+    assert L.vr_shard_rows_ctx(None, 1080, 8, 8) == 0
+    assert L.vr_debug_timing_member(None, 0, None) == -22
 
 
 def test_struct_layouts_match_header():
@@ -84,8 +90,10 @@ def test_struct_layouts_match_header():
 #include "vr/vr.h"
 #include <stdio.h>
 #include <stddef.h>
-int main(void) { printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(vr_camera), sizeof(vr_params),
-  sizeof(vr_stats), offsetof(vr_params, spec_power), offsetof(vr_params, skip_empty), offsetof(vr_params, frames_in_flight), offsetof(vr_params, exact_gradient)); return 0; }
+#include "vr/vr_debug.h"
+int main(void) { printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(vr_camera), sizeof(vr_params),
+  sizeof(vr_stats), offsetof(vr_params, spec_power), offsetof(vr_params, skip_empty), offsetof(vr_params, frames_in_flight), offsetof(vr_params, exact_gradient),
+  sizeof(vr_memory_info), sizeof(vr_member_timing), offsetof(vr_member_timing, kernel_ms)); return 0; }
 """
     tmp = os.path.join("/tmp", "vr_abi_layout")
     with open(tmp + ".c", "w") as f:
@@ -96,8 +104,10 @@ int main(void) { printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(vr_camera), size
                                      C.sizeof(vr_amd.vr_stats), vr_amd.vr_params.spec_power.offset,
                                      vr_amd.vr_params.skip_empty.offset,
                                      vr_amd.vr_params.frames_in_flight.offset,
-                                     vr_amd.vr_params.exact_gradient.offset]
-    assert "VR_ABI_VERSION 6" in src
+                                     vr_amd.vr_params.exact_gradient.offset,
+                                     C.sizeof(vr_amd.vr_memory_info), C.sizeof(vr_amd.vr_member_timing),
+                                     vr_amd.vr_member_timing.kernel_ms.offset]
+    assert "VR_ABI_VERSION 7" in src
 
 
 def test_create_without_device_fails_cleanly():

@@ -197,14 +197,17 @@ def _glib():
     return lib
 
 
-@pytest.mark.parametrize("members,inflight,nframes",
-                         [(2, 3, 7), (3, 2, 5), (3, 1, 3), (1, 2, 3), (8, 3, 6), (8, 1, 3)])
-def test_group_schedule_one_process(members, inflight, nframes):
+@pytest.mark.parametrize("members,inflight,nframes,share",
+                         [(2, 3, 7, (1, 1)), (3, 2, 5, (1, 1)), (3, 1, 3, (1, 1)), (1, 2, 3, (1, 1)),
+                          (8, 3, 6, (1, 1)), (8, 1, 3, (1, 1)), (8, 3, 4, (7, 8)), (3, 2, 4, (1, 3)),
+                          (4, 2, 3, (3, 1))])
+def test_group_schedule_one_process(members, inflight, nframes, share):
     """A multi-device context (vr_create_mask) in ONE process: vr_frame_workers.h issues every
     frame on N members -- member 0 on the calling thread, the others on worker threads -- each
     member running the same FrameSchedule as vr_dist (vr_dist.cpp group_render).  Here the
     members' streams are host threads, the render is the CPU oracle on the member's 8-row blocks,
-    the gather a host rendezvous standing in for ncclGather.  Every frame the caller consumes
+    the gather a host rendezvous standing in for ncclGather, the rows split by the row share
+    (vr_set_row_share: w0 blocks for member 0 per w0 + (N - 1) w).  Every frame the caller consumes
     equals the oracle's single-device frame bit for bit, and each member's op log honours the
     schedule (slot reuse, gather order, assembly after the caller consumed the previous frame)."""
     import sys
@@ -212,7 +215,7 @@ def test_group_schedule_one_process(members, inflight, nframes):
         sys.path.insert(0, os.path.join(ROOT, sub))
     import vr_dist
     W, H, rb = 36, 41, 8
-    rows = [vr_dist.shard_global_rows(H, rb, m, members) for m in range(members)]
+    rows = [vr_dist.shard_global_rows(H, rb, m, members, share) for m in range(members)]
     sr = len(rows[0])
     shards = [[np.zeros((sr, W, 4), np.float32) for _ in range(inflight)] for _ in range(members)]
     gbufs = [np.zeros((members, sr, W, 4), np.float32) for _ in range(inflight)]
@@ -246,7 +249,7 @@ def test_group_schedule_one_process(members, inflight, nframes):
                         for k in range(members):
                             gbufs[slot][k] = deposits.pop((frame, k))
             elif op == 2:
-                frame_buf[:] = vr_dist.assemble_numpy(gbufs[slot], H, rb, members)
+                frame_buf[:] = vr_dist.assemble_numpy(gbufs[slot], H, rb, members, share)
             elif op == 3:
                 consumed.append((frame, frame_buf.copy()))
         except Exception as e:  # reported by the test, never across the C boundary
@@ -351,3 +354,25 @@ def test_group_member_issue_failure_aborts_collectives(members, fail_member, fai
     assert lib.vr_group_host_synchronize(g) == -5
     assert sorted(rv.abort_calls) == list(range(members))  # abort ran once only
     lib.vr_group_host_destroy(g)
+
+
+@pytest.mark.parametrize("H,rb", [(53, 1), (1080, 8), (1080, 16), (7, 4), (4096, 8)])
+@pytest.mark.parametrize("nranks", [1, 2, 3, 8])
+@pytest.mark.parametrize("share", [(1, 1), (1, 2), (3, 4), (2, 1), (7, 8), (64, 1)])
+def test_row_share_maps_every_row_once(H, rb, nranks, share):
+    """The weighted block-cyclic split (vr_internal.h RowShare, restated in vr_dist.py): every
+    frame row belongs to exactly one rank, shards are padded to the largest share, and the
+    assembly inverts the shards; (1, 1) is the plain block-cyclic split of SURVEY.md 8e."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "volumetric-renderer_amd"))
+    import vr_amd
+    import vr_dist
+    sr = vr_dist.shard_rows(H, rb, nranks, share)
+    if share == (1, 1):
+        assert sr == vr_amd.shard_rows(H, rb, nranks)
+    rows = [vr_dist.shard_global_rows(H, rb, r, nranks, share) for r in range(nranks)]
+    owned = np.concatenate([x[x >= 0] for x in rows])
+    assert sorted(owned.tolist()) == list(range(H))
+    assert max(int((x >= 0).sum()) for x in rows) <= sr
+    g = np.stack(rows)
+    assert np.array_equal(vr_dist.assemble_numpy(g, H, rb, nranks, share), np.arange(H))

@@ -89,7 +89,7 @@ struct vr_ctx {
     // row bands of vr_render), each with its own tile durations.
     struct TileSched {
         uint32_t tiles_x = 0, tiles_y = 0, supers_x = 0, per_xcd = 0;
-        uint32_t row_block = 0, rank = 0, nranks = 0;
+        uint32_t row_block = 0, rank = 0, nranks = 0, share_w0 = 1, share_w = 1;
         int pair = 0;
         uint32_t kernel = 0;  // march variant (tile_kernel_key): its tiles' durations differ
         void *stream = nullptr;
@@ -129,6 +129,12 @@ struct vr_ctx {
     vr::Group *group = nullptr;
     uint32_t device_mask = 0;
     hipStream_t group_stream = nullptr;  // vr_render's frame stream (device 0)
+    // row blocks over ranks for vr_render_device (nranks > 1), vr_assemble_rows and every frame
+    // of a multi-device context (vr_set_row_share; vr_internal.h RowShare)
+    RowShare share{1, 1};
+    // device bytes the derived structures (difference field, alternative copies, skip-empty
+    // classification) may take together (vr_set_memory_budget); ~0 = the default policy
+    uint64_t budget = ~0ull;
     std::string err;
 };
 
@@ -593,7 +599,7 @@ bool use_pair(const vr_ctx *c, const MarchParams &P, const vr_params *p)
 
 int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
                  int out_format, uint32_t row_block, uint32_t rank, uint32_t nranks,
-                 MarchParams &P)
+                 RowShare share, MarchParams &P)
 {
     if (!cam) return fail(c, VR_EINVAL, "camera is NULL");
     int rc = check_params(c, p);
@@ -645,7 +651,9 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.row_block = row_block;
     P.rank = rank;
     P.nranks = nranks;
-    P.local_rows = vr_shard_rows(c->height, row_block, nranks);
+    P.local_rows = share_shard_rows(c->height, row_block, nranks, share);
+    P.share_w0 = share.w0;
+    P.share_w = share.w;
     P.tiles_x = (c->width + 15) / 16;
     P.tiles_y = (P.local_rows + kMarchRows - 1) / kMarchRows;
     P.tile_order = p->tile_order >= 1 && p->tile_order <= 4 ? (uint32_t)p->tile_order : 4u;
@@ -677,12 +685,67 @@ int record_build(vr_ctx *c, hipStream_t s)
     return VR_OK;
 }
 
+// ---- memory budget of the derived structures (vr_set_memory_budget) ----
+constexpr size_t kSkipBytesPerBrick = sizeof(float2) + 2;  // range + distance field + scratch
+size_t derived_bytes(const vr_ctx *c)
+{
+    size_t b = c->grad ? c->grad_bytes : 0;
+    for (const auto &a : c->alt)
+        if (a.bricks) b += a.bytes + kBrickSlackBytes;
+    return b + c->nbricks_alloc * kSkipBytesPerBrick;
+}
+// Would adding `extra` bytes (replacing `replaced` bytes of the same structure) stay within the
+// budget?  The default budget (~0) always allows; the 2 GiB free-memory reserve applies apart.
+bool budget_allows(const vr_ctx *c, size_t extra, size_t replaced)
+{
+    if (c->budget == ~0ull) return true;
+    const size_t now = derived_bytes(c) - replaced;
+    return now + extra <= c->budget;
+}
+// Free every alternative copy but `keep` (frames in flight may still read them: the device
+// drains first, as for any resource swap).
+int evict_alt_except(vr_ctx *c, int keep, hipStream_t s)
+{
+    bool any = false;
+    for (int i = 0; i < (int)(sizeof c->alt / sizeof c->alt[0]); ++i)
+        if (i != keep && c->alt[i].bricks) any = true;
+    if (!any) return VR_OK;
+    (void)s;
+    HIP_TRY(c, hipDeviceSynchronize(), "hipDeviceSynchronize (evict copy)");
+    for (int i = 0; i < (int)(sizeof c->alt / sizeof c->alt[0]); ++i)
+        if (i != keep && c->alt[i].bricks) {
+            hipFree(c->alt[i].bricks);
+            c->alt[i] = vr_ctx::AltCopy();
+        }
+    return VR_OK;
+}
+// Free every derived structure (after the device drained); rebuilt lazily within the budget.
+void free_derived(vr_ctx *c)
+{
+    if (c->grad) hipFree(c->grad);
+    c->grad = nullptr;
+    c->grad_bytes = 0;
+    c->grad_valid = false;
+    for (auto &a : c->alt) {
+        if (a.bricks) hipFree(a.bricks);
+        a = vr_ctx::AltCopy();
+    }
+    if (c->brick_range) hipFree(c->brick_range);
+    if (c->skip_dist) hipFree(c->skip_dist);
+    c->brick_range = nullptr;
+    c->skip_dist = nullptr;
+    c->nbricks_alloc = 0;
+    c->range_valid = c->dist_valid = false;
+}
+
 // skip_empty: (re)build the per-brick ranges and the distance field when stale, on `s` ahead of
 // the march that reads them.
 int ensure_skip(vr_ctx *c, MarchParams &P, hipStream_t s)
 {
     const size_t nb = (size_t)bricks_for(c->nx, 0, c->layout) * bricks_for(c->ny, 1, c->layout) * bricks_for(c->nz, 2, c->layout);
     if (nb > 0xFFFFFFFFull) return fail(c, VR_EINVAL, "skip_empty: too many bricks");
+    if (c->nbricks_alloc != nb && !budget_allows(c, nb * kSkipBytesPerBrick, c->nbricks_alloc * kSkipBytesPerBrick))
+        return VR_OK;  // over the memory budget: the frame samples every step (same pixels)
     if (c->nbricks_alloc != nb) {
         if (c->brick_range) hipFree(c->brick_range);
         if (c->skip_dist) hipFree(c->skip_dist);
@@ -739,7 +802,8 @@ bool ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s, bool half)
         c->grad_bytes = 0;
         c->grad_valid = false;
         size_t free_b = 0, total_b = 0;
-        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < bytes + (2ull << 30))
+        if (!budget_allows(c, bytes, 0) || hipMemGetInfo(&free_b, &total_b) != hipSuccess ||
+            free_b < bytes + (2ull << 30))
             return built;
         void *g = nullptr;
         if (hipMalloc(&g, bytes) != hipSuccess) {
@@ -851,6 +915,13 @@ int ensure_alt(vr_ctx *c, int lay, hipStream_t s, bool *ready)
     if (a.failed) return VR_OK;
     const size_t lin = (size_t)c->nx * c->ny * c->nz * sizeof(float);
     if (!a.bricks || a.bytes != bytes) {
+        const size_t had = a.bricks ? a.bytes + kBrickSlackBytes : 0;
+        if (!budget_allows(c, bytes + kBrickSlackBytes, had)) {
+            // over the budget: drop the other views' copies (the next view change rebuilds
+            // them) if that makes room, else this frame reads the 8^3 bricks (same pixels)
+            if (int rc = evict_alt_except(c, alt_index(lay), s)) return rc;
+            if (!budget_allows(c, bytes + kBrickSlackBytes, had)) return VR_OK;
+        }
         if (a.bricks) hipFree(a.bricks);
         a.bricks = nullptr;
         a.bytes = 0;
@@ -900,7 +971,7 @@ vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P, void *stream, uint32_t 
         if (t.tiles_x == P.tiles_x && t.tiles_y == P.tiles_y && t.pair == P.pair &&
             t.kernel == kernel &&
             t.stream == stream && t.row_block == P.row_block && t.rank == P.rank &&
-            t.nranks == P.nranks) {
+            t.nranks == P.nranks && t.share_w0 == P.share_w0 && t.share_w == P.share_w) {
             P.tile_cost = t.cost;
             if (t.have_perm) {
                 P.tile_perm = t.perm;
@@ -924,6 +995,8 @@ vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P, void *stream, uint32_t 
     t.row_block = P.row_block;
     t.rank = P.rank;
     t.nranks = P.nranks;
+    t.share_w0 = P.share_w0;
+    t.share_w = P.share_w;
     // per-XCD tile lists (tile_order 3's super-tile assignment), padded with ~0
     std::vector<std::vector<uint32_t>> xl(8);
     if (VR_LIST_ORDER == 1) {  // super-tile major
@@ -1085,6 +1158,12 @@ hipEvent_t pooled_event(vr_ctx *c)
 }  // namespace
 
 bool vr::is_multi_device(const vr_ctx *c) { return is_group(c); }
+
+namespace {
+int render_device_impl(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out_dev,
+                       int out_format, uint32_t row_block, uint32_t rank, uint32_t nranks,
+                       RowShare share, void *stream, bool launch = true);
+}
 
 extern "C" {
 
@@ -1561,11 +1640,101 @@ uint32_t vr_shard_rows(uint32_t height, uint32_t row_block, uint32_t nranks)
     return ((blocks + nranks - 1) / nranks) * row_block;
 }
 
+uint32_t vr_shard_rows_ctx(const vr_ctx *c, uint32_t height, uint32_t row_block, uint32_t nranks)
+{
+    return c ? share_shard_rows(height, row_block, nranks, c->share) : 0;
+}
+
+int vr_set_row_share(vr_ctx *c, uint32_t first_weight, uint32_t other_weight)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (first_weight < 1 || other_weight < 1 || first_weight > 64 || other_weight > 64)
+        return fail(c, VR_EINVAL, "row share weights must be in [1, 64]");
+    if (is_group(c)) {  // frames in flight keep their split; the pipelines are rebuilt
+        if (int rc = group_idle(c)) return rc;
+        for (vr_ctx *m : c->members)
+            if (int rc = vr_set_row_share(m, first_weight, other_weight)) return member_rc(c, m, rc);
+    }
+    c->share = RowShare{first_weight, other_weight};
+    return VR_OK;
+}
+
+int vr_get_row_share(const vr_ctx *c, uint32_t *first_weight, uint32_t *other_weight)
+{
+    if (!c || !first_weight || !other_weight) return fail(nullptr, VR_EINVAL, "NULL argument");
+    *first_weight = c->share.w0;
+    *other_weight = c->share.w;
+    return VR_OK;
+}
+
+int vr_set_memory_budget(vr_ctx *c, uint64_t bytes)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (is_group(c)) {  // per device: every member holds its own replica's structures
+        if (int rc = group_idle(c)) return rc;
+        for (vr_ctx *m : c->members)
+            if (int rc = vr_set_memory_budget(m, bytes)) return member_rc(c, m, rc);
+        c->budget = bytes;
+        return VR_OK;
+    }
+    if (int rc = wait_idle(c)) return rc;  // frames in flight may read what is freed
+    c->budget = bytes;
+    if (derived_bytes(c) > bytes) free_derived(c);
+    return VR_OK;
+}
+
+int vr_memory_report(const vr_ctx *c, vr_memory_info *out)
+{
+    if (!c || !out) return fail(nullptr, VR_EINVAL, "NULL argument");
+    if (is_group(c)) return vr_memory_report(c->members[0], out);  // per device (replicated)
+    std::memset(out, 0, sizeof *out);
+    out->volume_bytes = c->brick_bytes;
+    out->field_bytes = c->grad ? c->grad_bytes : 0;
+    uint64_t *copies[3] = {&out->oblique_copy_bytes, &out->plain_copy_bytes, &out->stencil_copy_bytes};
+    for (int i = 0; i < 3; ++i)
+        *copies[i] = c->alt[i].bricks ? c->alt[i].bytes + kBrickSlackBytes : 0;
+    out->skip_bytes = c->nbricks_alloc * kSkipBytesPerBrick;
+    out->derived_bytes = derived_bytes(c);
+    out->budget_bytes = c->budget;
+    return VR_OK;
+}
+
+int vr_prepare(vr_ctx *c, const vr_camera *cam, const vr_params *p)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (is_group(c)) {
+        if (int rc = group_idle(c)) return rc;
+        for (vr_ctx *m : c->members)
+            if (int rc = vr_prepare(m, cam, p)) return member_rc(c, m, rc);
+        hipSetDevice(c->device);
+        return VR_OK;
+    }
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    // the whole frame as vr_render_device launches it (one rank), up to the launch
+    if (int rc = render_device_impl(c, cam, p, c->counters, VR_OUT_RGBA8, 16, 0, 1, c->share,
+                                    nullptr, false))
+        return rc;
+    HIP_TRY(c, hipStreamSynchronize(nullptr), "hipStreamSynchronize (prepare)");
+    return VR_OK;
+}
+
 int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out_dev,
                      int out_format, uint32_t row_block, uint32_t rank, uint32_t nranks,
                      void *stream)
 {
     if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    return render_device_impl(c, cam, p, out_dev, out_format, row_block, rank, nranks, c->share,
+                              stream);
+}
+
+}  // extern "C"
+namespace {
+// launch = false (vr_prepare): everything up to the launch -- the derived structures this frame
+// reads are built on `stream` -- and no launch.
+int render_device_impl(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out_dev,
+                       int out_format, uint32_t row_block, uint32_t rank, uint32_t nranks,
+                       RowShare share, void *stream, bool launch)
+{
     if (!out_dev) return fail(c, VR_EINVAL, "output buffer is NULL");
     if (is_group(c)) {
         // the whole frame, split over the devices internally (8-row blocks, block-cyclic)
@@ -1582,7 +1751,7 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
         return VR_OK;
     }
     MarchParams P;
-    int rc = build_params(c, cam, p, out_dev, out_format, row_block, rank, nranks, P);
+    int rc = build_params(c, cam, p, out_dev, out_format, row_block, rank, nranks, share, P);
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1609,6 +1778,7 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
             P.nby = bricks_for(c->ny, 1, layout);
         }
     }
+    if (!launch) return VR_OK;
     vr_ctx::TileSched *ts =
         tile_sched(c, P, stream, tile_kernel_key(P, p->shading != 0, layout));
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1633,6 +1803,8 @@ int vr_render_device(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *
     }
     return VR_OK;
 }
+}  // namespace
+extern "C" {
 
 int vr_render(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out, int out_format)
 {
@@ -1675,7 +1847,8 @@ int vr_render(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out, in
         c->frame_bytes = bytes;
     }
     if (nb == 1) {
-        int rc = vr_render_device(c, cam, p, c->frame_dev, out_format, 16, 0, 1, nullptr);
+        int rc = render_device_impl(c, cam, p, c->frame_dev, out_format, 16, 0, 1, RowShare{1, 1},
+                                    nullptr);
         if (rc) return rc;
         HIP_TRY(c, hipMemcpy(out, c->frame_dev, (size_t)W * H * bpp, hipMemcpyDeviceToHost),
                 "hipMemcpy(frame)");
@@ -1695,8 +1868,9 @@ int vr_render(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out, in
     if (pb.frames_in_flight < 2) pb.frames_in_flight = 2;
     for (int b = 0; b < nb; ++b) {
         hipStream_t s = c->band_stream[b & 1];
-        int rc = vr_render_device(c, cam, &pb, static_cast<char *>(c->frame_dev) + (size_t)b * R * W * bpp,
-                                  out_format, R, (uint32_t)b, (uint32_t)nb, s);
+        int rc = render_device_impl(c, cam, &pb,
+                                    static_cast<char *>(c->frame_dev) + (size_t)b * R * W * bpp,
+                                    out_format, R, (uint32_t)b, (uint32_t)nb, RowShare{1, 1}, s);
         if (rc) return rc;
         HIP_TRY(c, hipEventRecord(c->band_ev[b], s), "hipEventRecord(band)");
     }
@@ -1729,7 +1903,8 @@ int vr_assemble_rows(vr_ctx *c, const void *gathered_dev, void *out_dev, int out
                                                             out_format, row_block, nranks, stream));
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     HIP_TRY(c, launch_assemble(gathered_dev, out_dev, out_format, c->width, c->height, row_block,
-                               nranks, vr_shard_rows(c->height, row_block, nranks),
+                               nranks, share_shard_rows(c->height, row_block, nranks, c->share),
+                               c->share,
                                static_cast<hipStream_t>(stream)),
             "assemble kernel");
     return VR_OK;
@@ -1802,8 +1977,9 @@ int vr_count_work(vr_ctx *c, const vr_camera *cam, const vr_params *p, uint32_t 
                          vr_count_work(c->members[0], cam, p, row_block, rank, nranks, out));
     }
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
-    const size_t bytes = (size_t)c->width * vr_shard_rows(c->height, row_block ? row_block : 1,
-                                                          nranks ? nranks : 1) * 4;
+    const size_t bytes = (size_t)c->width *
+                         share_shard_rows(c->height, row_block ? row_block : 1, nranks ? nranks : 1,
+                                          c->share) * 4;
     if (c->frame_bytes < bytes) {
         if (c->frame_dev) hipFree(c->frame_dev);
         c->frame_dev = nullptr;
@@ -1812,7 +1988,8 @@ int vr_count_work(vr_ctx *c, const vr_camera *cam, const vr_params *p, uint32_t 
         c->frame_bytes = bytes;
     }
     MarchParams P;
-    int rc = build_params(c, cam, p, c->frame_dev, VR_OUT_RGBA8, row_block, rank, nranks, P);
+    int rc = build_params(c, cam, p, c->frame_dev, VR_OUT_RGBA8, row_block, rank, nranks,
+                          c->share, P);
     if (rc) return rc;
     rc = ensure_derived(c, p, P, nullptr);
     if (rc) return rc;
@@ -1832,10 +2009,37 @@ int vr_timing_enable(vr_ctx *c, int enable)
 {
     if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
     // the members' frame workers may be inside vr_render_device: drain them first
-    if (is_group(c))
+    if (is_group(c)) {
         if (int rc = group_idle(c)) return rc;
+        vr::group_timing_enable(c->group, enable != 0);
+    }
     for (vr_ctx *m : c->members) vr_timing_enable(m, enable);
     c->timing = enable != 0;
+    return VR_OK;
+}
+
+int vr_debug_timing_member(vr_ctx *c, int member, vr_member_timing *out)
+{
+    if (!c || !out) return fail(c, VR_EINVAL, "NULL argument");
+    std::memset(out, 0, sizeof *out);
+    if (!is_group(c)) {  // one device: its kernel time only
+        if (member != 0) return fail(c, VR_EINVAL, "no such member");
+        out->device = c->device;
+        return vr_timing_read(c, &out->kernel_ms, &out->frames);
+    }
+    double ms[3] = {0.0, 0.0, 0.0};
+    uint64_t frames = 0;
+    std::string m;
+    if (int rc = vr::group_timing_member(c->group, member, ms, &frames, &m)) return fail(c, rc, m);
+    vr_ctx *mc = c->members[(size_t)member];
+    uint64_t launches = 0;
+    if (int rc = vr_timing_read(mc, &out->kernel_ms, &launches)) return member_rc(c, mc, rc);
+    hipSetDevice(c->device);
+    out->device = mc->device;
+    out->frames = frames;
+    out->render_ms = ms[0];
+    out->gather_ms = ms[1];
+    out->assemble_ms = ms[2];
     return VR_OK;
 }
 
@@ -1878,6 +2082,8 @@ int vr_timing_reset(vr_ctx *c)
 {
     if (is_group(c)) {
         if (int rc = group_idle(c)) return rc;
+        std::string m;
+        if (int rc = vr::group_timing_reset(c->group, &m)) return fail(c, rc, m);
         for (vr_ctx *m : c->members)
             if (int rc = vr_timing_reset(m)) return member_rc(c, m, rc);
         return VR_OK;

@@ -124,7 +124,7 @@ struct vr_dist {
     const vr_camera *cam = nullptr;  // the frame being issued
     const vr_params *params = nullptr;
     bool timing = false;
-    std::vector<TimedOp> t_render, t_gather;
+    std::vector<TimedOp> t_render, t_gather, t_assemble;
     std::string err;
 };
 
@@ -234,21 +234,45 @@ int HipExec::gather(int slot, uint64_t, Stream s)
 }
 int HipExec::assemble(int slot, uint64_t, void *frame_dev, Stream s)
 {
+    DTRY(timed_begin(d, d->t_assemble, s));
     if (vr_assemble_rows(d->ctx, d->bufs[slot].gbuf, frame_dev, d->out_format, d->row_block,
-                         (uint32_t)d->nranks, s) != VR_OK)
+                         (uint32_t)d->nranks, s) != VR_OK) {
+        timed_abort(d, d->t_assemble);
         return dfail(d, VR_EIO, std::string("assemble: ") + vr_last_error(d->ctx));
-    return VR_OK;
+    }
+    return timed_end(d, d->t_assemble, s);
 }
 
 void free_timing(vr_dist *d)
 {
-    for (auto *v : {&d->t_render, &d->t_gather}) {
+    for (auto *v : {&d->t_render, &d->t_gather, &d->t_assemble}) {
         for (auto &t : *v) {
             hipEventDestroy(t.t0);
             hipEventDestroy(t.t1);
         }
         v->clear();
     }
+}
+
+// Summed span of each timed op since the last read (render, gather, assemble) and the frames
+// timed; the record is cleared (on failure too).
+int timing_read3(vr_dist *d, double ms[3], uint64_t *frames)
+{
+    DTRY(vr_dist_synchronize(d));
+    int i = 0, rc = VR_OK;
+    for (auto *v : {&d->t_render, &d->t_gather, &d->t_assemble}) {
+        ms[i] = 0.0;
+        for (auto &t : *v) {
+            float x = 0.0f;
+            if (rc == VR_OK)
+                rc = hip_check(d, hipEventElapsedTime(&x, t.t0, t.t1), "hipEventElapsedTime");
+            ms[i] += x;
+        }
+        ++i;
+    }
+    if (frames) *frames = d->t_render.size();
+    free_timing(d);
+    return rc;
 }
 
 void release(vr_dist *d)
@@ -359,7 +383,7 @@ vr_dist *dist_create(vr_ctx *ctx, const void *id, ncclComm_t comm, int nranks, i
         delete d;
         return nullptr;
     }
-    d->shard_rows = vr_shard_rows(d->height, row_block, (uint32_t)nranks);
+    d->shard_rows = vr_shard_rows_ctx(ctx, d->height, row_block, (uint32_t)nranks);
     if (setup(d, id, comm, frames_in_flight) != VR_OK) {
         g_dist_err = d->err;
         release(d);
@@ -426,23 +450,10 @@ int vr_dist_timing_enable(vr_dist *d, int enable)
 int vr_dist_timing_read(vr_dist *d, double *render_ms, double *gather_ms, uint64_t *frames)
 {
     if (!d) return dfail(nullptr, VR_EINVAL, "dist is NULL");
-    DTRY(vr_dist_synchronize(d));
-    double acc[2] = {0.0, 0.0};
-    int i = 0;
-    int rc = VR_OK;
-    for (auto *v : {&d->t_render, &d->t_gather}) {
-        for (auto &t : *v) {
-            float ms = 0.0f;
-            if (rc == VR_OK)
-                rc = hip_check(d, hipEventElapsedTime(&ms, t.t0, t.t1), "hipEventElapsedTime");
-            acc[i] += ms;
-        }
-        ++i;
-    }
+    double acc[3];
+    const int rc = timing_read3(d, acc, frames);
     if (render_ms) *render_ms = acc[0];
     if (gather_ms) *gather_ms = acc[1];
-    if (frames) *frames = d->t_render.size();
-    free_timing(d);  // on failure too: the record is cleared either way, nothing leaks
     return rc;
 }
 
@@ -480,6 +491,14 @@ struct Group {
     std::vector<hipStream_t> own;      // members 1..: the stream standing in for the caller's
     uint32_t width = 0, height = 0;
     int frames = 0, out_format = -1;
+    uint32_t share_w0 = 1, share_w = 1;  // the row share the pipelines were built for
+    bool timing = false;                 // per-member render / gather / assembly spans
+    // per member: spans read from the pipelines so far (render, gather, assemble ms; frames)
+    struct Spans {
+        double ms[3] = {0.0, 0.0, 0.0};
+        uint64_t frames = 0;
+    };
+    std::vector<Spans> spans;
     std::unique_ptr<sched::FrameWorkers<GroupJob>> workers;
 };
 
@@ -494,9 +513,23 @@ int member_issue(Group *g, int m, const GroupJob &j, std::string *msg)
     return rc;
 }
 
+void fold_spans(Group *g)
+{
+    g->spans.resize(g->members.size());
+    for (size_t m = 0; m < g->dists.size(); ++m) {
+        double ms[3];
+        uint64_t n = 0;
+        if (g->dists[m] && timing_read3(g->dists[m], ms, &n) == VR_OK) {
+            for (int i = 0; i < 3; ++i) g->spans[m].ms[i] += ms[i];
+            g->spans[m].frames += n;
+        }
+    }
+}
+
 void free_pipelines(Group *g)
 {
     g->workers.reset();  // drains the queues and joins the threads
+    fold_spans(g);
     for (vr_dist *d : g->dists) {
         if (!d) continue;
         release(d);
@@ -510,10 +543,11 @@ void free_pipelines(Group *g)
 // The slot pipelines for this frame shape (size, frames in flight, pixel format).
 int ensure_pipelines(Group *g, int frames, int out_format, std::string *err)
 {
-    uint32_t w = 0, h = 0;
+    uint32_t w = 0, h = 0, s0 = 1, s1 = 1;
     vr_get_size(g->members[0], &w, &h);
+    vr_get_row_share(g->members[0], &s0, &s1);
     if (!g->dists.empty() && g->frames == frames && g->out_format == out_format && g->width == w &&
-        g->height == h)
+        g->height == h && g->share_w0 == s0 && g->share_w == s1)
         return VR_OK;
     std::string m;
     if (g->workers && g->workers->drain(&m) != VR_OK) {
@@ -531,10 +565,13 @@ int ensure_pipelines(Group *g, int frames, int out_format, std::string *err)
             free_pipelines(g);
             return VR_EIO;
         }
+        d->timing = g->timing;
         g->dists.push_back(d);
     }
     g->width = w;
     g->height = h;
+    g->share_w0 = s0;
+    g->share_w = s1;
     g->frames = frames;
     g->out_format = out_format;
     g->workers.reset(new sched::FrameWorkers<GroupJob>(
@@ -648,6 +685,33 @@ void group_destroy(Group *g)
         }
     if (!g->devices.empty()) hipSetDevice(g->devices[0]);
     delete g;
+}
+
+void group_timing_enable(Group *g, bool on)
+{
+    g->timing = on;
+    for (vr_dist *d : g->dists) d->timing = on;
+}
+
+int group_timing_member(Group *g, int m, double ms[3], uint64_t *frames, std::string *err)
+{
+    if (m < 0 || m >= (int)g->members.size()) {
+        *err = "no such member";
+        return VR_EINVAL;
+    }
+    if (int rc = group_synchronize(g, err)) return rc;
+    fold_spans(g);
+    for (int i = 0; i < 3; ++i) ms[i] = g->spans[m].ms[i];
+    *frames = g->spans[m].frames;
+    return VR_OK;
+}
+
+int group_timing_reset(Group *g, std::string *err)
+{
+    if (int rc = group_synchronize(g, err)) return rc;
+    fold_spans(g);
+    g->spans.assign(g->members.size(), Group::Spans());
+    return VR_OK;
 }
 
 int group_render(Group *g, const vr_camera *cam, const vr_params *p, void *out_dev,

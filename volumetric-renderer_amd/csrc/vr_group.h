@@ -38,5 +38,10 @@ int group_synchronize(Group *g, std::string *err);
 // complete once `stream` passes this point (the vr_dist_render contract).
 int group_render(Group *g, const vr_camera *cam, const vr_params *p, void *out_dev,
                  int out_format, hipStream_t stream, std::string *err);
+// Per-member spans (HIP events on the member's own streams; vr_debug_timing_member): render of
+// its row blocks, its ncclGather, and (member 0) the assembly, summed since the last reset.
+void group_timing_enable(Group *g, bool on);
+int group_timing_member(Group *g, int member, double ms[3], uint64_t *frames, std::string *err);
+int group_timing_reset(Group *g, std::string *err);
 
 }  // namespace vr

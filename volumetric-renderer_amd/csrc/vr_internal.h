@@ -245,6 +245,62 @@ inline uint32_t bricks_for(uint32_t n, int a, int st)
     return ((n + 3) / (uint32_t)brick_cells(st, a) + 1 + kGroupMask) & ~kGroupMask;
 }
 
+// ---- Frame rows over ranks (sort-first tiling) ------------------------------
+// The frame's rows are cut into blocks of row_block rows and dealt in periods of
+// w0 + (n - 1) w blocks: rank 0 takes the first w0 blocks of each period, rank r > 0 the w
+// blocks after w0 + (r - 1) w.  w0 = w = 1 (the default) is block b -> rank b mod n.  A smaller
+// w0 / w lightens rank 0, which also receives the other shards and assembles the frame
+// (vr_set_row_share).  Every rank sends the same number of rows (ncclGather
+// counts are equal): the largest share, padded.
+struct RowShare {
+    uint32_t w0, w;
+};
+__host__ __device__ inline uint32_t share_period(uint32_t n, RowShare s) { return s.w0 + (n - 1) * s.w; }
+__host__ __device__ inline uint32_t share_offset(uint32_t r, RowShare s)
+{
+    return r == 0 ? 0u : s.w0 + (r - 1) * s.w;
+}
+// global block of rank r's local block lb
+__host__ __device__ inline uint32_t share_global_block(uint32_t lb, uint32_t r, uint32_t n, RowShare s)
+{
+    const uint32_t w = r == 0 ? s.w0 : s.w;
+    return (lb / w) * share_period(n, s) + share_offset(r, s) + lb % w;
+}
+// owner rank and local block of global block gb
+__host__ __device__ inline void share_owner(uint32_t gb, uint32_t n, RowShare s, uint32_t &r,
+                                            uint32_t &lb)
+{
+    const uint32_t P = share_period(n, s), q = gb / P, o = gb - q * P;
+    if (o < s.w0) {
+        r = 0;
+        lb = q * s.w0 + o;
+    } else {
+        const uint32_t t = o - s.w0;
+        r = 1 + t / s.w;
+        lb = q * s.w + t % s.w;
+    }
+}
+// blocks rank r owns among the nb blocks of a frame
+inline uint32_t share_blocks(uint32_t nb, uint32_t r, uint32_t n, RowShare s)
+{
+    const uint32_t P = share_period(n, s), q = nb / P, o = nb - q * P;
+    const uint32_t w = r == 0 ? s.w0 : s.w, off = share_offset(r, s);
+    const uint32_t tail = o > off ? (o - off < w ? o - off : w) : 0u;
+    return q * w + tail;
+}
+// rows of every rank's shard buffer: the largest share
+inline uint32_t share_shard_rows(uint32_t height, uint32_t row_block, uint32_t n, RowShare s)
+{
+    if (row_block == 0 || n == 0 || s.w0 == 0 || s.w == 0) return 0;
+    const uint32_t nb = (height + row_block - 1) / row_block;
+    uint32_t m = share_blocks(nb, 0, n, s);
+    if (n > 1) {
+        const uint32_t b1 = share_blocks(nb, 1, n, s);  // rank 1 owns the most of ranks >= 1
+        m = b1 > m ? b1 : m;
+    }
+    return m * row_block;
+}
+
 // ---- Kernel parameters (one frame) -------------------------------------------------------
 struct MarchParams {
     const void *vol;        // bricked voxels, storage type per kernel instantiation
@@ -299,6 +355,7 @@ struct MarchParams {
     // 2^k (field_scale_log2; the shading normalises the gradient, so the scale cancels)
     int32_t grad_half;
     float inv_range;        // RN(1 / range) (div_fast)
+    uint32_t share_w0, share_w;  // RowShare of the row blocks over nranks
 };
 
 // Launchers (vr_kernels.hip).  All asynchronous on `stream`.
@@ -356,7 +413,7 @@ hipError_t launch_generate(int kind, int storage, void *dst_linear, uint32_t nx,
                            hipStream_t stream);
 hipError_t launch_assemble(const void *gathered, void *out, int out_format, uint32_t W,
                            uint32_t H, uint32_t row_block, uint32_t nranks,
-                           uint32_t shard_rows, hipStream_t stream);
+                           uint32_t shard_rows, RowShare share, hipStream_t stream);
 // Integer range of a LINEAR buffer of 32-bit or 64-bit voxels (vr_dtype 5..9): out3_dev = {min,
 // max, not-all-integers flag}, pre-set by the caller to {INT_MAX, INT_MIN, 0}.  Integers are
 // counted only in [-32768, 65535]; -0.0, NaN, infinities and fractions set the flag.

@@ -1066,7 +1066,8 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
     const uint32_t ly = tile_y * kMarchRows + (wave / wpr) * wh + (lane >> ws);
     bool active = px < P.W && ly < P.local_rows;
     const uint32_t blk = ly / P.row_block;
-    const uint32_t gy = (blk * P.nranks + P.rank) * P.row_block + (ly - blk * P.row_block);
+    const uint32_t gy = share_global_block(blk, P.rank, P.nranks, RowShare{P.share_w0, P.share_w}) *
+                            P.row_block + (ly - blk * P.row_block);
     active = active && gy < P.H;
 
     float tex[3] = {0.f, 0.f, 0.f}, dir[3] = {0.f, 0.f, 0.f};
@@ -1371,7 +1372,8 @@ __global__ __launch_bounds__(kThreads) void march_pair_kernel(const MarchParams 
     const uint32_t ly = tile_y * (kTile / L) + wave * (4 / L) + (q >> 4);
     bool active = px < P.W && ly < P.local_rows;
     const uint32_t blk = ly / P.row_block;
-    const uint32_t gy = (blk * P.nranks + P.rank) * P.row_block + (ly - blk * P.row_block);
+    const uint32_t gy = share_global_block(blk, P.rank, P.nranks, RowShare{P.share_w0, P.share_w}) *
+                            P.row_block + (ly - blk * P.row_block);
     active = active && gy < P.H;
 
     float tex[3] = {0.f, 0.f, 0.f}, dir[3] = {0.f, 0.f, 0.f};
@@ -1921,14 +1923,15 @@ template <typename PixT>
 __global__ __launch_bounds__(256) void assemble_kernel(const PixT *__restrict__ gathered,
                                                        PixT *__restrict__ out, uint32_t W,
                                                        uint32_t H, uint32_t rb, uint32_t nranks,
-                                                       uint32_t shard_rows)
+                                                       uint32_t shard_rows, RowShare share)
 {
     const size_t total = (size_t)W * H;
     for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
          g += (size_t)gridDim.x * blockDim.x) {
         const uint32_t y = (uint32_t)(g / W), x = (uint32_t)(g - (size_t)y * W);
         const uint32_t blk = y / rb;
-        const uint32_t rank = blk % nranks, lb = blk / nranks;
+        uint32_t rank, lb;
+        share_owner(blk, nranks, share, rank, lb);
         const uint32_t ly = lb * rb + (y - blk * rb);
         out[g] = gathered[((size_t)rank * shard_rows + ly) * W + x];
     }
@@ -2217,15 +2220,17 @@ hipError_t launch_int_range(int src_dtype, const void *src, size_t count, int *o
 
 hipError_t launch_assemble(const void *gathered, void *out, int out_format, uint32_t W,
                            uint32_t H, uint32_t row_block, uint32_t nranks,
-                           uint32_t shard_rows, hipStream_t s)
+                           uint32_t shard_rows, RowShare share, hipStream_t s)
 {
     const unsigned g = grid_for((size_t)W * H);
     if (out_format == 0)
         hipLaunchKernelGGL((assemble_kernel<uint32_t>), dim3(g), dim3(256), 0, s,
-                           (const uint32_t *)gathered, (uint32_t *)out, W, H, row_block, nranks, shard_rows);
+                           (const uint32_t *)gathered, (uint32_t *)out, W, H, row_block, nranks,
+                           shard_rows, share);
     else
         hipLaunchKernelGGL((assemble_kernel<float4>), dim3(g), dim3(256), 0, s,
-                           (const float4 *)gathered, (float4 *)out, W, H, row_block, nranks, shard_rows);
+                           (const float4 *)gathered, (float4 *)out, W, H, row_block, nranks,
+                           shard_rows, share);
     return hipGetLastError();
 }
 

@@ -62,6 +62,17 @@ class vr_orbit_camera(C.Structure):
                 ("radius", C.c_float)]
 
 
+class vr_memory_info(C.Structure):  # vr.h (ABI 7)
+    _fields_ = [(n, C.c_uint64) for n in (
+        "volume_bytes", "field_bytes", "oblique_copy_bytes", "plain_copy_bytes",
+        "stencil_copy_bytes", "skip_bytes", "derived_bytes", "budget_bytes")]
+
+
+class vr_member_timing(C.Structure):  # vr_debug.h (ABI 7)
+    _fields_ = [("device", C.c_int32), ("frames", C.c_uint64), ("kernel_ms", C.c_double),
+                ("render_ms", C.c_double), ("gather_ms", C.c_double), ("assemble_ms", C.c_double)]
+
+
 class vr_dataset(C.Structure):
     _fields_ = [("dims", C.c_uint32 * 3), ("dtype", C.c_int), ("data", C.c_void_p),
                 ("vmin", C.c_float), ("vmax", C.c_float)]
@@ -77,6 +88,8 @@ ABI_SYMBOLS = [
     "vr_shard_rows", "vr_assemble_rows", "vr_count_work", "vr_timing_enable",
     "vr_timing_read", "vr_timing_reset", "vr_kernel_name",
     "vr_import_memory_fd", "vr_release_external_memory",
+    "vr_set_row_share", "vr_get_row_share", "vr_shard_rows_ctx",
+    "vr_set_memory_budget", "vr_memory_report", "vr_prepare",
 ]
 HOST_SYMBOLS = [
     "vr_cam_init", "vr_cam_rotate", "vr_cam_zoom", "vr_cam_position", "vr_cam_view",
@@ -93,14 +106,14 @@ DIST_SYMBOLS = [
     "vr_dist_last_error", "vr_dist_destroy", "vr_dist_timing_enable", "vr_dist_timing_read",
 ]
 DIST_ID_BYTES = 128  # include/vr/vr_dist.h VR_DIST_ID_BYTES
-DEBUG_SYMBOLS = ["vr_debug_set_knob", "vr_debug_get_knob"]
+DEBUG_SYMBOLS = ["vr_debug_set_knob", "vr_debug_get_knob", "vr_debug_timing_member"]
 # include/vr/vr_debug.h enum vr_knob (launch-policy overrides: speed only, never results)
 KNOBS = {"pipeline": 1, "pair": 2, "pair_lanes": 3, "grad_field": 4, "u8_layout": 6,
          "tile_order": 7, "narrow": 8, "alt_geometry": 9}
 KNOB_AUTO = {"pipeline": -1, "pair": -1, "pair_lanes": 0, "grad_field": -1,
              "u8_layout": -1, "tile_order": 0, "narrow": 1, "alt_geometry": -1}
 
-ABI_VERSION = 6  # include/vr/vr.h VR_ABI_VERSION
+ABI_VERSION = 7  # include/vr/vr.h VR_ABI_VERSION
 _LIB = None
 
 
@@ -165,6 +178,13 @@ def lib() -> C.CDLL:
                                           C.POINTER(vp)]),
         "vr_release_external_memory": (C.c_int, [vp, vp]),
         "vr_debug_set_knob": (i32, [vp, i32, i32]),
+        "vr_debug_timing_member": (i32, [vp, i32, C.POINTER(vr_member_timing)]),
+        "vr_set_row_share": (i32, [vp, u32, u32]),
+        "vr_get_row_share": (i32, [vp, C.POINTER(u32), C.POINTER(u32)]),
+        "vr_shard_rows_ctx": (u32, [vp, u32, u32, u32]),
+        "vr_set_memory_budget": (i32, [vp, C.c_uint64]),
+        "vr_memory_report": (i32, [vp, C.POINTER(vr_memory_info)]),
+        "vr_prepare": (i32, [vp, C.POINTER(vr_camera), C.POINTER(vr_params)]),
         "vr_debug_get_knob": (i32, [vp, i32, C.POINTER(i32)]),
         "vr_cam_init": (None, [C.POINTER(vr_orbit_camera)]),
         "vr_cam_rotate": (None, [C.POINTER(vr_orbit_camera), f32, f32]),
@@ -514,6 +534,38 @@ class OffscreenPass:
 
     def kernel_name(self, params) -> str:
         return lib().vr_kernel_name(self._ctx, C.byref(params)).decode()
+
+    def timing_member(self, member: int) -> dict:
+        """vr_debug_timing_member: one device's summed kernel / render / gather / assembly ms."""
+        t = vr_member_timing()
+        self._check(lib().vr_debug_timing_member(self._ctx, member, C.byref(t)), "timing_member")
+        return dict(device=int(t.device), frames=int(t.frames), kernel_ms=float(t.kernel_ms),
+                    render_ms=float(t.render_ms), gather_ms=float(t.gather_ms),
+                    assemble_ms=float(t.assemble_ms))
+
+    # -- ABI 7: row shares, derived-structure memory, preparation --
+    def set_row_share(self, first_weight: int, other_weight: int):
+        self._check(lib().vr_set_row_share(self._ctx, first_weight, other_weight), "set_row_share")
+
+    def row_share(self):
+        a, b = C.c_uint32(), C.c_uint32()
+        self._check(lib().vr_get_row_share(self._ctx, C.byref(a), C.byref(b)), "row_share")
+        return int(a.value), int(b.value)
+
+    def shard_rows(self, height: int, row_block: int, nranks: int) -> int:
+        return int(lib().vr_shard_rows_ctx(self._ctx, height, row_block, nranks))
+
+    def set_memory_budget(self, nbytes: int):
+        self._check(lib().vr_set_memory_budget(self._ctx, C.c_uint64(nbytes)), "set_memory_budget")
+
+    def memory_report(self) -> dict:
+        m = vr_memory_info()
+        self._check(lib().vr_memory_report(self._ctx, C.byref(m)), "memory_report")
+        return {n: int(getattr(m, n)) for n, _ in vr_memory_info._fields_}
+
+    def prepare(self, camera, params):
+        cam = camera.to_vr_camera() if isinstance(camera, OrbitCamera) else camera
+        self._check(lib().vr_prepare(self._ctx, C.byref(cam), C.byref(params)), "prepare")
 
     # -- include/vr/vr_debug.h: launch-policy overrides for tests (speed only, never results) --
     def set_knob(self, name: str, value: int):

@@ -14,26 +14,51 @@ from __future__ import annotations
 import numpy as np
 
 
-def shard_rows(height: int, row_block: int, nranks: int) -> int:
-    blocks = (height + row_block - 1) // row_block
-    return ((blocks + nranks - 1) // nranks) * row_block
+def _blocks(nb: int, r: int, nranks: int, share) -> int:
+    """Blocks rank r owns among nb (vr_internal.h share_blocks)."""
+    w0, w = share
+    P = w0 + (nranks - 1) * w
+    q, o = divmod(nb, P)
+    wr, off = (w0, 0) if r == 0 else (w, w0 + (r - 1) * w)
+    return q * wr + (min(o - off, wr) if o > off else 0)
 
 
-def shard_global_rows(height: int, row_block: int, rank: int, nranks: int) -> np.ndarray:
+def shard_rows(height: int, row_block: int, nranks: int, share=(1, 1)) -> int:
+    """Rows of every rank's shard (the largest share; vr_shard_rows / vr_shard_rows_ctx)."""
+    nb = (height + row_block - 1) // row_block
+    return max(_blocks(nb, r, nranks, share) for r in range(min(nranks, 2))) * row_block
+
+
+def global_block(lb, rank: int, nranks: int, share=(1, 1)):
+    """Global block of rank's local block(s) lb (vr_internal.h share_global_block): per period of
+    w0 + (n - 1) w blocks rank 0 takes the first w0, rank r > 0 the w after w0 + (r - 1) w."""
+    w0, w = share
+    P = w0 + (nranks - 1) * w
+    wr, off = (w0, 0) if rank == 0 else (w, w0 + (rank - 1) * w)
+    return (lb // wr) * P + off + lb % wr
+
+
+def shard_global_rows(height: int, row_block: int, rank: int, nranks: int, share=(1, 1)) -> np.ndarray:
     """Global row of every local shard row (-1 for padding rows past the frame)."""
-    sr = shard_rows(height, row_block, nranks)
+    sr = shard_rows(height, row_block, nranks, share)
     ly = np.arange(sr)
     blk = ly // row_block
-    gy = (blk * nranks + rank) * row_block + ly % row_block
+    gy = global_block(blk, rank, nranks, share) * row_block + ly % row_block
     return np.where(gy < height, gy, -1)
 
 
-def assemble_numpy(gathered: np.ndarray, height: int, row_block: int, nranks: int) -> np.ndarray:
+def assemble_numpy(gathered: np.ndarray, height: int, row_block: int, nranks: int,
+                   share=(1, 1)) -> np.ndarray:
     """gathered: (nranks, shard_rows, W, ...) rank-major -> (height, W, ...) (vr_assemble_rows)."""
+    w0, w = share
+    P = w0 + (nranks - 1) * w
     y = np.arange(height)
     blk = y // row_block
-    rank = blk % nranks
-    ly = (blk // nranks) * row_block + y % row_block
+    q, o = blk // P, blk % P
+    first = o < w0
+    rank = np.where(first, 0, 1 + (o - w0) // w)
+    lb = np.where(first, q * w0 + o, q * w + (o - w0) % w)
+    ly = lb * row_block + y % row_block
     return gathered[rank, ly]
 
 
