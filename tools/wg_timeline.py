@@ -33,10 +33,11 @@ def timeline(lib, rp, cam, p, nranks, W, H, rb=8):
     lib.vr_debug_wg_times(None, 0, None, 1)
     rp.render_device(cam, p, out.data_ptr(), vr_amd.OUT_RGBA8, rb, 0, nranks, stream)
     torch.cuda.synchronize()
-    buf = (C.c_ulonglong * (2 * 131072))()
+    buf = (C.c_ulonglong * (4 * 131072))()
     n = C.c_uint(0)
     lib.vr_debug_wg_times(buf, 131072, C.byref(n), 0)
-    t = np.frombuffer(buf, dtype=np.uint64, count=2 * n.value).reshape(-1, 2).astype(np.int64)
+    # 4 words per workgroup: start, end, tile id, XCC_ID << 32 | HW_ID
+    t = np.frombuffer(buf, dtype=np.uint64, count=4 * n.value).reshape(-1, 4)[:, :2].astype(np.int64)
     t0 = t[:, 0].min()
     s, e = (t[:, 0] - t0) * 0.01, (t[:, 1] - t0) * 0.01  # us
     span = e.max()

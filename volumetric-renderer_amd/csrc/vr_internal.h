@@ -356,6 +356,13 @@ struct MarchParams {
     int32_t grad_half;
     float inv_range;        // RN(1 / range) (div_fast)
     uint32_t share_w0, share_w;  // RowShare of the row blocks over nranks
+    // tile_order 5 (march_queue_kernel): per-XCD strip lists in tile_perm (x + 8 j, per_xcd
+    // entries each, ~0 = none), queue heads (9 words, zero between launches), persistent grid
+    uint32_t *queue;
+    uint32_t per_xcd;
+    // bytes of the volume copy P.vol points at and of the output buffer (bounds-checking
+    // debug builds, -DVR_BOUNDS_CHECK: an out-of-range access is printed and skipped)
+    unsigned long long vol_bytes, out_bytes;
 };
 
 // Launchers (vr_kernels.hip).  All asynchronous on `stream`.

@@ -42,6 +42,21 @@ constexpr int kTfLut = 2 * (kTfLds + 2);  // float4s of the staged LUT (tf_looku
 
 __device__ __forceinline__ float lerpf(float a, float b, float w) { return fmaf(w, b - a, a); }
 
+// Bounds-checking debug builds (-DVR_BOUNDS_CHECK): an out-of-range index is printed (the first
+// 32 per process) and the access redirected to element 0.  Product builds compile it away.
+#ifdef VR_BOUNDS_CHECK
+__device__ unsigned int g_oob_reports;
+__device__ __noinline__ void oob_report(int what, unsigned long long a, unsigned long long b)
+{
+    if (atomicAdd(&g_oob_reports, 1u) < 32u)
+        printf("VR_OOB what=%d index=%llu limit=%llu block=%u thread=%u\n", what, a, b,
+               (unsigned)blockIdx.x, (unsigned)threadIdx.x);
+}
+#define VR_OOB(what, a, b) ((unsigned long long)(a) >= (unsigned long long)(b) ? (oob_report((what), (a), (b)), true) : false)
+#else
+#define VR_OOB(what, a, b) false
+#endif
+
 // Two independent lerps in one packed-FP32 pair (v_pk_add_f32 + v_pk_fma_f32): the same IEEE
 // operations per element as lerpf, so bit-identical to two scalar lerps.
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -258,8 +273,48 @@ struct CellRaw<VT, std::enable_if_t<kStencilWide<VT>>> {
 template <typename VT>
 struct CellRaw<VT, std::enable_if_t<kPlainByte<VT> && GeomByte::EX == 8>> {
     u4a q0, q1;    // slices z and z + 1: the 16 bytes from the 4-aligned address at or below e
-    uint32_t sh;   // e mod 4
+    uint32_t sh;   // e mod 4 (kShare: the cell's byte in its 8-byte row, 0..6)
+    uint32_t mode; // kShare: 0 own loads; 1 / 2 shared with the partner lane, which loaded
+                   // slice z + 1 / z (this lane's q0 holds the other slice)
 };
+
+// ---- cross-lane sharing of 8-bit cells (VR_U8_SHARE, pipelined plain-byte march) ----------
+// At the C4/C5 pixel spans (0.5-0.8 voxels per pixel) neighbouring lanes mostly sample cells in
+// the same brick row pair.  A lane pair whose cells share the row pair (y, y + 1) of one brick
+// issues ONE 16-B load each -- the two rows of slice z from one lane, of slice z + 1 from the
+// other, both from the 8-aligned row start -- instead of two each, and the lanes trade their
+// load through a cross-lane move before the filter: half the lanes' data returns through the
+// texture data path (TD, busy 0.93 of the C4 frame).  Pairs stay together in the march loop
+// until both rays end, so the partner is active at every exchange.  The cell's voxels and the
+// filter are the same: frames are identical.
+//   VR_U8_SHARE = 1: partners are x-neighbours l, l ^ 1 (DPP quad_perm);
+//   VR_U8_SHARE = 2: partners l, l ^ 32, x-neighbours by a 16x4 lane map with x = 2 (l & 7) +
+//                    (l >> 5), so a shared pair leaves lanes 32-63 (two whole quarter-waves)
+//                    out of its second load (v_permlane32_swap).
+#ifndef VR_U8_SHARE
+#define VR_U8_SHARE 0
+#endif
+template <typename VT>
+constexpr bool kShare = kPlainByte<VT> && GeomByte::EX == 8 && VR_U8_SHARE != 0;
+__device__ __forceinline__ uint32_t partner_u32(uint32_t v, uint32_t lane)
+{
+#if VR_U8_SHARE == 2
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return lane < 32 ? r[1] : r[0];
+#else
+    (void)lane;
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // l ^ 1
+#endif
+}
+__device__ __forceinline__ bool share_role(uint32_t lane)
+{
+    return VR_U8_SHARE == 2 ? lane >= 32 : (lane & 1) != 0;
+}
+// bytes x, x + 1 of an 8-byte row held as (lo, hi) (x <= 6), in the low 16 bits
+__device__ __forceinline__ uint32_t row_bytes(uint32_t lo, uint32_t hi, uint32_t x)
+{
+    return x < 4 ? __builtin_amdgcn_alignbyte(hi, lo, x) : hi >> (8 * (x - 4));
+}
 
 // the stencil copy with 16-B density loads keeps each row's x - 1 / x + 2 voxels for the
 // gradient (row r = dy + 2 dz)
@@ -860,7 +915,8 @@ __device__ __forceinline__ float4 tf_lookup(const float4 *lut, int n, float nf, 
     u = fminf(fmaxf(u, -1.0f), nf);
     const float f = floorf(u);
     const float w = u - f;
-    const int e = (int)f + 1;
+    int e = (int)f + 1;
+    if (VR_OOB(1, (unsigned long long)(long long)e, (unsigned long long)(n + 2))) e = 0;
     const float4 a = lut[2 * e], d = lut[2 * e + 1];
     return make_float4(fmaf(w, d.x, a.x), fmaf(w, d.y, a.y), fmaf(w, d.z, a.z),
                        fmaf(w, d.w, a.w));
@@ -898,11 +954,24 @@ __device__ __forceinline__ int wave_min_leap(int k)
 }
 
 #ifdef VR_WG_TIMES
-// Experiment builds: per-workgroup start/end wall clock (100 MHz) of the last march launch,
-// read by vr_debug_wg_times (tools/wg_timeline.py).
+// Experiment builds: per workgroup of the march launches since the last reset, 4 words: start
+// and end wall clock (100 MHz), the tile id, and (XCC_ID << 32 | HW_ID) from the hardware
+// registers (which XCD / SE / CU ran it); read by vr_debug_wg_times (tools/wg_timeline.py).
 constexpr uint32_t kWgTimesMax = 1u << 17;
-__device__ unsigned long long g_wg_times[2 * kWgTimesMax];
+__device__ unsigned long long g_wg_times[4 * kWgTimesMax];
 __device__ unsigned int g_wg_count;
+__device__ __forceinline__ void wg_times_record(unsigned long long t0, uint32_t tile)
+{
+    const unsigned int slot = atomicAdd(&g_wg_count, 1u);
+    if (slot < kWgTimesMax) {
+        const unsigned long long hw = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        const unsigned long long xcc = (unsigned)__builtin_amdgcn_s_getreg((3 << 11) | 20);
+        g_wg_times[4 * slot] = t0;
+        g_wg_times[4 * slot + 1] = (unsigned long long)wall_clock64();
+        g_wg_times[4 * slot + 2] = tile;
+        g_wg_times[4 * slot + 3] = (xcc << 32) | hw;
+    }
+}
 #endif
 
 // Occupancy floor (waves per SIMD): the shaded f32 kernel holds 2 x 16-B centre loads plus
@@ -953,7 +1022,9 @@ __device__ __forceinline__ bool block_tile(const MarchParams &P, uint32_t &tile_
 {
     const uint32_t nwg = gridDim.x, b = blockIdx.x;
     if (P.tile_perm) {  // adaptive order (launch_order_tiles)
+        if (VR_OOB(5, b, P.nperm)) return false;
         const uint32_t t = P.tile_perm[b];
+        if (t != 0xFFFFFFFFu && VR_OOB(6, t, P.tiles_x * P.tiles_y)) return false;
         tile_x = t % P.tiles_x;
         tile_y = t / P.tiles_x;
         return t != 0xFFFFFFFFu;
@@ -1037,33 +1108,31 @@ __device__ __forceinline__ void shade_sample(const MarchParams &P, const char *_
 // composited (two samples of the ray in flight).  For launches with few waves per CU (one
 // rank's share of a multi-GPU frame), where every wave's serial chain of memory round trips,
 // not the chip's throughput, sets the time.  Reference-semantics results are identical.
+// One wavefront's strip of a tile (wave index `wave` of the 16 x kMarchRows tile (tile_x,
+// tile_y)): every ray of it marched and its pixels written.  s_tf: the TF staged in LDS (when
+// tf_in_lds).  march_kernel runs one tile per workgroup; march_queue_kernel runs strips pulled
+// from a queue by each wavefront on its own.
 template <typename VT, bool SHADE, bool COUNT, bool SKIP, bool GF, bool PIPE>
-__global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, PIPE>)) void march_kernel(const MarchParams P)
+__device__ __forceinline__ void march_strip(const MarchParams &P, const float4 *s_tf,
+                                            bool tf_in_lds, uint32_t tile_x, uint32_t tile_y,
+                                            uint32_t wave, uint32_t lane)
 {
-    __shared__ float4 s_tf[kTfLut];  // {texel, difference to the next} pairs + sentinels
-    const int tid = threadIdx.x;
-
-    uint32_t tile_x, tile_y;
-    if (!block_tile(P, tile_x, tile_y)) return;
-    const long long wg_start = wall_clock64();
-#ifdef VR_WG_TIMES
-    const unsigned long long wg_t0 = wg_start;
-#endif
-
-    const bool tf_in_lds = P.tf_n <= kTfLds;
-    if (tf_in_lds)
-        for (int i = tid; i < 2 * (P.tf_n + 2); i += (int)kThreadsPerTile) s_tf[i] = P.tf[i];
-    __syncthreads();
     using G = GeomOf<VT>;
     const long by_stride = (long)P.nbx * G::Elems;  // elements between brick rows/slabs
     const long bz_stride = (long)P.nbx * P.nby * G::Elems;
 
     // wavefront -> (ww x wh) pixels, ww = 2^wave_w_shift, together tiling the 16 x kMarchRows tile
-    const uint32_t wave = tid >> 6, lane = tid & 63;
     const uint32_t ws = P.wave_w_shift, ww = 1u << ws, wh = 64u >> ws;
     const uint32_t wpr = kTile >> ws;  // wavefronts per tile row
-    const uint32_t px = tile_x * kTile + (wave % wpr) * ww + (lane & (ww - 1));
-    const uint32_t ly = tile_y * kMarchRows + (wave / wpr) * wh + (lane >> ws);
+    uint32_t lx_ = lane & (ww - 1), ly_ = lane >> ws;
+    if constexpr (kShare<VT> && PIPE && VR_U8_SHARE == 2) {
+        if (ws == 4) {  // 16x4: lanes l and l ^ 32 are x-neighbours
+            lx_ = ((lane & 7u) << 1) | (lane >> 5);
+            ly_ = (lane >> 3) & 3u;
+        }
+    }
+    const uint32_t px = tile_x * kTile + (wave % wpr) * ww + lx_;
+    const uint32_t ly = tile_y * kMarchRows + (wave / wpr) * wh + ly_;
     bool active = px < P.W && ly < P.local_rows;
     const uint32_t blk = ly / P.row_block;
     const uint32_t gy = share_global_block(blk, P.rank, P.nranks, RowShare{P.share_w0, P.share_w}) *
@@ -1124,7 +1193,43 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
             S.pj = j + kPad;
             S.pk = kk + kPad;
             S.ce = cell_offset<VT>(S.pi, S.pj, S.pk, P.nbx, P.nby);
-            Cell8<VT>::issue(S.w, vol, S.ce);
+            if (VR_OOB(3, S.ce * kElemBytes<VT>, P.vol_bytes)) S.ce = 0;
+            if constexpr (kShare<VT> && PIPE) {
+                // the cell's row pair (y, y + 1) of slice z starts at the 8-aligned row start
+                const uint32_t bx = (uint32_t)S.pi % (uint32_t)G::BX;
+                const size_t row = S.ce - bx;
+                const uint32_t plo = partner_u32((uint32_t)row, lane);
+                const uint32_t phi = partner_u32((uint32_t)(row >> 32), lane);
+                const uint32_t pslab = partner_u32(S.slab ? 1u : 0u, lane);
+                const bool shared = S.slab && pslab != 0u && plo == (uint32_t)row &&
+                                    phi == (uint32_t)(row >> 32);
+                const bool role = share_role(lane);
+                S.w.sh = bx;
+                S.w.mode = shared ? (role ? 2u : 1u) : 0u;
+                S.w.q0 = *reinterpret_cast<const u4a *>(vol + row + (shared && role ? G::Slice : 0));
+                if (!shared) S.w.q1 = *reinterpret_cast<const u4a *>(vol + row + G::Slice);
+            } else {
+                Cell8<VT>::issue(S.w, vol, S.ce);
+            }
+        };
+        // kShare: the exchange with the partner lane (every loop-active lane runs it) and the
+        // cell's 8 voxels from the row pairs of slices z and z + 1
+        auto decode_shared = [&](const Stage &S, Cell8<VT> &c) {
+            if constexpr (kShare<VT> && PIPE) {
+                const u4a o = {partner_u32(S.w.q0.x, lane), partner_u32(S.w.q0.y, lane),
+                               partner_u32(S.w.q0.z, lane), partner_u32(S.w.q0.w, lane)};
+                const u4a z0 = S.w.mode == 2u ? o : S.w.q0;
+                const u4a z1 = S.w.mode == 1u ? o : (S.w.mode == 2u ? S.w.q0 : S.w.q1);
+                const uint32_t q[4] = {row_bytes(z0.x, z0.y, S.w.sh), row_bytes(z0.z, z0.w, S.w.sh),
+                                       row_bytes(z1.x, z1.y, S.w.sh), row_bytes(z1.z, z1.w, S.w.sh)};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {  // r = dy + 2 dz
+                    c.v[2 * r] = byte_value<VT>(q[r], 0);
+                    c.v[2 * r + 1] = byte_value<VT>(q[r], 1);
+                }
+            } else {
+                c.decode(S.w);
+            }
         };
         auto composite = [&](const float4 &sm) -> bool {  // volume.frag:44-45
             cr = cr + (sm.x * sm.w) * T;
@@ -1155,10 +1260,8 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
             phong(P, gx, gy_, gz, d0, d1, d2, X.sm);
             return composite(X.sm);
         };
-        auto consume = [&](const Stage &S) -> bool {  // true: the ray ends (T == 0 or ERT)
+        auto consume_cell = [&](const Stage &S, const Cell8<VT> &c) -> bool {  // true: the ray ends
             if (kDefer && finish()) return true;
-            Cell8<VT> c;
-            c.decode(S.w);
             const float d = c.tri(S.ax, S.ay, S.az);
             const float tt = div_by_range(d - P.vmin, P);
             float4 sm = tf_lookup(s_tf, P.tf_n, P.tf_nf, tt);
@@ -1179,6 +1282,11 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
                                            bz_stride, S.ax, S.ay, S.az, d0, d1, d2, sm);
             return composite(sm);
         };
+        auto consume = [&](const Stage &S) -> bool {
+            Cell8<VT> c;
+            c.decode(S.w);
+            return consume_cell(S, c);
+        };
         auto advance = [&]() {
             p0 = p0 + d0 * P.step;
             p1 = p1 + d1 * P.step;
@@ -1186,14 +1294,36 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
         };
         Stage A, B;
         int k = 0;
-        prep(A, k);
-        while (A.ok) {  // ping-pong: no register copies between the two stages
-            advance();
-            prep(B, ++k);
-            if (consume(A) || !B.ok) break;
-            advance();
-            prep(A, ++k);
-            if (consume(B)) break;
+        if constexpr (kShare<VT>) {
+            // pairs leave together: a lane whose ray ended keeps stepping (stages not ok, dummy
+            // loads, nothing composited) until its partner's ray has ended too
+            prep(A, k);
+            bool done = !A.ok;
+            auto both_done = [&]() { return done && partner_u32(done ? 1u : 0u, lane) != 0u; };
+            if (!both_done())
+                for (;;) {
+                    advance();
+                    prep(B, ++k, !done);
+                    Cell8<VT> c;
+                    decode_shared(A, c);
+                    if (!done) done = consume_cell(A, c) || !B.ok;
+                    if (both_done()) break;
+                    advance();
+                    prep(A, ++k, !done);
+                    decode_shared(B, c);
+                    if (!done) done = consume_cell(B, c) || !A.ok;
+                    if (both_done()) break;
+                }
+        } else {
+            prep(A, k);
+            while (A.ok) {  // ping-pong: no register copies between the two stages
+                advance();
+                prep(B, ++k);
+                if (consume(A) || !B.ok) break;
+                advance();
+                prep(A, ++k);
+                if (consume(B)) break;
+            }
         }
         finish();  // deferred shading: the sample still held when the ray left the volume
     } else
@@ -1262,7 +1392,8 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
                     it += k;
                 }
             } else {
-                const size_t ce = cell_offset<VT>(pi, pj, pk, P.nbx, P.nby);
+                size_t ce = cell_offset<VT>(pi, pj, pk, P.nbx, P.nby);
+                if (VR_OOB(2, ce * kElemBytes<VT>, P.vol_bytes)) ce = 0;
                 Cell8<VT> c;
                 c.load(vol, ce);
                 const float d = c.tri(ax, ay, az);
@@ -1307,22 +1438,6 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
             atomicAdd(&P.counters[4], sk);
         }
     }
-    if (P.tile_cost) {  // adaptive order: this tile's duration for the next launch
-        __syncthreads();
-        if (tid == 0)
-            P.tile_cost[tile_y * P.tiles_x + tile_x] =
-                (uint32_t)min(wall_clock64() - wg_start, 0x7FFFFFFFLL);
-    }
-#ifdef VR_WG_TIMES
-    __syncthreads();
-    if (tid == 0) {
-        const unsigned int slot = atomicAdd(&g_wg_count, 1u);
-        if (slot < kWgTimesMax) {
-            g_wg_times[2 * slot] = (unsigned long long)wg_t0;
-            g_wg_times[2 * slot + 1] = (unsigned long long)wall_clock64();
-        }
-    }
-#endif
     if (!active) return;
 
     // volume.frag:50 + blend (offscreen_pass.cpp:715-725); uncovered: T = 1, C = 0 -> clear
@@ -1333,11 +1448,92 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
     const float o2 = cb * A + P.clear[2] * omA;
     const float o3 = A * A + P.clear[3] * omA;
     const size_t idx = (size_t)ly * P.W + px;
+    if (VR_OOB(4, idx * (P.out_format == 0 ? 4 : 16), P.out_bytes)) return;
     if (P.out_format == 0) {
         static_cast<uint32_t *>(P.out)[idx] =
             unorm8(o0) | (unorm8(o1) << 8) | (unorm8(o2) << 16) | (unorm8(o3) << 24);
     } else {
         static_cast<float4 *>(P.out)[idx] = make_float4(o0, o1, o2, o3);
+    }
+}
+
+template <typename VT, bool SHADE, bool COUNT, bool SKIP, bool GF, bool PIPE>
+__global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, PIPE>)) void march_kernel(const MarchParams P)
+{
+    __shared__ float4 s_tf[kTfLut];  // {texel, difference to the next} pairs + sentinels
+    const int tid = threadIdx.x;
+
+    uint32_t tile_x, tile_y;
+    if (!block_tile(P, tile_x, tile_y)) return;
+    const long long wg_start = wall_clock64();
+
+    const bool tf_in_lds = P.tf_n <= kTfLds;
+    if (tf_in_lds)
+        for (int i = tid; i < 2 * (P.tf_n + 2); i += (int)kThreadsPerTile) s_tf[i] = P.tf[i];
+    __syncthreads();
+    march_strip<VT, SHADE, COUNT, SKIP, GF, PIPE>(P, s_tf, tf_in_lds, tile_x, tile_y,
+                                                  (uint32_t)tid >> 6, (uint32_t)tid & 63u);
+    if (P.tile_cost) {  // adaptive order: this tile's duration for the next launch
+        __syncthreads();
+        if (tid == 0)
+            P.tile_cost[tile_y * P.tiles_x + tile_x] =
+                (uint32_t)min(wall_clock64() - wg_start, 0x7FFFFFFFLL);
+    }
+#ifdef VR_WG_TIMES
+    __syncthreads();
+    if (tid == 0) wg_times_record((unsigned long long)wg_start, tile_y * P.tiles_x + tile_x);
+#endif
+}
+
+// ---- wavefront work queue (tile_order 5) -------------------------------------------------------
+// A persistent grid (as many workgroups as fit the chip at once): every wavefront pulls strips
+// (one wavefront's 16x4 part of a tile) from its XCD's list, longest first by the strips' last
+// recorded durations (order_tiles_kernel over strip lists), and when that list is empty steals
+// from the other XCDs' lists.  A workgroup never waits for its slowest wavefront (tiles of a
+// sparse view mix long and short strips), the strips at a list's end are the shortest, and an
+// XCD that runs out of work takes another's: the frame's tail shrinks to the longest strip.
+// Queue heads: P.queue[0..7] (one per XCD list), P.queue[8] counts finished wavefronts; the last
+// one resets all nine for the next launch on the stream (stream order: the next launch starts
+// after this one has finished).  Same strips, same rays, same operations: frames are identical.
+template <typename VT, bool SHADE, bool GF, bool PIPE>
+__global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<false, false, GF, PIPE>)) void
+march_queue_kernel(const MarchParams P)
+{
+    __shared__ float4 s_tf[kTfLut];
+    const int tid = threadIdx.x;
+    const bool tf_in_lds = P.tf_n <= kTfLds;
+    if (tf_in_lds)
+        for (int i = tid; i < 2 * (P.tf_n + 2); i += (int)kThreadsPerTile) s_tf[i] = P.tf[i];
+    __syncthreads();
+    const uint32_t lane = (uint32_t)tid & 63u;
+    const uint32_t wpt = kThreadsPerTile / 64;  // strips per tile
+    // the XCD this wavefront runs on (HW_REG_XCC_ID): its own list first
+    uint32_t x = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;
+    for (uint32_t tried = 0; tried < 8;) {
+        uint32_t j = 0;
+        if (lane == 0) j = atomicAdd(&P.queue[x], 1u);
+        j = (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
+        const uint32_t strip = j < P.per_xcd ? P.tile_perm[x + 8 * j] : 0xFFFFFFFFu;
+        if (strip == 0xFFFFFFFFu) {  // this list is done: the next XCD's
+            x = (x + 1) & 7u;
+            ++tried;
+            continue;
+        }
+        const long long t0 = wall_clock64();
+        const uint32_t tile = strip / wpt;
+        march_strip<VT, SHADE, false, false, GF, PIPE>(P, s_tf, tf_in_lds, tile % P.tiles_x,
+                                                       tile / P.tiles_x, strip % wpt, lane);
+        if (P.tile_cost && lane == 0)
+            P.tile_cost[strip] = (uint32_t)min(wall_clock64() - t0, 0x7FFFFFFFLL);
+#ifdef VR_WG_TIMES
+        if (lane == 0) wg_times_record((unsigned long long)t0, strip);
+#endif
+    }
+    if (lane == 0) {
+        const uint32_t done = atomicAdd(&P.queue[8], 1u);
+        if (done + 1 == gridDim.x * wpt) {  // the last wavefront: reset the heads
+            for (int q = 0; q < 9; ++q) atomicExch(&P.queue[q], 0u);
+        }
     }
 }
 
@@ -1465,13 +1661,7 @@ __global__ __launch_bounds__(kThreads) void march_pair_kernel(const MarchParams 
     }
 #ifdef VR_WG_TIMES
     __syncthreads();
-    if (tid == 0) {
-        const unsigned int slot = atomicAdd(&g_wg_count, 1u);
-        if (slot < kWgTimesMax) {
-            g_wg_times[2 * slot] = (unsigned long long)wg_t0;
-            g_wg_times[2 * slot + 1] = (unsigned long long)wall_clock64();
-        }
-    }
+    if (tid == 0) wg_times_record((unsigned long long)wg_t0, tile_y * P.tiles_x + tile_x);
 #endif
     if (!active || half) return;
     const float A = 1.0f - T;  // volume.frag:50 + blend (offscreen_pass.cpp:715-725)
@@ -1940,6 +2130,26 @@ __global__ __launch_bounds__(256) void assemble_kernel(const PixT *__restrict__ 
 template <typename VT, bool SHADE, bool COUNT, bool SKIP, bool GF = false, bool PIPE = false>
 hipError_t launch_march_t(const MarchParams &p, hipStream_t stream)
 {
+    if constexpr (!COUNT && !SKIP) {
+        if (p.queue) {  // tile_order 5: the persistent wavefront queue (host: a strip permutation)
+            if (p.tiles_x * p.tiles_y == 0) return hipSuccess;
+            // as many workgroups as the chip holds at once (occupancy x CUs), once per variant
+            static unsigned grid = 0;
+            if (grid == 0) {
+                int per_cu = 0, dev = 0, cus = 0;
+                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                        &per_cu, march_queue_kernel<VT, SHADE, GF, PIPE>, kThreadsPerTile, 0) != hipSuccess ||
+                    hipGetDevice(&dev) != hipSuccess ||
+                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                    per_cu <= 0 || cus <= 0)
+                    return hipErrorInvalidValue;
+                grid = (unsigned)(per_cu * cus);
+            }
+            hipLaunchKernelGGL((march_queue_kernel<VT, SHADE, GF, PIPE>), dim3(grid),
+                               dim3(kThreadsPerTile), 0, stream, p);
+            return hipGetLastError();
+        }
+    }
     const uint32_t nblocks = p.tile_perm ? p.nperm
                              : p.tile_order >= 3 ? ((p.supers_total + 7) / 8) * 8 * kSuper * kSuper
                                                  : p.tiles_x * p.tiles_y;
@@ -2297,7 +2507,7 @@ hipError_t debug_wg_times_read(unsigned long long *out, unsigned int max, unsign
     n = n < kWgTimesMax ? n : kWgTimesMax;
     n = n < max ? n : max;
     *count = n;
-    return n ? hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_times), 2 * n * sizeof(unsigned long long))
+    return n ? hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_times), 4 * n * sizeof(unsigned long long))
              : hipSuccess;
 }
 #endif
