@@ -1,5 +1,5 @@
 set -o pipefail
-O=gpurun_out/r04_e1b; mkdir -p $O
+O=gpurun_out/r04_e1c; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log

@@ -908,7 +908,16 @@ __device__ __forceinline__ float div_by_range(float x, const MarchParams &P)
 // floor(u) = i0 lies in [-1, n] and lerp(c_i0, c_i1, w) = fma(w, d, c) is one fma per channel
 // with no index clamp: below the first texel centre (i0 = -1) and at u = n the sentinel's
 // difference 0 returns the edge texel for any w.  NaN t clamps to u = -1 (texel 0).
-__device__ __forceinline__ float4 tf_lookup(const float4 *lut, int n, float nf, float t)
+// The LUT is read through an LDS-typed pointer (LdsF4) when staged, a global one otherwise:
+// never through a generic pointer chosen between the two.  (With one generic pointer the
+// compiler merged both lookups into FLAT loads and folded the +1 texel offset into the
+// instruction offset; for u < 0 (texel -1, the low sentinel) the base then sat 32 B below the
+// LDS aperture, the access was routed as a global one to the aperture's base address, and the
+// launch faulted with MEMORY_APERTURE_VIOLATION.)
+typedef float F4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const F4v LdsF4;
+template <typename Lut>
+__device__ __forceinline__ float4 tf_lookup(Lut *lut, int n, float nf, float t)
 {
     (void)n;
     float u = t * nf - 0.5f;
@@ -917,7 +926,7 @@ __device__ __forceinline__ float4 tf_lookup(const float4 *lut, int n, float nf, 
     const float w = u - f;
     int e = (int)f + 1;
     if (VR_OOB(1, (unsigned long long)(long long)e, (unsigned long long)(n + 2))) e = 0;
-    const float4 a = lut[2 * e], d = lut[2 * e + 1];
+    const auto a = lut[2 * e], d = lut[2 * e + 1];
     return make_float4(fmaf(w, d.x, a.x), fmaf(w, d.y, a.y), fmaf(w, d.z, a.z),
                        fmaf(w, d.w, a.w));
 }
@@ -1113,7 +1122,7 @@ __device__ __forceinline__ void shade_sample(const MarchParams &P, const char *_
 // tf_in_lds).  march_kernel runs one tile per workgroup; march_queue_kernel runs strips pulled
 // from a queue by each wavefront on its own.
 template <typename VT, bool SHADE, bool COUNT, bool SKIP, bool GF, bool PIPE>
-__device__ __forceinline__ void march_strip(const MarchParams &P, const float4 *s_tf,
+__device__ __forceinline__ void march_strip(const MarchParams &P, LdsF4 *s_tf,
                                             bool tf_in_lds, uint32_t tile_x, uint32_t tile_y,
                                             uint32_t wave, uint32_t lane)
 {
@@ -1471,7 +1480,7 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
     if (tf_in_lds)
         for (int i = tid; i < 2 * (P.tf_n + 2); i += (int)kThreadsPerTile) s_tf[i] = P.tf[i];
     __syncthreads();
-    march_strip<VT, SHADE, COUNT, SKIP, GF, PIPE>(P, s_tf, tf_in_lds, tile_x, tile_y,
+    march_strip<VT, SHADE, COUNT, SKIP, GF, PIPE>(P, (LdsF4 *)s_tf, tf_in_lds, tile_x, tile_y,
                                                   (uint32_t)tid >> 6, (uint32_t)tid & 63u);
     if (P.tile_cost) {  // adaptive order: this tile's duration for the next launch
         __syncthreads();
@@ -1521,7 +1530,7 @@ march_queue_kernel(const MarchParams P)
         }
         const long long t0 = wall_clock64();
         const uint32_t tile = strip / wpt;
-        march_strip<VT, SHADE, false, false, GF, PIPE>(P, s_tf, tf_in_lds, tile % P.tiles_x,
+        march_strip<VT, SHADE, false, false, GF, PIPE>(P, (LdsF4 *)s_tf, tf_in_lds, tile % P.tiles_x,
                                                        tile / P.tiles_x, strip % wpt, lane);
         if (P.tile_cost && lane == 0)
             P.tile_cost[strip] = (uint32_t)min(wall_clock64() - t0, 0x7FFFFFFFLL);
@@ -1615,7 +1624,7 @@ __global__ __launch_bounds__(kThreads) void march_pair_kernel(const MarchParams 
     // this lane's sample -> exchange -> the pair's two samples composited in order; true: the
     // ray ends (bounds, nsteps, T == 0 or ERT), identically in both lanes
     auto consume = [&](const Stage &S) -> bool {
-        float4 sm = tf_lookup(s_tf, P.tf_n, P.tf_nf,
+        float4 sm = tf_lookup((LdsF4 *)s_tf, P.tf_n, P.tf_nf,
                               div_by_range(S.c.tri(S.ax, S.ay, S.az) - P.vmin, P));
         if (!S.slab) sm.w = 0.0f;
         if (SHADE && sm.w > 0.0f)
