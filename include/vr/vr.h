@@ -264,7 +264,11 @@ int vr_assemble_rows(vr_ctx *ctx, const void *gathered_dev, void *out_dev, int o
  * `offset` of it on the context's device (the lowest device of a vr_create_mask context).
  * *dev_ptr can be passed to vr_render_device.  The caller keeps `fd`: neither call closes it
  * (measured on ROCm 7.2: the descriptor is still open after the release), so close it after
- * vr_release_external_memory.  Release the mapping before the exporter frees the memory. */
+ * vr_release_external_memory.  Release the mapping before the exporter frees the memory.
+ * The import describes the whole exported allocation as `offset + size` bytes (the HIP import
+ * descriptor's size): pass offset + size == the exporter's allocation size (Vulkan
+ * VkMemoryAllocateInfo::allocationSize), i.e. map the window that runs to the allocation's
+ * end; a smaller window of a larger allocation may fail to import on some drivers. */
 typedef struct vr_external_memory vr_external_memory;
 int vr_import_memory_fd(vr_ctx *ctx, int fd, uint64_t size, uint64_t offset,
                         vr_external_memory **mem, void **dev_ptr);

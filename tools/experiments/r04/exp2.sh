@@ -1,5 +1,5 @@
-# u8 cross-lane sharing A/B (C4: 1024^3 u8 @ 2048^2), alternating builds, 2 rounds, then the
-# GPU suite on the share builds (bit-identity) -- round 4
+# round 4: u8 cross-lane sharing A/B (C4: 1024^3 u8 @ 2048^2), alternating builds, 2 rounds;
+# TD/TCP counters per build on the C4 bench; the GPU parity files on the share builds
 set -o pipefail
 O=gpurun_out/r04_e2; mkdir -p $O
 export TMPDIR=/tmp
@@ -9,6 +9,14 @@ for r in 1 2; do
   done
 done
 cat $O/u8_ab.jsonl
+for b in lib lib_share1 lib_share2; do
+  i=0
+  for G in "TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_GUI_ACTIVE" "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum" "SQ_INSTS_VMEM_RD SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES"; do
+    i=$((i+1))
+    VR_AMD_LIB=$PWD/volumetric-renderer_amd/$b/libvr_amd.so timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $G -d $O/pmc_$b/p$i -o run --output-format csv -- python3 bench.py --config c4 --no-variants --no-cpu-baseline --steps 10 --warmup 3 > $O/pmc_${b}_p$i.log 2>&1 || exit 1
+  done
+done
+python tools/pmc_report.py $O/pmc_lib > $O/pmc_lib.txt 2>&1; python tools/pmc_report.py $O/pmc_lib_share1 > $O/pmc_lib_share1.txt 2>&1; python tools/pmc_report.py $O/pmc_lib_share2 > $O/pmc_lib_share2.txt 2>&1
 for b in lib_share1 lib_share2; do
   VR_AMD_LIB=$PWD/volumetric-renderer_amd/$b/libvr_amd.so timeout -k 10 400 python -u -m pytest tests/test_gpu_random.py tests/test_gpu_fullsize.py tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_$b.log 2>&1; echo "$b rc=$?"; tail -2 $O/pytest_$b.log
 done

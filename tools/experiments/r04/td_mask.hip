@@ -1,13 +1,15 @@
-// td_mask.hip — does the vector-memory data return (TA/TD) cost scale with the active lanes of
-// a load, and with its width?  (round 4, u8 cross-lane sharing design)
+// td_mask.hip — what does a wave-level global load cost in the vector-memory path (TA/TD/TCP),
+// as a function of its active lanes, its width and its address footprint?  (round 4: the u8
+// cross-lane sharing design, and the meaning of TCP_TOTAL_CACHE_ACCESSES per load on C3)
 //
 // Each wave issues ITER global loads from a 16 KiB table that stays in L1, so the loop is
-// bound by the address/data path (TA/TD), not by L2 or HBM.  Patterns of active lanes per load:
-//   0 all 64 lanes, 1 even lanes (32), 2 lanes 0-31 (two whole quarter-waves idle),
-//   3 lanes 0-15 (one quarter-wave), 4 every 4th lane (16, spread over all quarter-waves)
-// and widths 4, 8, 16 B per lane.  Lane l reads 16 B at (l * 16 + it * 1024) mod 16 KiB: every
-// wave-level load touches 8 consecutive 128-B lines when all lanes are active.
-// Build: hipcc --offload-arch=gfx950 -O3 -o td_mask td_mask.hip ; run: ./td_mask  (prints JSON)
+// bound by the address/data path, not by L2 or HBM.  Case = (width, lane stride, active lanes):
+//   lane l reads WIDTH bytes at (l * STRIDE + it * 1024 + block * 64) mod 16 KiB;
+//   active lanes: 0 all 64, 1 even lanes (32), 2 lanes 0-31 (two whole quarter-waves idle),
+//   3 lanes 0-15 (one quarter-wave), 4 every 4th lane (16, spread over all quarter-waves).
+// The cases run in the order printed, each launched twice (warm, timed): under rocprofv3 --pmc
+// the timed launch of case k is dispatch 2k + 1 (tools/experiments/r04/td_pmc.py reads them).
+// Build: hipcc --offload-arch=gfx950 -O3 -o td_mask td_mask.hip ; run: ./td_mask (prints JSON)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -15,7 +17,7 @@
 typedef unsigned u4 __attribute__((ext_vector_type(4)));
 typedef unsigned u2 __attribute__((ext_vector_type(2)));
 
-template <int WIDTH, int PATTERN>
+template <int WIDTH, int STRIDE, int PATTERN>
 __global__ __launch_bounds__(256) void td_kernel(const unsigned *__restrict__ tab, unsigned *out, int iters)
 {
     const unsigned lane = threadIdx.x & 63;
@@ -30,7 +32,7 @@ __global__ __launch_bounds__(256) void td_kernel(const unsigned *__restrict__ ta
     unsigned acc = 0;
     const char *base = reinterpret_cast<const char *>(tab);
     for (int it = 0; it < iters; ++it) {
-        const unsigned off = (lane * 16 + (unsigned)it * 1024 + blockIdx.x * 64) & (16384 - 1);
+        const unsigned off = (lane * STRIDE + (unsigned)it * 1024 + blockIdx.x * 64) & (16384 - 1);
         if (on) {
             if constexpr (WIDTH == 16) {
                 const u4 v = *reinterpret_cast<const u4 *>(base + off);
@@ -46,23 +48,28 @@ __global__ __launch_bounds__(256) void td_kernel(const unsigned *__restrict__ ta
     if (acc == 0x12345678u) out[blockIdx.x] = acc;  // keeps the loads
 }
 
-template <int WIDTH, int PATTERN>
-float run(const unsigned *tab, unsigned *out, int iters)
+constexpr int kBlocks = 256 * 8;  // 8 workgroups of 4 waves per CU
+constexpr int kIters = 4096;
+
+template <int WIDTH, int STRIDE, int PATTERN>
+void run(const unsigned *tab, unsigned *out, const char *name, bool last)
 {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    const int blocks = 256 * 8;  // 8 workgroups of 4 waves per CU
-    hipLaunchKernelGGL((td_kernel<WIDTH, PATTERN>), dim3(blocks), dim3(256), 0, 0, tab, out, iters);
+    hipLaunchKernelGGL((td_kernel<WIDTH, STRIDE, PATTERN>), dim3(kBlocks), dim3(256), 0, 0, tab, out, kIters);
     hipEventRecord(a);
-    hipLaunchKernelGGL((td_kernel<WIDTH, PATTERN>), dim3(blocks), dim3(256), 0, 0, tab, out, iters);
+    hipLaunchKernelGGL((td_kernel<WIDTH, STRIDE, PATTERN>), dim3(kBlocks), dim3(256), 0, 0, tab, out, kIters);
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms = 0.0f;
     hipEventElapsedTime(&ms, a, b);
     hipEventDestroy(a);
     hipEventDestroy(b);
-    return ms;
+    const double wave_loads_per_cu = (double)kBlocks * 4 * kIters / 256.0;
+    std::printf("  {\"case\": \"%s\", \"width\": %d, \"stride\": %d, \"pattern\": %d, "
+                "\"ns_per_wave_load_per_cu\": %.4f}%s\n",
+                name, WIDTH, STRIDE, PATTERN, ms * 1e6 / wave_loads_per_cu, last ? "" : ",");
 }
 
 int main()
@@ -71,28 +78,26 @@ int main()
     hipMalloc(&tab, 16384);
     hipMalloc(&out, 1 << 20);
     hipMemset(tab, 1, 16384);
-    const int iters = 4096;
-    const double loads = 256.0 * 8 * 4 * iters;  // wave-level loads per launch
-    std::printf("{\"iters\": %d, \"wave_loads\": %.0f, \"ns_per_wave_load_per_cu\": {\n", iters, loads);
-    const char *pn[5] = {"all64", "even32", "lo32", "lo16", "every4th"};
-    float t[3][5];
-    t[0][0] = run<16, 0>(tab, out, iters); t[0][1] = run<16, 1>(tab, out, iters);
-    t[0][2] = run<16, 2>(tab, out, iters); t[0][3] = run<16, 3>(tab, out, iters);
-    t[0][4] = run<16, 4>(tab, out, iters);
-    t[1][0] = run<8, 0>(tab, out, iters); t[1][1] = run<8, 1>(tab, out, iters);
-    t[1][2] = run<8, 2>(tab, out, iters); t[1][3] = run<8, 3>(tab, out, iters);
-    t[1][4] = run<8, 4>(tab, out, iters);
-    t[2][0] = run<4, 0>(tab, out, iters); t[2][1] = run<4, 1>(tab, out, iters);
-    t[2][2] = run<4, 2>(tab, out, iters); t[2][3] = run<4, 3>(tab, out, iters);
-    t[2][4] = run<4, 4>(tab, out, iters);
-    const int w[3] = {16, 8, 4};
-    for (int i = 0; i < 3; ++i) {
-        std::printf("  \"w%d\": {", w[i]);
-        for (int p = 0; p < 5; ++p)
-            std::printf("\"%s\": %.3f%s", pn[p], t[i][p] * 1e6 / (loads / 256.0), p < 4 ? ", " : "");
-        std::printf("}%s\n", i < 2 ? "," : "");
-    }
-    std::printf("}}\n");
+    std::printf("{\"iters\": %d, \"wave_loads\": %.0f, \"cases\": [\n", kIters, (double)kBlocks * 4 * kIters);
+    // active-lane patterns (contiguous 16-B lanes: 8 lines per full wave)
+    run<16, 16, 0>(tab, out, "w16 all64", false);
+    run<16, 16, 1>(tab, out, "w16 even32", false);
+    run<16, 16, 2>(tab, out, "w16 lo32", false);
+    run<16, 16, 3>(tab, out, "w16 lo16", false);
+    run<16, 16, 4>(tab, out, "w16 every4th", false);
+    run<8, 16, 0>(tab, out, "w8 all64 (16-B stride)", false);
+    run<8, 16, 1>(tab, out, "w8 even32", false);
+    run<8, 16, 2>(tab, out, "w8 lo32", false);
+    run<4, 16, 0>(tab, out, "w4 all64 (16-B stride)", false);
+    // address footprint at full occupancy: how TCP counts accesses per wave-level load
+    run<16, 0, 0>(tab, out, "w16 broadcast (1 address)", false);
+    run<4, 4, 0>(tab, out, "w4 contiguous (256 B: 2 lines)", false);
+    run<8, 8, 0>(tab, out, "w8 contiguous (512 B: 4 lines)", false);
+    run<16, 32, 0>(tab, out, "w16 stride 32 (2 KiB: 16 lines)", false);
+    run<16, 64, 0>(tab, out, "w16 stride 64 (4 KiB: 32 lines)", false);
+    run<16, 128, 0>(tab, out, "w16 stride 128 (64 lines)", false);
+    run<4, 128, 0>(tab, out, "w4 stride 128 (64 lines)", true);
+    std::printf("]}\n");
     hipFree(tab);
     hipFree(out);
     return 0;

@@ -220,3 +220,66 @@ def views_u8(n=256, ntiles=60, W=1024, H=1024):
             r = simulate(fn, n, 1, list(vc.view), list(vc.position), W=W, H=H, ntiles=ntiles, tile=(16, 4))
             print(f"{cname:13s} {lname:28s} x{foot:.2f}  lines/instr {r['lines_per_instr']:6.2f}  "
                   f"lines/sample {r['lines_per_sample']:.3f}", flush=True)
+
+
+# ---- round 4: what TCP counts per wave-level load, and lane-pair sharing ---------------------
+def tcp_counts(addr, width, lanes_on=None, sector=64, line=128):
+    """For one wave-level load (64 lane addresses, `width` bytes each): three candidate counts
+    of TCP_TOTAL_CACHE_ACCESSES -- distinct 128-B lines of the wave (H0), distinct lines per
+    quarter-wave summed (H2), distinct 64-B sectors per quarter-wave summed (H1)."""
+    a = np.asarray(addr)
+    on = np.ones(len(a), bool) if lanes_on is None else np.asarray(lanes_on)
+    first_l, last_l = a // line, (a + width - 1) // line
+    first_s, last_s = a // sector, (a + width - 1) // sector
+    h0 = len(np.unique(np.concatenate([first_l[on], last_l[on]])))
+    h1 = h2 = 0
+    for q in range(4):
+        m = on.copy()
+        m[:] = False
+        m[q * 16:(q + 1) * 16] = on[q * 16:(q + 1) * 16]
+        if m.any():
+            h2 += len(np.unique(np.concatenate([first_l[m], last_l[m]])))
+            h1 += len(np.unique(np.concatenate([first_s[m], last_s[m]])))
+    return h0, h1, h2
+
+
+def tcp_model(view_name="fill", n=512, W=1920, H=1080, ntiles=40, seed=0, vb=4):
+    """C3's density gathers (f32 z-pairs in 8^3 bricks, 16x4 wavefronts, 2 x 16-B loads per
+    sample) under the three counting hypotheses, and the share of x-neighbour lane pairs
+    (l, l ^ 1) whose cells are the same cell (VR_F32_SHARE) or in the same row pair of a brick
+    (the 8-bit plain layout's VR_U8_SHARE=1 criterion)."""
+    sys.path.insert(0, os.path.join(ROOT, "volumetric-renderer_amd"))
+    import synth
+    vc = synth.camera(view_name).to_vr_camera()
+    view, pos = list(vc.view), list(vc.position)
+    layout = brick_apron_zpair(8, vb)
+    rng = np.random.default_rng(seed)
+    nb = (n + 3) // 4 + 1
+    tw, th = 16, 4
+    tot = np.zeros(3)
+    loads = 0
+    pairs = same_cell = 0
+    tiles = 0
+    while tiles < ntiles:
+        tx, ty = rng.integers(0, W // tw), rng.integers(0, H // th)
+        px, py = np.meshgrid(np.arange(tw) + tx * tw, np.arange(th) + ty * th)
+        ok, pos0, dirs = rays(view, pos, W, H, px.ravel().astype(float), py.ravel().astype(float))
+        if ok.sum() < 64:
+            continue
+        tiles += 1
+        p = pos0.copy()
+        for _ in range(360):
+            inside = np.all((p >= 0) & (p <= 1), axis=1)
+            if not inside.all():
+                break
+            i0 = np.floor(p * n - 0.5).astype(np.int64)
+            for addr, width in layout(i0[:, 0], i0[:, 1], i0[:, 2], nb):
+                tot += tcp_counts(addr, width)
+                loads += 1
+            cell = (i0[:, 2] * (n + 8) + i0[:, 1]) * (n + 8) + i0[:, 0]
+            pairs += 32
+            same_cell += int((cell[0::2] == cell[1::2]).sum())
+            p = p + dirs * 0.005
+    return dict(view=view_name, wave_loads=loads, h0_lines_per_wave=tot[0] / loads,
+                h1_sectors_per_quarter=tot[1] / loads, h2_lines_per_quarter=tot[2] / loads,
+                pair_same_cell=same_cell / max(1, pairs))

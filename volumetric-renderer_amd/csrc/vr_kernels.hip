@@ -265,6 +265,8 @@ struct CellRaw {  // generic: the decoded cell itself (loaded and decoded togeth
 template <typename VT>
 struct CellRaw<VT, std::enable_if_t<kZPair<VT> && !kPlainF32<VT>>> {
     f4a r0, r1;  // rows y and y + 1: elements x, x + 1 as z-pairs
+    uint32_t mode;  // kShareF: 0 own loads; 1 / 2 the partner lane loaded row y + 1 / y (r0
+                    // holds this lane's row)
 };
 template <typename VT>
 struct CellRaw<VT, std::enable_if_t<kStencilWide<VT>>> {
@@ -296,6 +298,17 @@ struct CellRaw<VT, std::enable_if_t<kPlainByte<VT> && GeomByte::EX == 8>> {
 #endif
 template <typename VT>
 constexpr bool kShare = kPlainByte<VT> && GeomByte::EX == 8 && VR_U8_SHARE != 0;
+// VR_F32_SHARE = 1: the same for f32 z-pair cells (x-neighbour lanes l, l ^ 1): a lane pair
+// whose two cells are the same cell loads row y in one lane and row y + 1 in the other and
+// trades them (4 DPP moves), instead of two 16-B loads in each lane.
+#ifndef VR_F32_SHARE
+#define VR_F32_SHARE 0
+#endif
+template <typename VT>
+constexpr bool kShareF = kZPair<VT> && !kPlainF32<VT> && VR_F32_SHARE != 0;
+// the march loop keeps partner lanes stepping together (both rays ended before either leaves)
+template <typename VT>
+constexpr bool kPairStep = kShare<VT> || kShareF<VT>;
 __device__ __forceinline__ uint32_t partner_u32(uint32_t v, uint32_t lane)
 {
 #if VR_U8_SHARE == 2
@@ -1217,6 +1230,16 @@ __device__ __forceinline__ void march_strip(const MarchParams &P, LdsF4 *s_tf,
                 S.w.mode = shared ? (role ? 2u : 1u) : 0u;
                 S.w.q0 = *reinterpret_cast<const u4a *>(vol + row + (shared && role ? G::Slice : 0));
                 if (!shared) S.w.q1 = *reinterpret_cast<const u4a *>(vol + row + G::Slice);
+            } else if constexpr (kShareF<VT> && PIPE) {
+                const uint32_t clo = (uint32_t)S.ce, chi = (uint32_t)(S.ce >> 32);
+                const uint32_t plo = partner_u32(clo, lane);
+                const uint32_t phi = partner_u32(chi, lane);
+                const uint32_t pslab = partner_u32(S.slab ? 1u : 0u, lane);
+                const bool shared = S.slab && pslab != 0u && plo == clo && phi == chi;
+                const bool role = share_role(lane);
+                S.w.mode = shared ? (role ? 2u : 1u) : 0u;
+                S.w.r0 = zpair_load2(vol, S.ce + (shared && role ? (size_t)G::Row : 0));
+                if (!shared) S.w.r1 = zpair_load2(vol, S.ce + G::Row);
             } else {
                 Cell8<VT>::issue(S.w, vol, S.ce);
             }
@@ -1236,6 +1259,15 @@ __device__ __forceinline__ void march_strip(const MarchParams &P, LdsF4 *s_tf,
                     c.v[2 * r] = byte_value<VT>(q[r], 0);
                     c.v[2 * r + 1] = byte_value<VT>(q[r], 1);
                 }
+            } else if constexpr (kShareF<VT> && PIPE) {
+                auto xf = [&](float v) {
+                    return __uint_as_float(partner_u32(__float_as_uint(v), lane));
+                };
+                const f4a o = {xf(S.w.r0.x), xf(S.w.r0.y), xf(S.w.r0.z), xf(S.w.r0.w)};
+                CellRaw<VT> w;
+                w.r0 = S.w.mode == 2u ? o : S.w.r0;
+                w.r1 = S.w.mode == 1u ? o : (S.w.mode == 2u ? S.w.r0 : S.w.r1);
+                c.decode(w);
             } else {
                 c.decode(S.w);
             }
@@ -1303,7 +1335,7 @@ __device__ __forceinline__ void march_strip(const MarchParams &P, LdsF4 *s_tf,
         };
         Stage A, B;
         int k = 0;
-        if constexpr (kShare<VT>) {
+        if constexpr (kPairStep<VT>) {
             // pairs leave together: a lane whose ray ended keeps stepping (stages not ok, dummy
             // loads, nothing composited) until its partner's ray has ended too
             prep(A, k);
