@@ -262,9 +262,11 @@ def test_queue_order_renders_the_same_frames(gpu, dtype):
                     rp.render_device(cam, base, ref.data_ptr(), vr_amd.OUT_RGBA8, 8, 0, 1)
                     outs = [torch.zeros((H, W), dtype=torch.int32, device="cuda") for _ in range(3)]
                     streams = [torch.cuda.Stream() for _ in range(3)]
+                    torch.cuda.synchronize()  # the allocations' fills ran on the null stream
                     for it in range(9):  # order kernel every 4 launches: sorted strip lists too
                         k = it % 3
-                        outs[k].zero_()
+                        with torch.cuda.stream(streams[k]):  # ordered before that frame
+                            outs[k].zero_()
                         rp.render_device(cam, q, outs[k].data_ptr(), vr_amd.OUT_RGBA8, 8, 0, 1,
                                          streams[k].cuda_stream)
                     torch.cuda.synchronize()

@@ -1047,17 +1047,21 @@ vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P, void *stream, uint32_t 
     for (int x = 0; x < 8; ++x)
         for (uint32_t j = 0; j < t.per_xcd; ++j) perm0[x + 8 * (size_t)j] = lists[(size_t)x * t.per_xcd + j];
     const size_t nt = (size_t)P.tiles_x * P.tiles_y * units;
-    const uint32_t zero9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // uploads on the frame's stream: a plain hipMemcpy from pageable memory may return before
+    // its DMA lands, and the first launch, on a non-blocking stream, would then read recycled
+    // memory (queue heads past the lists' end: a frame left unwritten).  Pageable sources are
+    // staged before hipMemcpyAsync returns, so the vectors may go out of scope.
+    hipStream_t hs = static_cast<hipStream_t>(stream);
     if (hipMalloc(&t.cost, nt * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&t.perm, lists.size() * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&t.lists, lists.size() * sizeof(uint32_t)) != hipSuccess ||
-        hipMemcpy(t.lists, lists.data(), lists.size() * sizeof(uint32_t), hipMemcpyHostToDevice) !=
-            hipSuccess ||
+        hipMemcpyAsync(t.lists, lists.data(), lists.size() * sizeof(uint32_t),
+                       hipMemcpyHostToDevice, hs) != hipSuccess ||
         (t.order == 5 &&
-         (hipMalloc(&t.queue, sizeof zero9) != hipSuccess ||
-          hipMemcpy(t.queue, zero9, sizeof zero9, hipMemcpyHostToDevice) != hipSuccess ||
-          hipMemcpy(t.perm, perm0.data(), perm0.size() * sizeof(uint32_t), hipMemcpyHostToDevice) !=
-              hipSuccess))) {
+         (hipMalloc(&t.queue, 9 * sizeof(uint32_t)) != hipSuccess ||
+          hipMemsetAsync(t.queue, 0, 9 * sizeof(uint32_t), hs) != hipSuccess ||
+          hipMemcpyAsync(t.perm, perm0.data(), perm0.size() * sizeof(uint32_t),
+                         hipMemcpyHostToDevice, hs) != hipSuccess))) {
         (void)hipGetLastError();
         hipFree(t.cost);
         hipFree(t.perm);
