@@ -33,7 +33,7 @@ def _scene(W, H, k=0):
                                       cam, W, H, p)
 
 
-def _worker(rank, world, port, W, H, rb, inflight, nframes, q):
+def _worker(rank, world, port, W, H, rb, inflight, nframes, q, share=(1, 1)):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for sub in ("volumetric-renderer_amd", "oracle", "tools"):
@@ -42,7 +42,7 @@ def _worker(rank, world, port, W, H, rb, inflight, nframes, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        rows = vr_dist.shard_global_rows(H, rb, rank, world)
+        rows = vr_dist.shard_global_rows(H, rb, rank, world, share)
         sr = len(rows)
         slots = [vr_dist.Slot(torch.zeros((sr, W, 4), dtype=torch.float32),
                               torch.zeros((world, sr, W, 4), dtype=torch.float32) if rank == 0 else None)
@@ -59,7 +59,7 @@ def _worker(rank, world, port, W, H, rb, inflight, nframes, q):
             state["k"] += 1
 
         def assemble(slot):
-            frames.append(vr_dist.assemble_numpy(slot.gbuf.numpy().copy(), H, rb, world))
+            frames.append(vr_dist.assemble_numpy(slot.gbuf.numpy().copy(), H, rb, world, share))
 
         pipe = vr_dist.FramePipeline(slots, rank, world, dist, render, assemble)
         for _ in range(nframes):
@@ -73,18 +73,20 @@ def _worker(rank, world, port, W, H, rb, inflight, nframes, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,rb,inflight,nframes",
-                         [(2, 16, 2, 3), (2, 4, 1, 3), (3, 8, 3, 5), (2, 8, 3, 2)])
-def test_gloo_sharded_frames_match_single_process(world, rb, inflight, nframes):
+@pytest.mark.parametrize("world,rb,inflight,nframes,share",
+                         [(2, 16, 2, 3, (1, 1)), (2, 4, 1, 3, (1, 1)), (3, 8, 3, 5, (1, 1)),
+                          (2, 8, 3, 2, (1, 1)), (3, 4, 2, 3, (1, 2)), (2, 4, 2, 2, (3, 2))])
+def test_gloo_sharded_frames_match_single_process(world, rb, inflight, nframes, share):
     """N ranks, several frames through vr_dist.FramePipeline (the benchmark's frame loop):
     every assembled frame equals the single-process oracle frame bit for bit, in order,
     serial (1 frame in flight) and with 2-3 frames in flight (gathers waited for only when
-    their slot comes round again; fewer frames than slots too)."""
+    their slot comes round again; fewer frames than slots too), and with weighted row shares
+    (vr_set_row_share: the first rank w0 blocks per w of every other rank)."""
     W, H = 40, 45
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, rb, inflight, nframes, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, rb, inflight, nframes, q, share))
              for r in range(world)]
     for p in procs:
         p.start()
