@@ -264,21 +264,23 @@ def tcp_model(view_name="fill", n=512, W=1920, H=1080, ntiles=40, seed=0, vb=4):
         tx, ty = rng.integers(0, W // tw), rng.integers(0, H // th)
         px, py = np.meshgrid(np.arange(tw) + tx * tw, np.arange(th) + ty * th)
         ok, pos0, dirs = rays(view, pos, W, H, px.ravel().astype(float), py.ravel().astype(float))
-        if ok.sum() < 64:
+        if ok.sum() < 32:
             continue
         tiles += 1
-        p = pos0.copy()
+        p = np.clip(pos0.copy(), 0.0, 1.0)  # the entry-face snap (pixel_ray)
+        alive = ok.copy()
         for _ in range(360):
-            inside = np.all((p >= 0) & (p <= 1), axis=1)
-            if not inside.all():
+            alive &= np.all((p >= 0) & (p <= 1), axis=1)
+            if not alive.any():
                 break
-            i0 = np.floor(p * n - 0.5).astype(np.int64)
+            i0 = np.floor(np.clip(p, 0, 1) * n - 0.5).astype(np.int64)
             for addr, width in layout(i0[:, 0], i0[:, 1], i0[:, 2], nb):
-                tot += tcp_counts(addr, width)
+                tot += tcp_counts(addr, width, alive)
                 loads += 1
             cell = (i0[:, 2] * (n + 8) + i0[:, 1]) * (n + 8) + i0[:, 0]
-            pairs += 32
-            same_cell += int((cell[0::2] == cell[1::2]).sum())
+            both = alive[0::2] & alive[1::2]
+            pairs += int(both.sum())
+            same_cell += int(((cell[0::2] == cell[1::2]) & both).sum())
             p = p + dirs * 0.005
     return dict(view=view_name, wave_loads=loads, h0_lines_per_wave=tot[0] / loads,
                 h1_sectors_per_quarter=tot[1] / loads, h2_lines_per_quarter=tot[2] / loads,
