@@ -16,8 +16,13 @@ Workload (configs[2] of BASELINE.json, the configuration the metric is quoted on
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W].
   N > 1 under torch.distributed.run (WORLD_SIZE set): one process per GPU, the library's RCCL
         frame path (vr_dist.h); WORLD_SIZE must equal N.
-  N > 1 without WORLD_SIZE: ONE process driving N devices through a multi-device context
-        (vr_create_mask, the drop-in boundary's own multi-GPU form).
+  N > 1 without WORLD_SIZE: bench.py starts `python -m torch.distributed.run --nproc-per-node N
+        --master-addr 127.0.0.1` on itself as a child process, before anything touches the GPU,
+        and exits with its status (the per-process RCCL path INTEGRATION.md recommends).
+        --multi-device-context instead drives the N devices from ONE process through
+        vr_create_mask (the drop-in boundary's own multi-GPU form).
+  --members-on-one-gpu M (rehearsal): one process, a multi-device context of M members all on
+        device 0 (vr_debug_create_members, copy exchange): the multi-device machinery on one GPU.
   Either way a run that cannot use exactly N GPUs fails (exit 2) naming what is missing.
 """
 from __future__ import annotations
@@ -101,8 +106,9 @@ def algorithmic_bytes(stats, voxel_bytes, pixels, out_bytes=4):
             + pixels * out_bytes)
 
 
-def setup_pass(cfg, device, device_mask=None):
-    rp = vr_amd.OffscreenPass(cfg["W"], cfg["H"], device=device, device_mask=device_mask)
+def setup_pass(cfg, device, device_mask=None, members=None):
+    rp = vr_amd.OffscreenPass(cfg["W"], cfg["H"], device=device, device_mask=device_mask,
+                              members=members)
     if cfg.get("source") == "ct_head":
         # host-generated u8 CT head through the Dataset path (volume_dataset_changed)
         rp.volume_dataset_changed(synth.dataset(synth.ct_head(cfg["dims"][0], cfg["seed"])))
@@ -300,7 +306,7 @@ def run_variant(rp, cfg, steps, warmup, rank, world, inflight, row_block=8, grou
         # HIP events (vr_debug_timing_member), so a slow frame names its straggler
         loop = round((t1 - t0) / steps * 1e3, 4)
         per_rank = []
-        for m in range(bin(rp.device_mask).count("1")):
+        for m in range(rp.n_members):
             t = rp.timing_member(m)
             n = max(t["frames"], 1)
             per_rank.append(dict(rank=m, device=t["device"], loop_ms_per_frame=loop,
@@ -426,13 +432,28 @@ def volume_layout(rp):
     return f"st{st}:{rp.volume_bytes()}"
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """--gpus N > 1 without WORLD_SIZE: run this script under torch.distributed.run, one process
+    per GPU, as a child (nothing here has touched the GPU: torch.cuda.device_count() does not
+    initialise it), and return its exit status.  The child's rank 0 prints the JSON line on the
+    stdout this process hands down."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"bench: --gpus {n} without WORLD_SIZE: launching {' '.join(cmd)}", file=sys.stderr,
+          flush=True)
+    return subprocess.run(cmd).returncode
+
+
 def main():
-    # stdout carries exactly one line, the JSON result (rank 0).  Libraries print banners to
-    # fd 1 on their own (RCCL writes its version block when a communicator is created), so fd
-    # 1 points at stderr for the whole run and is restored only for the result line.
-    sys.stdout.flush()
-    result_fd = os.dup(1)
-    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -453,15 +474,34 @@ def main():
                     help="GPU_MAX_HW_QUEUES for this process (set before HIP starts; default: the "
                          "environment's, HIP default 4)")
     ap.add_argument("--multi-device-context", action="store_true",
-                    help="without WORLD_SIZE: drive the GPUs through vr_create_mask even for --gpus 1 "
-                         "(the default for --gpus > 1)")
+                    help="without WORLD_SIZE: drive the N GPUs from one process through "
+                         "vr_create_mask (default for N > 1: one process per GPU, launched here)")
+    ap.add_argument("--members-on-one-gpu", type=int, default=0,
+                    help="rehearsal: a multi-device context of M members all on device 0 "
+                         "(vr_debug_create_members, copy exchange); --gpus must be 1")
     args = ap.parse_args()
     if args.gpus < 1:
         fail_exit("--gpus must be >= 1")
+    if args.members_on_one_gpu and (args.gpus != 1 or os.environ.get("WORLD_SIZE")):
+        fail_exit("--members-on-one-gpu needs --gpus 1 and no torch.distributed launch")
+    if (os.environ.get("WORLD_SIZE") is None and args.gpus > 1 and not args.multi_device_context):
+        ndev = torch.cuda.device_count()
+        if ndev < args.gpus:
+            fail_exit(f"--gpus {args.gpus} needs {args.gpus} HIP devices; device {ndev} is not "
+                      f"present ({ndev} visible)")
+        sys.exit(launch_ranks(args.gpus))
+
+    # stdout carries exactly one line, the JSON result (rank 0).  Libraries print banners to
+    # fd 1 on their own (RCCL writes its version block when a communicator is created), so fd
+    # 1 points at stderr for the whole run and is restored only for the result line.
+    sys.stdout.flush()
+    result_fd = os.dup(1)
+    os.dup2(2, 1)
 
     # How the N GPUs are driven.  torch.distributed.run sets WORLD_SIZE: one process per GPU,
-    # and the launch must match --gpus.  Without it, --gpus N > 1 is ONE process over N devices
-    # (vr_create_mask).  Either way exactly N devices must be there.
+    # and the launch must match --gpus.  Without it (and with --multi-device-context), --gpus N
+    # is ONE process over N devices (vr_create_mask).  Either way exactly N devices must be
+    # there.
     world_env = os.environ.get("WORLD_SIZE")
     world = int(world_env) if world_env is not None else 1
     rank = int(os.environ.get("RANK", "0"))
@@ -469,7 +509,9 @@ def main():
     if world_env is not None and world != args.gpus:
         fail_exit(f"--gpus {args.gpus} but torch.distributed.run started WORLD_SIZE={world} "
                   "ranks; they must agree")
-    group = world_env is None and (args.gpus > 1 or args.multi_device_context)
+    group = world_env is None and (args.gpus > 1 or args.multi_device_context
+                                   or args.members_on_one_gpu > 0)
+    members = [0] * args.members_on_one_gpu if args.members_on_one_gpu else None
     ndev = torch.cuda.device_count()
     global BACKEND, GATHER
     # VR_DIST_BACKEND=gloo rehearses the N > 1 path with ranks sharing devices (host-staged
@@ -497,7 +539,8 @@ def main():
     n_gpus = args.gpus if group else world
 
     cfg = CONFIGS[args.config]
-    rp = setup_pass(cfg, device, device_mask=((1 << args.gpus) - 1) if group else None)
+    rp = setup_pass(cfg, device, device_mask=((1 << args.gpus) - 1) if group and not members else None,
+                    members=members)
     if group and rp.device_mask != (1 << args.gpus) - 1:
         fail_exit(f"multi-device context spans mask {rp.device_mask:#x}, not {args.gpus} devices")
     vbytes = np.dtype(cfg["dtype"]).itemsize
@@ -691,12 +734,12 @@ def main():
                                 for n in ("c1", "c2")}
 
     if rank == 0:
-        if group:
+        if group and members:
+            parallelism = (f"REHEARSAL: image 8-row blocks cyclic x{len(members)} members all on "
+                           "device 0 in one process (vr_debug_create_members) + copy exchange")
+        elif group:
             parallelism = (f"image 8-row blocks cyclic x{n_gpus} devices in one process "
                            "(vr_create_mask) + RCCL ncclGather (ncclCommInitAll), stream-ordered")
-            if n_gpus > 1:
-                parallelism += ("; NOTE: the vr_create_mask path with >= 2 devices had not run on "
-                                "hardware before this run (frame_check verifies its frame)")
         elif world > 1:
             parallelism = f"image 8-row blocks cyclic x{world} processes" + (
                 " + gloo host-staged gather (rehearsal, ranks share devices)" if BACKEND != "nccl"

@@ -59,6 +59,28 @@ typedef struct vr_member_timing {
 } vr_member_timing;
 int vr_debug_timing_member(vr_ctx *ctx, int member, vr_member_timing *out);
 
+/* One-GPU rehearsal of the multi-device path (round 5).  A multi-device context over an explicit
+ * member list: devices[m] is member m's device (member 0 assembles the frame), and a device may
+ * be listed more than once -- two members on device 0 exercise on one GPU what vr_create_mask
+ * runs on several: the frame workers, the volume replication, the per-member slot pipelines,
+ * the row shares and the assembly.  `exchange` is how the shards reach member 0:
+ *   VR_EXCHANGE_RCCL  ncclGather over ncclCommInitAll communicators (vr_create_mask's; the
+ *                     devices must be distinct -- RCCL holds one rank per device)
+ *   VR_EXCHANGE_COPY  stream-ordered device-to-device copies of every member's shard into
+ *                     member 0's gather buffer, enqueued by member 0 (peer copies across
+ *                     devices), with host-side frame handshakes between the member threads
+ * Frames are byte-identical to a one-device context's in both.  NULL on failure
+ * (vr_last_error(NULL)). */
+enum vr_exchange { VR_EXCHANGE_RCCL = 0, VR_EXCHANGE_COPY = 1 };
+vr_ctx *vr_debug_create_members(const int *devices, int n, uint32_t width, uint32_t height,
+                                int exchange);
+/* Failure injection on a multi-device context: member `member`'s enqueue of its pipelines'
+ * frame number `frame` (counted from 0 since the pipelines were built for the current frame
+ * shape; the first frame after creation is 0) fails with VR_EIO, as a device error would.  The
+ * context then aborts the frame exchange and every later frame fails; vr_destroy still returns
+ * (no stream waits forever).  member < 0 clears it.  VR_EINVAL on a one-device context. */
+int vr_debug_fail_member(vr_ctx *ctx, int member, uint64_t frame);
+
 /* Set / read one knob of `ctx` (a multi-device context sets it on every device).
  * VR_EINVAL for an unknown knob or an out-of-range value. */
 int vr_debug_set_knob(vr_ctx *ctx, int knob, int value);

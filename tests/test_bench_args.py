@@ -29,3 +29,16 @@ def test_launcher_world_size_must_match_gpus():
     r = _bench(["--gpus", "2"], WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
     assert "WORLD_SIZE=1" in r.stderr and "must agree" in r.stderr
+
+
+def test_multi_device_context_needs_the_devices_too():
+    import torch
+    n = torch.cuda.device_count()
+    r = _bench(["--gpus", str(n + 1), "--multi-device-context"])
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert f"device {n} is not present" in r.stderr, r.stderr[-2000:]
+
+
+def test_member_rehearsal_is_one_gpu_only():
+    r = _bench(["--gpus", "2", "--members-on-one-gpu", "2"])
+    assert r.returncode == 2 and "--members-on-one-gpu needs --gpus 1" in r.stderr

@@ -59,3 +59,21 @@ def test_bench_multi_device_context_path(gpu):
     assert d["n_gpus"] == 1 and d["frame_check"] is True
     assert "vr_create_mask" in d["config"]["parallelism"]
     assert d["value"] > 0
+
+
+def test_bench_member_rehearsal_on_one_gpu(gpu):
+    """--members-on-one-gpu 2: the multi-device context with two members on device 0 (copy
+    exchange) under bench.py's frame loop; the assembled frame equals a one-device frame and
+    the per-member rows name both members."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "6", "--warmup", "2",
+                        "--no-cpu-baseline", "--no-variants", "--members-on-one-gpu", "2"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["frame_check"] is True
+    assert "REHEARSAL" in d["config"]["parallelism"]
+    pr = d["per_rank"]
+    assert [x["rank"] for x in pr] == [0, 1] and all(x["device"] == 0 for x in pr)
+    assert all(x["frames"] > 0 and x["kernel_ms"] > 0 for x in pr)

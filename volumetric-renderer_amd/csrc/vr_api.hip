@@ -1196,6 +1196,48 @@ hipEvent_t pooled_event(vr_ctx *c)
     return e;
 }
 
+// A multi-device context over `devices` (member m on devices[m]; member 0 assembles).
+vr_ctx *create_members(const std::vector<int> &devices, uint32_t width, uint32_t height,
+                       int exchange)
+{
+    if (width == 0 || height == 0) {
+        fail(nullptr, VR_EINVAL, "framebuffer size must be non-zero");
+        return nullptr;
+    }
+    vr_ctx *c = new (std::nothrow) vr_ctx();
+    if (!c) {
+        fail(nullptr, VR_ENOMEM, "out of host memory");
+        return nullptr;
+    }
+    c->device = devices[0];
+    for (int d : devices) c->device_mask |= 1u << d;
+    c->width = width;
+    c->height = height;
+#ifdef VR_EXPERIMENTS
+    knobs_from_env(c);
+#endif
+    for (int d : devices) {
+        vr_ctx *m = vr_create(d, width, height);  // the reference constructor's placeholders
+        if (!m) {
+            const std::string e = g_err;
+            vr_destroy(c);
+            fail(nullptr, VR_ENODEV, "device " + std::to_string(d) + ": " + e);
+            return nullptr;
+        }
+        m->knobs = c->knobs;
+        c->members.push_back(m);
+    }
+    std::string err;
+    c->group = vr::group_create(c->members, exchange, &err);
+    if (!c->group) {
+        vr_destroy(c);
+        fail(nullptr, VR_ENODEV, "multi-device context: " + err);
+        return nullptr;
+    }
+    hipSetDevice(c->device);
+    return c;
+}
+
 }  // namespace
 
 bool vr::is_multi_device(const vr_ctx *c) { return is_group(c); }
@@ -1288,51 +1330,45 @@ vr_ctx *vr_create_mask(uint32_t device_mask, uint32_t width, uint32_t height)
         fail(nullptr, VR_EINVAL, "device_mask is empty");
         return nullptr;
     }
-    for (int d = 0; d < 32; ++d)
-        if ((device_mask >> d) & 1u && d >= ndev) {
+    std::vector<int> devices;
+    for (int d = 0; d < 32; ++d) {
+        if (!((device_mask >> d) & 1u)) continue;
+        if (d >= ndev) {
             fail(nullptr, VR_ENODEV, "device " + std::to_string(d) + " of device_mask 0x" +
                                          [&] { char b[16]; std::snprintf(b, sizeof b, "%x", device_mask); return std::string(b); }() +
                                          " is not present (" + std::to_string(ndev) +
                                          " HIP device(s) visible)");
             return nullptr;
         }
-    if (width == 0 || height == 0) {
-        fail(nullptr, VR_EINVAL, "framebuffer size must be non-zero");
+        devices.push_back(d);
+    }
+    return create_members(devices, width, height, VR_EXCHANGE_RCCL);
+}
+
+vr_ctx *vr_debug_create_members(const int *devices, int n, uint32_t width, uint32_t height,
+                                int exchange)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        fail(nullptr, VR_ENODEV, "no HIP device available");
         return nullptr;
     }
-    vr_ctx *c = new (std::nothrow) vr_ctx();
-    if (!c) {
-        fail(nullptr, VR_ENOMEM, "out of host memory");
+    if (!devices || n < 1 || n > 64) {
+        fail(nullptr, VR_EINVAL, "devices must list 1..64 members");
         return nullptr;
     }
-    c->device = __builtin_ctz(device_mask);
-    c->device_mask = device_mask;
-    c->width = width;
-    c->height = height;
-#ifdef VR_EXPERIMENTS
-    knobs_from_env(c);
-#endif
-    for (int d = 0; d < 32; ++d) {
-        if (!((device_mask >> d) & 1u)) continue;
-        vr_ctx *m = vr_create(d, width, height);  // the reference constructor's placeholders
-        if (!m) {
-            const std::string e = g_err;
-            vr_destroy(c);
-            fail(nullptr, VR_ENODEV, "device " + std::to_string(d) + ": " + e);
+    if (exchange != VR_EXCHANGE_RCCL && exchange != VR_EXCHANGE_COPY) {
+        fail(nullptr, VR_EINVAL, "exchange must be VR_EXCHANGE_RCCL or VR_EXCHANGE_COPY");
+        return nullptr;
+    }
+    std::vector<int> devs(devices, devices + n);
+    for (int d : devs)
+        if (d < 0 || d >= ndev) {
+            fail(nullptr, VR_ENODEV, "device " + std::to_string(d) + " is not present (" +
+                                         std::to_string(ndev) + " HIP device(s) visible)");
             return nullptr;
         }
-        m->knobs = c->knobs;
-        c->members.push_back(m);
-    }
-    std::string err;
-    c->group = vr::group_create(c->members, &err);
-    if (!c->group) {
-        vr_destroy(c);
-        fail(nullptr, VR_ENODEV, "multi-device context: " + err);
-        return nullptr;
-    }
-    hipSetDevice(c->device);
-    return c;
+    return create_members(devs, width, height, exchange);
 }
 
 void vr_destroy(vr_ctx *c)
@@ -2086,6 +2122,15 @@ int vr_debug_timing_member(vr_ctx *c, int member, vr_member_timing *out)
     out->render_ms = ms[0];
     out->gather_ms = ms[1];
     out->assemble_ms = ms[2];
+    return VR_OK;
+}
+
+int vr_debug_fail_member(vr_ctx *c, int member, uint64_t frame)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (!is_group(c)) return fail(c, VR_EINVAL, "not a multi-device context");
+    std::string m;
+    if (int rc = vr::group_fail_member(c->group, member, frame, &m)) return fail(c, rc, m);
     return VR_OK;
 }
 

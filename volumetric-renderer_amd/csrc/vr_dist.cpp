@@ -25,7 +25,10 @@
 #include "vr_frame_workers.h"
 #include "vr_group.h"
 
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -87,6 +90,46 @@ Rccl &rccl()
 struct Buffers {
     void *shard = nullptr;  // shard_rows x W pixels (RGBA8, or RGBA32F in multi-device contexts)
     void *gbuf = nullptr;   // rank 0: nranks shards, rank-major
+    hipEvent_t xev = nullptr;  // copy exchange: member > 0 shard ready / member 0 copies done
+};
+
+// The copy exchange of a multi-device context (vr_debug_create_members, VR_EXCHANGE_COPY):
+// the frame's gather as device-to-device copies that member 0 enqueues on its communication
+// stream, for members that RCCL cannot put in one communicator (the same device twice: the
+// one-GPU rehearsal of the multi-device path) or when RCCL is absent.  Per frame f and slot k:
+//   member m > 0 : [its comm stream, after rendered_k] record xev_k; publish sent[m] = f + 1;
+//                  host-wait copied > f; its comm stream waits member 0's xev_k (the copy read
+//                  its shard, so the slot may be reused after gathered_k)
+//   member 0     : copy its own shard; for every m: host-wait sent[m] > f, wait m's xev_k,
+//                  copy m's shard into gbuf_k + m * shard; record xev_k; publish copied = f + 1
+// A stream only ever waits on an event recorded (and published) before: nothing on a device
+// can wait for a record that never comes.  Slot events are re-recorded F frames later, only
+// after every waiter has enqueued its wait (the host waits above order them).  A member that
+// fails sets `aborted`, which ends every host wait with VR_EIO.
+struct CopyExchange {
+    std::mutex m;
+    std::condition_variable cv;
+    std::vector<uint64_t> sent;   // per member: frames whose shard-ready event is recorded
+    uint64_t copied = 0;          // frames whose copies member 0 has enqueued
+    bool aborted = false;
+    std::vector<vr_dist *> peers;  // the members' pipelines (member order)
+
+    void abort()
+    {
+        {
+            std::lock_guard<std::mutex> g(m);
+            aborted = true;
+        }
+        cv.notify_all();
+    }
+    // Waits until pred() holds (true) or the exchange is aborted / 120 s pass (false).
+    template <class P>
+    bool wait(P pred)
+    {
+        std::unique_lock<std::mutex> g(m);
+        return cv.wait_for(g, std::chrono::seconds(120), [&] { return aborted || pred(); }) &&
+               !aborted;
+    }
 };
 
 // Timing pairs (vr_dist_timing_enable): recorded per frame on the op's stream, read and freed
@@ -117,6 +160,8 @@ struct vr_dist {
     uint32_t row_block = 8, width = 0, height = 0, shard_rows = 0;
     ncclComm_t comm = nullptr;
     bool owns_comm = true;  // false: a multi-device context's communicator (vr_group.h)
+    CopyExchange *xch = nullptr;  // not null: the copy exchange replaces ncclGather
+    uint32_t share_w0 = 1, share_w = 1;  // the row share shard_rows was sized for
     int out_format = VR_OUT_RGBA8;
     uint32_t words_per_pixel = 1;  // 32-bit words a pixel of out_format takes (gather count)
     std::vector<Buffers> bufs;  // per slot
@@ -217,10 +262,69 @@ int HipExec::render(int slot, uint64_t, Stream s)
     }
     return timed_end(d, d->t_render, s);
 }
-int HipExec::gather(int slot, uint64_t, Stream s)
+size_t shard_bytes(const vr_dist *d)
+{
+    return (size_t)d->shard_rows * d->width * 4 * d->words_per_pixel;
+}
+
+int copy_gather(vr_dist *d, int slot, uint64_t frame, hipStream_t s)
+{
+    CopyExchange &x = *d->xch;
+    Buffers &b = d->bufs[slot];
+    const size_t bytes = shard_bytes(d);
+    if (d->rank != 0) {
+        DTRY(hip_check(d, hipEventRecord(b.xev, s), "hipEventRecord(shard ready)"));
+        {
+            std::lock_guard<std::mutex> g(x.m);
+            x.sent[d->rank] = frame + 1;
+        }
+        x.cv.notify_all();
+        if (!x.wait([&] { return x.copied > frame; }))
+            return dfail(d, VR_EIO, "copy exchange: member 0 did not copy frame " +
+                                        std::to_string(frame) + " (aborted or timed out)");
+        return hip_check(d, hipStreamWaitEvent(s, x.peers[0]->bufs[slot].xev, 0),
+                         "hipStreamWaitEvent(copies done)");
+    }
+    char *dst = static_cast<char *>(b.gbuf);
+    DTRY(hip_check(d, hipMemcpyAsync(dst, b.shard, bytes, hipMemcpyDeviceToDevice, s),
+                   "hipMemcpyAsync(own shard)"));
+    for (int m = 1; m < d->nranks; ++m) {
+        if (!x.wait([&] { return x.sent[m] > frame; }))
+            return dfail(d, VR_EIO, "copy exchange: member " + std::to_string(m) +
+                                        " did not render frame " + std::to_string(frame) +
+                                        " (aborted or timed out)");
+        vr_dist *p = x.peers[m];
+        DTRY(hip_check(d, hipStreamWaitEvent(s, p->bufs[slot].xev, 0),
+                       "hipStreamWaitEvent(shard ready)"));
+        const hipError_t e =
+            p->device == d->device
+                ? hipMemcpyAsync(dst + (size_t)m * bytes, p->bufs[slot].shard, bytes,
+                                 hipMemcpyDeviceToDevice, s)
+                : hipMemcpyPeerAsync(dst + (size_t)m * bytes, d->device, p->bufs[slot].shard,
+                                     p->device, bytes, s);
+        DTRY(hip_check(d, e, "copy exchange (shard copy)"));
+    }
+    DTRY(hip_check(d, hipEventRecord(b.xev, s), "hipEventRecord(copies done)"));
+    {
+        std::lock_guard<std::mutex> g(x.m);
+        x.copied = frame + 1;
+    }
+    x.cv.notify_all();
+    return VR_OK;
+}
+
+int HipExec::gather(int slot, uint64_t frame, Stream s)
 {
     const Buffers &b = d->bufs[slot];
     DTRY(timed_begin(d, d->t_gather, s));
+    if (d->xch) {
+        const int rc = copy_gather(d, slot, frame, s);
+        if (rc != VR_OK) {
+            timed_abort(d, d->t_gather);
+            return rc;
+        }
+        return timed_end(d, d->t_gather, s);
+    }
     const int rc = nccl_check(d, rccl().gather(b.shard, d->rank == 0 ? b.gbuf : nullptr,
                                                (size_t)d->shard_rows * d->width * d->words_per_pixel,
                                                ncclUint32, 0,
@@ -287,6 +391,7 @@ void release(vr_dist *d)
     for (auto &b : d->bufs) {
         if (b.shard) hipFree(b.shard);
         if (b.gbuf) hipFree(b.gbuf);
+        if (b.xev) hipEventDestroy(b.xev);
     }
     for (auto &s : S.slots) {
         for (hipEvent_t e : {s.rendered, s.gathered, s.done})
@@ -299,12 +404,14 @@ void release(vr_dist *d)
     d->bufs.clear();
 }
 
-// Join the communicator of `id` (vr_dist_create) or adopt `comm` (multi-device contexts), then
-// allocate the slots.
+// Join the communicator of `id` (vr_dist_create), adopt `comm` (multi-device contexts) or use
+// the copy exchange (d->xch set), then allocate the slots.
 int setup(vr_dist *d, const void *id, ncclComm_t comm, int frames)
 {
     DTRY(hip_check(d, hipSetDevice(d->device), "hipSetDevice"));
-    if (comm) {
+    if (d->xch) {
+        d->owns_comm = false;
+    } else if (comm) {
         d->comm = comm;
         d->owns_comm = false;
     } else {
@@ -319,7 +426,7 @@ int setup(vr_dist *d, const void *id, ncclComm_t comm, int frames)
     DTRY(hip_check(d, hipStreamCreateWithFlags(&S.comm, hipStreamNonBlocking),
                    "hipStreamCreate(comm)"));
     DTRY(hip_check(d, hipEventCreateWithFlags(&S.called, hipEventDisableTiming), "hipEventCreate"));
-    const size_t shard_bytes = (size_t)d->shard_rows * d->width * 4 * d->words_per_pixel;
+    const size_t sbytes = shard_bytes(d);
     S.slots.resize(frames);
     d->bufs.resize(frames);
     for (int k = 0; k < frames; ++k) {
@@ -327,9 +434,12 @@ int setup(vr_dist *d, const void *id, ncclComm_t comm, int frames)
         auto &b = d->bufs[k];
         DTRY(hip_check(d, hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking),
                        "hipStreamCreate(slot)"));
-        DTRY(hip_check(d, hipMalloc(&b.shard, shard_bytes), "hipMalloc(shard)"));
+        DTRY(hip_check(d, hipMalloc(&b.shard, sbytes), "hipMalloc(shard)"));
         if (d->rank == 0)
-            DTRY(hip_check(d, hipMalloc(&b.gbuf, shard_bytes * d->nranks), "hipMalloc(gather)"));
+            DTRY(hip_check(d, hipMalloc(&b.gbuf, sbytes * d->nranks), "hipMalloc(gather)"));
+        if (d->xch)
+            DTRY(hip_check(d, hipEventCreateWithFlags(&b.xev, hipEventDisableTiming),
+                           "hipEventCreate(exchange)"));
         for (hipEvent_t *e : {&s.rendered, &s.gathered, &s.done})
             DTRY(hip_check(d, hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate"));
     }
@@ -356,14 +466,15 @@ int vr_dist_unique_id(void *id_out)
 namespace {
 
 vr_dist *dist_create(vr_ctx *ctx, const void *id, ncclComm_t comm, int nranks, int rank,
-                     uint32_t row_block, int frames_in_flight, int out_format)
+                     uint32_t row_block, int frames_in_flight, int out_format,
+                     CopyExchange *xch = nullptr)
 {
     if (nranks < 1 || rank < 0 || rank >= nranks || row_block == 0 || frames_in_flight < 1 ||
         frames_in_flight > 8) {
         dfail(nullptr, VR_EINVAL, "bad nranks/rank/row_block/frames_in_flight");
         return nullptr;
     }
-    if (!rccl().ok) {
+    if (!xch && !rccl().ok) {
         dfail(nullptr, VR_ENODEV, rccl().err);
         return nullptr;
     }
@@ -378,7 +489,9 @@ vr_dist *dist_create(vr_ctx *ctx, const void *id, ncclComm_t comm, int nranks, i
     d->row_block = row_block;
     d->out_format = out_format;
     d->words_per_pixel = out_format == VR_OUT_RGBA32F ? 4 : 1;
-    if (vr_get_device(ctx, &d->device) != VR_OK || vr_get_size(ctx, &d->width, &d->height) != VR_OK) {
+    d->xch = xch;
+    if (vr_get_device(ctx, &d->device) != VR_OK || vr_get_size(ctx, &d->width, &d->height) != VR_OK ||
+        vr_get_row_share(ctx, &d->share_w0, &d->share_w) != VR_OK) {
         dfail(nullptr, VR_EINVAL, "bad ctx");
         delete d;
         return nullptr;
@@ -418,9 +531,14 @@ int vr_dist_render(vr_dist *d, const vr_camera *cam, const vr_params *p, void *f
     if (!d) return dfail(nullptr, VR_EINVAL, "dist is NULL");
     if (!cam || !p) return dfail(d, VR_EINVAL, "camera or params is NULL");
     if (d->rank == 0 && !frame_dev) return dfail(d, VR_EINVAL, "rank 0 needs frame_dev");
-    uint32_t w = 0, h = 0;
+    uint32_t w = 0, h = 0, s0 = 1, s1 = 1;
     if (vr_get_size(d->ctx, &w, &h) != VR_OK || w != d->width || h != d->height)
         return dfail(d, VR_EINVAL, "the context was resized: create a new vr_dist");
+    // the shard buffers, the gather count and the assembly stride were sized for the row share
+    // in force at creation: a rank whose share grew would write past its shard
+    if (vr_get_row_share(d->ctx, &s0, &s1) != VR_OK || s0 != d->share_w0 || s1 != d->share_w)
+        return dfail(d, VR_EINVAL,
+                     "the context's row share changed (vr_set_row_share): create a new vr_dist");
     DTRY(hip_check(d, hipSetDevice(d->device), "hipSetDevice"));
     d->cam = cam;
     d->params = p;
@@ -500,6 +618,13 @@ struct Group {
     };
     std::vector<Spans> spans;
     std::unique_ptr<sched::FrameWorkers<GroupJob>> workers;
+    // VR_EXCHANGE_COPY: the gather as device copies (one exchange per pipeline build, whose
+    // frame counters start at 0 with the pipelines'); comms stay null
+    int exchange = VR_EXCHANGE_RCCL;
+    std::unique_ptr<CopyExchange> xch;
+    // vr_debug_fail_member: member fail_member's issue of pipeline frame fail_frame fails
+    int fail_member = -1;
+    uint64_t fail_frame = 0;
 };
 
 namespace {
@@ -507,9 +632,18 @@ namespace {
 int member_issue(Group *g, int m, const GroupJob &j, std::string *msg)
 {
     vr_dist *d = g->dists[m];
-    const int rc = vr_dist_render(d, &j.cam, &j.p, m == 0 ? j.out : nullptr,
-                                  m == 0 ? j.stream : g->own[m]);
-    if (rc && msg) *msg = d->err;
+    int rc;
+    if (m == g->fail_member && d->sched.frame == g->fail_frame)
+        rc = dfail(d, VR_EIO, "injected failure (vr_debug_fail_member) of frame " +
+                                  std::to_string(d->sched.frame));
+    else
+        rc = vr_dist_render(d, &j.cam, &j.p, m == 0 ? j.out : nullptr,
+                            m == 0 ? j.stream : g->own[m]);
+    if (rc) {
+        if (msg) *msg = d->err;
+        // the copy exchange's peers wait on this member's frames on their host threads
+        if (g->xch) g->xch->abort();
+    }
     return rc;
 }
 
@@ -557,9 +691,13 @@ int ensure_pipelines(Group *g, int frames, int out_format, std::string *err)
     if (int rc = group_synchronize(g, err)) return rc;
     free_pipelines(g);
     const int n = (int)g->members.size();
+    if (g->exchange == VR_EXCHANGE_COPY) {
+        g->xch.reset(new CopyExchange());
+        g->xch->sent.assign(n, 0);
+    }
     for (int k = 0; k < n; ++k) {
         vr_dist *d = dist_create(g->members[k], nullptr, g->comms[k], n, k, kGroupRowBlock, frames,
-                                 out_format);
+                                 out_format, g->xch.get());
         if (!d) {
             *err = g_dist_err;
             free_pipelines(g);
@@ -568,6 +706,7 @@ int ensure_pipelines(Group *g, int frames, int out_format, std::string *err)
         d->timing = g->timing;
         g->dists.push_back(d);
     }
+    if (g->xch) g->xch->peers = g->dists;
     g->width = w;
     g->height = h;
     g->share_w0 = s0;
@@ -582,13 +721,17 @@ int ensure_pipelines(Group *g, int frames, int out_format, std::string *err)
 
 }  // namespace
 
-Group *group_create(const std::vector<vr_ctx *> &members, std::string *err)
+Group *group_create(const std::vector<vr_ctx *> &members, int exchange, std::string *err)
 {
     if (members.empty()) {
         *err = "no devices";
         return nullptr;
     }
-    if (!rccl().ok) {
+    if (exchange != VR_EXCHANGE_RCCL && exchange != VR_EXCHANGE_COPY) {
+        *err = "unknown exchange";
+        return nullptr;
+    }
+    if (exchange == VR_EXCHANGE_RCCL && !rccl().ok) {
         *err = rccl().err;
         return nullptr;
     }
@@ -604,11 +747,21 @@ Group *group_create(const std::vector<vr_ctx *> &members, std::string *err)
         g->devices.push_back(dev);
     }
     g->comms.assign(members.size(), nullptr);
-    const ncclResult_t r =
-        rccl().comm_init_all(g->comms.data(), (int)members.size(), g->devices.data());
-    if (r != ncclSuccess) {
-        *err = std::string("ncclCommInitAll: ") + rccl().error_string(r);
-        return nullptr;
+    g->exchange = exchange;
+    if (exchange == VR_EXCHANGE_RCCL) {
+        for (size_t a = 0; a < g->devices.size(); ++a)
+            for (size_t b = a + 1; b < g->devices.size(); ++b)
+                if (g->devices[a] == g->devices[b]) {
+                    *err = "device " + std::to_string(g->devices[a]) +
+                           " listed twice: RCCL holds one rank per device (use VR_EXCHANGE_COPY)";
+                    return nullptr;
+                }
+        const ncclResult_t r =
+            rccl().comm_init_all(g->comms.data(), (int)members.size(), g->devices.data());
+        if (r != ncclSuccess) {
+            *err = std::string("ncclCommInitAll: ") + rccl().error_string(r);
+            return nullptr;
+        }
     }
     g->own.assign(members.size(), nullptr);
     for (size_t m = 1; m < members.size(); ++m) {
@@ -630,6 +783,7 @@ Group *group_create(const std::vector<vr_ctx *> &members, std::string *err)
 // drained, before any stream is synchronised).  The context is unusable afterwards.
 void abort_comms(Group *g)
 {
+    if (g->xch) g->xch->abort();
     for (size_t m = 0; m < g->comms.size(); ++m)
         if (g->comms[m]) {
             hipSetDevice(g->devices[m]);
@@ -685,6 +839,20 @@ void group_destroy(Group *g)
         }
     if (!g->devices.empty()) hipSetDevice(g->devices[0]);
     delete g;
+}
+
+int group_exchange(const Group *g) { return g->exchange; }
+
+int group_fail_member(Group *g, int member, uint64_t frame, std::string *err)
+{
+    if (member >= (int)g->members.size()) {
+        *err = "no such member";
+        return VR_EINVAL;
+    }
+    // frames count from the next pipeline build; the current pipelines' counter otherwise
+    g->fail_member = member;
+    g->fail_frame = frame;
+    return VR_OK;
 }
 
 void group_timing_enable(Group *g, bool on)

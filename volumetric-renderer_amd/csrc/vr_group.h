@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/vr/vr.h"
+#include "../../include/vr/vr_debug.h"
 
 namespace vr {
 
@@ -24,9 +25,14 @@ constexpr uint32_t kGroupRowBlock = 8;
 // True for a vr_create_mask context (vr_api.hip).
 bool is_multi_device(const vr_ctx *c);
 
-// The communicators over the members' devices (one member per device, member 0 = the frame's
-// device).  nullptr on failure (*err says why).
-Group *group_create(const std::vector<vr_ctx *> &members, std::string *err);
+// The frame exchange over the members' devices (member 0 = the frame's device):
+// VR_EXCHANGE_RCCL, one communicator per member from ncclCommInitAll (distinct devices), or
+// VR_EXCHANGE_COPY, device copies onto member 0 (any devices, the same one repeated included).
+// nullptr on failure (*err says why).
+Group *group_create(const std::vector<vr_ctx *> &members, int exchange, std::string *err);
+int group_exchange(const Group *g);
+// vr_debug_fail_member: member's issue of pipeline frame `frame` fails (member < 0: never).
+int group_fail_member(Group *g, int member, uint64_t frame, std::string *err);
 // Waits for every frame issued so far (enqueue and device work), then frees the pipelines and
 // communicators; the member contexts stay.
 void group_destroy(Group *g);

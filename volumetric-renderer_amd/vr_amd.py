@@ -106,7 +106,10 @@ DIST_SYMBOLS = [
     "vr_dist_last_error", "vr_dist_destroy", "vr_dist_timing_enable", "vr_dist_timing_read",
 ]
 DIST_ID_BYTES = 128  # include/vr/vr_dist.h VR_DIST_ID_BYTES
-DEBUG_SYMBOLS = ["vr_debug_set_knob", "vr_debug_get_knob", "vr_debug_timing_member"]
+DEBUG_SYMBOLS = ["vr_debug_set_knob", "vr_debug_get_knob", "vr_debug_timing_member",
+                 "vr_debug_create_members", "vr_debug_fail_member"]
+# include/vr/vr_debug.h enum vr_exchange (multi-device contexts: how shards reach member 0)
+EXCHANGE_RCCL, EXCHANGE_COPY = 0, 1
 # include/vr/vr_debug.h enum vr_knob (launch-policy overrides: speed only, never results)
 KNOBS = {"pipeline": 1, "pair": 2, "pair_lanes": 3, "grad_field": 4, "u8_layout": 6,
          "tile_order": 7, "narrow": 8, "alt_geometry": 9}
@@ -186,6 +189,8 @@ def lib() -> C.CDLL:
         "vr_memory_report": (i32, [vp, C.POINTER(vr_memory_info)]),
         "vr_prepare": (i32, [vp, C.POINTER(vr_camera), C.POINTER(vr_params)]),
         "vr_debug_get_knob": (i32, [vp, i32, C.POINTER(i32)]),
+        "vr_debug_create_members": (vp, [C.POINTER(i32), i32, u32, u32, i32]),
+        "vr_debug_fail_member": (i32, [vp, i32, C.c_uint64]),
         "vr_cam_init": (None, [C.POINTER(vr_orbit_camera)]),
         "vr_cam_rotate": (None, [C.POINTER(vr_orbit_camera), f32, f32]),
         "vr_cam_zoom": (None, [C.POINTER(vr_orbit_camera), f32]),
@@ -381,11 +386,20 @@ def write_nrrd_raw(nhdr_path: str, data: np.ndarray) -> None:
 class OffscreenPass:
     """Mirror of Vol::Rendering::OffscreenPass (offscreen_pass.h:40-54) over the C ABI."""
 
-    def __init__(self, width: int, height: int, device: int = 0, device_mask: Optional[int] = None):
+    def __init__(self, width: int, height: int, device: int = 0, device_mask: Optional[int] = None,
+                 members: Optional[Sequence[int]] = None, exchange: int = EXCHANGE_COPY):
         """device: the HIP device (vr_create); device_mask: render every frame across these
-        devices instead (vr_create_mask, bit d = device d)."""
+        devices instead (vr_create_mask, bit d = device d); members: an explicit member list
+        whose devices may repeat (vr_debug_create_members, the one-GPU rehearsal), with the
+        shards reaching member 0 by `exchange` (EXCHANGE_COPY or EXCHANGE_RCCL)."""
         L = lib()
-        if device_mask is None:
+        self.n_members = len(members) if members is not None else (
+            1 if device_mask is None else bin(device_mask).count("1"))
+        if members is not None:
+            devs = (C.c_int * len(members))(*members)
+            self._ctx = L.vr_debug_create_members(devs, len(members), width, height, exchange)
+            what = "vr_debug_create_members"
+        elif device_mask is None:
             self._ctx = L.vr_create(device, width, height)
             what = "vr_create"
         else:
@@ -544,6 +558,10 @@ class OffscreenPass:
                     assemble_ms=float(t.assemble_ms))
 
     # -- ABI 7: row shares, derived-structure memory, preparation --
+    def fail_member(self, member: int, frame: int):
+        """vr_debug_fail_member: member's enqueue of pipeline frame `frame` fails (VR_EIO)."""
+        self._check(lib().vr_debug_fail_member(self._ctx, member, frame), "vr_debug_fail_member")
+
     def set_row_share(self, first_weight: int, other_weight: int):
         self._check(lib().vr_set_row_share(self._ctx, first_weight, other_weight), "set_row_share")
 
