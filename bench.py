@@ -68,6 +68,7 @@ GATHER = "native"  # N > 1 over RCCL: "native" (vr_dist.h) or "torch" (torch.dis
 # pipelined frames 10-15% slower (profiles/r02/warm_state/), so a fixed warm-up makes each
 # number independent of what ran before it.  The frames actually run are recorded.
 STEADY_WARMUP = 120
+BUDGET_DEFAULT = 2 ** 64 - 2  # vr.h VR_MEMORY_BUDGET_DEFAULT (ABI 8)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "Gsamples/sec + fps, 512³ NRRD @ 1080p; achieved HBM GB/s vs peak"
 
@@ -663,14 +664,14 @@ def main():
         # A camera crossing view classes: after frames of the fill view (the
         # difference field), the reference's default camera needs the stencil copy (~0.76 GB for
         # 512^3).  Built lazily, inside its first frame; or ahead by vr_prepare.  Serial frames,
-        # host-timed, derived structures freed before each arm (budget 0, then unlimited).
+        # host-timed, derived structures freed before each arm (budget 0, then the default).
         fcam = synth.camera(cfg["cam"]).to_vr_camera()
         dcam = synth.camera("default").to_vr_camera()
         vp = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"])
 
         def fresh_fill():
             rp.set_memory_budget(0)
-            rp.set_memory_budget(2 ** 64 - 1)
+            rp.set_memory_budget(BUDGET_DEFAULT)
             for _ in range(3):
                 rp.render_device(fcam, vp, R["last_frame_ptr"], vr_amd.OUT_RGBA8, 8, 0, 1)
             torch.cuda.synchronize()
@@ -695,6 +696,7 @@ def main():
             first_frame_lazy_ms=round(lazy, 3), first_frame_after_prepare_ms=round(prepared, 3),
             prepare_ms=round(prep, 3), steady_serial_frame_ms=round(steady, 3),
             derived_bytes_after_switch=built["derived_bytes"],
+            budget_bytes=built["budget_bytes"],
             stencil_copy_bytes=built["stencil_copy_bytes"], field_bytes=built["field_bytes"],
             note="host-timed serial frames around vr_render_device; vr_prepare builds the copy "
                  "outside the frame (vr.h ABI 7)")
@@ -733,6 +735,10 @@ def main():
         cpu["other_configs"] = {n: cpu_baseline_other(n, device, min(4.0, args.cpu_budget), cpu["cores"])
                                 for n in ("c1", "c2")}
 
+    mrep = rp.memory_report()
+    memory = dict(volume_bytes=mrep["volume_bytes"], derived_bytes=mrep["derived_bytes"],
+                  field_bytes=mrep["field_bytes"], budget_bytes=mrep["budget_bytes"],
+                  devices=rp.n_members)
     if rank == 0:
         if group and members:
             parallelism = (f"REHEARSAL: image 8-row blocks cyclic x{len(members)} members all on "
@@ -817,6 +823,11 @@ def main():
                                       "counts L1/L2 hits, so it can exceed 1 (not HBM traffic)",
             },
             "cpu_baseline": cpu,
+            # device memory of the context after the run, per device (a multi-device context
+            # replicates the volume and its derived structures on every device): bricks,
+            # derived structures (difference field, alternative copies, skip-empty) and the
+            # budget that caps them (vr.h VR_MEMORY_BUDGET_DEFAULT: 4x the bricks)
+            "memory_per_device": memory,
             "frame_check": R["check"],  # N > 1: assembled frame == single-GPU frame, bit for bit
             "per_rank": R["per_rank"],
             "variants": variants,

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 7
+#define VR_ABI_VERSION 8
 
 /* ---- status codes (negative errno style) ---- */
 #define VR_OK 0
@@ -138,6 +138,15 @@ typedef struct vr_params {
      * 1: exact f32 differences: every frame bit-identical to the f32 oracle.
      * Frames that form the gradient from the density stencil are exact either way. */
     int32_t exact_gradient;
+    /* (ABI 8) glm's clip-space depth form of the projection (offscreen_pass.cpp:1166
+     * glm::perspectiveRH).  0 (default): the [-1, 1] form (perspectiveRH_NO) -- the reference
+     * defines GLM_FORCE_DEPTH_ZERO_TO_ONE at offscreen_pass.cpp:3, after glm was first included
+     * through offscreen_pass.h, so the define has no effect there and Vulkan's 0 <= z_ndc <= 1
+     * clip puts the effective near plane at 0.198 (not 0.1).  1: the [0, 1] form
+     * (perspectiveRH_ZO), for a host built so that the define does take effect: the near
+     * plane is the camera's znear.  Only views whose front face lies nearer than 0.198 differ
+     * (the camera's radius clamp [0.1, 10], camera.cpp:33, allows them). */
+    int32_t depth_zero_to_one;
 } vr_params;
 
 /* Work counters of one frame (filled by vr_count_work). */
@@ -285,7 +294,12 @@ int vr_release_external_memory(vr_ctx *ctx, vr_external_memory *mem);
  * structure that would not fit is not built, and its frames read the bricks instead (the same
  * pixels; with the binary16 field absent a shaded frame forms exact f32 differences, i.e. the
  * exact_gradient = 1 pixels).  An alternative copy may evict the others to fit.  0 keeps only
- * the bricks; UINT64_MAX (the default) builds whatever fits beside a 2 GiB free-memory reserve.
+ * the bricks.  VR_MEMORY_BUDGET_DEFAULT (ABI 8, the default) is 4x the bricked volume's bytes
+ * (+ the skip-empty classification): the difference field (3x) and one alternative copy, e.g.
+ * C3 512^3 f32: 1.6 GB of bricks, at most 6.4 GB derived (the field and the default camera's
+ * stencil copy, 5.6 GB).  VR_MEMORY_BUDGET_UNLIMITED builds whatever fits beside a 2 GiB
+ * free-memory reserve (ABI 7's default).  A multi-device context applies the budget on every
+ * device (each holds its replica's structures).
  * Lowering the budget waits for the device and frees the structures.
  * vr_memory_report: the bytes each structure takes now on the (first) device.
  * vr_prepare: builds everything a frame with this camera and params would read, synchronously,
@@ -298,8 +312,11 @@ typedef struct vr_memory_info {
     uint64_t stencil_copy_bytes;  /* 29^3-cell stencil copy (shaded sparse views)      */
     uint64_t skip_bytes;          /* skip-empty brick ranges + distance field          */
     uint64_t derived_bytes;       /* the sum of the five above: what the budget caps   */
-    uint64_t budget_bytes;        /* the budget in force (UINT64_MAX: default policy)  */
+    uint64_t budget_bytes;        /* the budget in force, in bytes (the default's value
+                                     for this volume; VR_MEMORY_BUDGET_UNLIMITED)       */
 } vr_memory_info;
+#define VR_MEMORY_BUDGET_UNLIMITED (~(uint64_t)0)
+#define VR_MEMORY_BUDGET_DEFAULT (~(uint64_t)0 - 1)
 int vr_set_memory_budget(vr_ctx *ctx, uint64_t bytes);
 int vr_memory_report(const vr_ctx *ctx, vr_memory_info *out);
 int vr_prepare(vr_ctx *ctx, const vr_camera *cam, const vr_params *p);

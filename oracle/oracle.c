@@ -50,8 +50,9 @@ static void glm_perspective_rh_no(float fovy, float aspect, float zn, float zf, 
     m[3 * 4 + 2] = -(2.0f * zf * zn) / (zf - zn);
 }
 
-/* glm::perspectiveRH_ZO: the form GLM_FORCE_DEPTH_ZERO_TO_ONE selects (conformance variant
- * OR_CONF_CLIP_ZO: the define at offscreen_pass.cpp:3 taking effect after all). */
+/* glm::perspectiveRH_ZO: the form GLM_FORCE_DEPTH_ZERO_TO_ONE selects (OR_CONF_CLIP_ZO: the
+ * define at offscreen_pass.cpp:3 taking effect after all; the product's
+ * vr_params.depth_zero_to_one = 1). */
 static void glm_perspective_rh_zo(float fovy, float aspect, float zn, float zf, float *m)
 {
     memset(m, 0, 16 * sizeof(float));
@@ -686,7 +687,9 @@ march_pixel_impl(const or_scene *s, const ray_frame *f, const float *lut, int px
 static void march_pixel(const or_scene *s, const ray_frame *f, const float *lut, int px,
                         int py, float *out, or_stats *st)
 {
-    if (s->conf_flags == 0 && s->conf_weight_bits == 0)
+    /* OR_CONF_CLIP_ZO only changes the ray frame (make_ray_frame): it is also the product's
+     * vr_params.depth_zero_to_one (ABI 8), so it keeps the oracle's own march */
+    if ((s->conf_flags & ~OR_CONF_CLIP_ZO) == 0 && s->conf_weight_bits == 0)
         march_pixel_impl(s, f, lut, px, py, out, st, 0);
     else
         march_pixel_impl(s, f, lut, px, py, out, st, 1);

@@ -112,7 +112,9 @@ typedef struct or_scene {
  * C.rgb = fma(rgb*a, T, C.rgb) (volume.frag:44). */
 #define OR_CONF_FMA 1
 /* glm's [0, 1] clip form: perspectiveRH_ZO instead of _NO (offscreen_pass.cpp:3,1166), i.e.
- * GLM_FORCE_DEPTH_ZERO_TO_ONE in effect; moves the effective near plane 0.198 -> 0.1. */
+ * GLM_FORCE_DEPTH_ZERO_TO_ONE in effect; moves the effective near plane 0.198 -> 0.1.  Also the
+ * product switch vr_params.depth_zero_to_one (vr.h ABI 8): alone it keeps the oracle's march
+ * (only the ray frame changes), so parity in both forms is bit-exact. */
 #define OR_CONF_CLIP_ZO 2
 /* Entry attributes (in_tex_coords, in_frag_position) from a rasteriser model instead of the
  * exact double ray/box intersection: float clip positions ((proj*view)*v, volume.vert:23),

@@ -146,7 +146,8 @@ class Scene:
                    clear=list(params.clear_color), ka=params.ambient, kd=params.diffuse,
                    ks=params.specular, spec_power=params.spec_power,
                    fovy_deg=camera.fovy_deg or 40.0, znear=camera.znear or 0.1,
-                   zfar=camera.zfar or 10.0, grad_f16=grad_f16)
+                   zfar=camera.zfar or 10.0, grad_f16=grad_f16,
+                   conf_flags=CONF_CLIP_ZO if getattr(params, "depth_zero_to_one", 0) else 0)
 
     def render(self, row0=0, row1=None, nthreads=0):
         """Float RGBA (H, W, 4) and work stats; rows outside [row0, row1) are left at NaN."""

@@ -58,7 +58,7 @@ def test_product_never_reads_the_environment():
 
 def test_library_loads_and_pure_entry_points():
     L = vr_amd.lib()
-    assert L.vr_abi_version() == 7
+    assert L.vr_abi_version() == 8
     p = vr_amd.default_params()
     assert p.step == pytest.approx(0.005) and p.ray_dist == pytest.approx(1.8)
     assert list(p.clear_color) == pytest.approx([0.11, 0.11, 0.11, 1.0])
@@ -83,7 +83,7 @@ def test_library_loads_and_pure_entry_points():
 def test_struct_layouts_match_header():
     # sizes of the ABI structs as declared in vr.h (no padding surprises across the boundary)
     assert C.sizeof(vr_amd.vr_camera) == 4 * (16 + 3 + 3)
-    assert C.sizeof(vr_amd.vr_params) == 4 * (3 + 1 + 4 + 3 + 1 + 5)
+    assert C.sizeof(vr_amd.vr_params) == 4 * (3 + 1 + 4 + 3 + 1 + 6)
     assert C.sizeof(vr_amd.vr_stats) == 40
     src = open(os.path.join(ROOT, "include", "vr", "vr.h")).read()
     test = r"""
@@ -91,8 +91,8 @@ def test_struct_layouts_match_header():
 #include <stdio.h>
 #include <stddef.h>
 #include "vr/vr_debug.h"
-int main(void) { printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(vr_camera), sizeof(vr_params),
-  sizeof(vr_stats), offsetof(vr_params, spec_power), offsetof(vr_params, skip_empty), offsetof(vr_params, frames_in_flight), offsetof(vr_params, exact_gradient),
+int main(void) { printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(vr_camera), sizeof(vr_params),
+  sizeof(vr_stats), offsetof(vr_params, spec_power), offsetof(vr_params, skip_empty), offsetof(vr_params, frames_in_flight), offsetof(vr_params, exact_gradient), offsetof(vr_params, depth_zero_to_one),
   sizeof(vr_memory_info), sizeof(vr_member_timing), offsetof(vr_member_timing, kernel_ms)); return 0; }
 """
     tmp = os.path.join("/tmp", "vr_abi_layout")
@@ -105,9 +105,10 @@ int main(void) { printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(vr_c
                                      vr_amd.vr_params.skip_empty.offset,
                                      vr_amd.vr_params.frames_in_flight.offset,
                                      vr_amd.vr_params.exact_gradient.offset,
+                                     vr_amd.vr_params.depth_zero_to_one.offset,
                                      C.sizeof(vr_amd.vr_memory_info), C.sizeof(vr_amd.vr_member_timing),
                                      vr_amd.vr_member_timing.kernel_ms.offset]
-    assert "VR_ABI_VERSION 7" in src
+    assert "VR_ABI_VERSION 8" in src
 
 
 def test_create_without_device_fails_cleanly():

@@ -330,6 +330,38 @@ def test_near_plane_clips_part_of_the_front_face(rp, radius, rotate):
         check(img, ref)
 
 
+@pytest.mark.parametrize("radius,rotate", [(0.65, (0.0, 0.0)), (0.7, (40.0, 25.0)), (0.75, (60.0, 45.0))])
+def test_clip_forms_both_match_the_oracle(rp, radius, rotate):
+    """vr_params.depth_zero_to_one (ABI 8): glm's [-1, 1] form (0, the
+    reference as built) and its [0, 1] form (1, GLM_FORCE_DEPTH_ZERO_TO_ONE in effect) move the
+    effective near plane from 0.198 to 0.1 (offscreen_pass.cpp:3,1166).  On near views the two
+    frames differ; each is bit-exact against the oracle in the same form (OR_CONF_CLIP_ZO), with
+    the same work counters."""
+    vol = synth.gaussians_numpy((20, 18, 22), seed=9)
+    rp.volume_dataset_changed(synth.dataset(vol))
+    tf = synth.tf_color()
+    rp.transfer_function_changed(tf)
+    W, H = 64, 48
+    rp.framebuffer_size_changed(W, H)
+    cam = vr_amd.make_camera(radius=radius, rotate=rotate).to_vr_camera()
+    frames, rays = {}, {}
+    for zo in (0, 1):
+        for shading in (0, 1):
+            p = vr_amd.default_params(shading=shading, depth_zero_to_one=zo)
+            img = rp.render(cam, p, vr_amd.OUT_RGBA32F)
+            ref, st = oracle_render(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p,
+                                    grad_f16=reads_half(rp, p))
+            assert rp.count_work(cam, p) == st
+            check(img, ref)
+            frames[zo, shading] = img
+            rays[zo] = st["rays"]
+    # the [0, 1] form clips less: never fewer rays, and strictly more on these near views
+    assert rays[1] > rays[0], rays
+    assert not np.array_equal(frames[0, 0], frames[1, 0])
+    with pytest.raises(RuntimeError, match="depth_zero_to_one"):
+        rp.render(cam, vr_amd.default_params(depth_zero_to_one=2))
+
+
 def test_constant_volume_and_large_tf(rp):
     """min == max (0/0 -> NaN density index: texel 0) and a TF beyond the LDS stage (1000 texels)."""
     W, H = 40, 30

@@ -135,8 +135,9 @@ struct vr_ctx {
     // of a multi-device context (vr_set_row_share; vr_internal.h RowShare)
     RowShare share{1, 1};
     // device bytes the derived structures (difference field, alternative copies, skip-empty
-    // classification) may take together (vr_set_memory_budget); ~0 = the default policy
-    uint64_t budget = ~0ull;
+    // classification) may take together (vr_set_memory_budget): VR_MEMORY_BUDGET_DEFAULT
+    // (kDerivedBudgetBricks x the bricks), VR_MEMORY_BUDGET_UNLIMITED, or a byte count
+    uint64_t budget = VR_MEMORY_BUDGET_DEFAULT;
     std::string err;
 };
 
@@ -232,6 +233,18 @@ void perspective_rh_no(float fovy, float aspect, float zn, float zf, float *m)
     m[14] = -(2.0f * zf * zn) / (zf - zn);
 }
 
+// glm::perspectiveRH_ZO (GLM_FORCE_DEPTH_ZERO_TO_ONE in effect; vr_params.depth_zero_to_one)
+void perspective_rh_zo(float fovy, float aspect, float zn, float zf, float *m)
+{
+    std::memset(m, 0, 16 * sizeof(float));
+    const float th = std::tan(fovy / 2.0f);
+    m[0] = 1.0f / (aspect * th);
+    m[5] = 1.0f / th;
+    m[10] = zf / (zn - zf);
+    m[11] = -1.0f;
+    m[14] = -(zf * zn) / (zf - zn);
+}
+
 void coordinate_conversion(float *m)
 {
     const float angle = 90.0f * 0.01745329251994329576923690768489f;
@@ -301,7 +314,9 @@ bool inverse4d(const double *m, double *inv)
 
 // update_uniform_buffer (offscreen_pass.cpp:1152-1169): proj = perspectiveRH(fovy, W/H, n, f)
 // * coordinate_conversion; the kernel needs inverse(proj * view) (volume.vert:23 order).
-bool unprojection(const vr_camera *cam, uint32_t W, uint32_t H, double *inv)
+// zo: glm's [0, 1] clip form (perspectiveRH_ZO) instead of its default [-1, 1] (_NO); the
+// kernel clips at 0 <= z_ndc <= 1 (Vulkan) either way, so only the near plane moves.
+bool unprojection(const vr_camera *cam, uint32_t W, uint32_t H, bool zo, double *inv)
 {
     const float fovy = (cam->fovy_deg > 0.0f ? cam->fovy_deg : 40.0f) *
                        0.01745329251994329576923690768489f;
@@ -309,7 +324,10 @@ bool unprojection(const vr_camera *cam, uint32_t W, uint32_t H, double *inv)
     const float zf = cam->zfar > 0.0f ? cam->zfar : 10.0f;
     const float aspect = (float)W / (float)H;
     float persp[16], conv[16], proj[16], pv[16];
-    perspective_rh_no(fovy, aspect, zn, zf, persp);
+    if (zo)
+        perspective_rh_zo(fovy, aspect, zn, zf, persp);
+    else
+        perspective_rh_no(fovy, aspect, zn, zf, persp);
     coordinate_conversion(conv);
     glm_mul(persp, conv, proj);
     glm_mul(proj, cam->view, pv);
@@ -488,6 +506,8 @@ int check_params(vr_ctx *c, const vr_params *p)
         return fail(c, VR_EINVAL, "params.frames_in_flight must be in [0, 16]");
     if (p->exact_gradient != 0 && p->exact_gradient != 1)
         return fail(c, VR_EINVAL, "params.exact_gradient must be 0 or 1");
+    if (p->depth_zero_to_one != 0 && p->depth_zero_to_one != 1)
+        return fail(c, VR_EINVAL, "params.depth_zero_to_one must be 0 or 1");
     const float n = p->ray_dist / p->step;
     if (n > 1.0e8f) return fail(c, VR_EINVAL, "params.ray_dist / step too large");
     return VR_OK;
@@ -611,7 +631,7 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     if (nranks == 0 || rank >= nranks || row_block == 0)
         return fail(c, VR_EINVAL, "bad shard (row_block, rank, nranks)");
     std::memset(&P, 0, sizeof(P));
-    if (!unprojection(cam, c->width, c->height, P.inv))
+    if (!unprojection(cam, c->width, c->height, p->depth_zero_to_one != 0, P.inv))
         return fail(c, VR_EINVAL, "proj * view is singular");
     P.vol = c->bricks;
     P.vol_bytes = c->brick_bytes;
@@ -698,13 +718,24 @@ size_t derived_bytes(const vr_ctx *c)
         if (a.bricks) b += a.bytes + kBrickSlackBytes;
     return b + c->nbricks_alloc * kSkipBytesPerBrick;
 }
+// The default budget: the difference field (3x the bricks) plus one alternative copy (about 1x),
+// plus the skip-empty classification -- at C3 the field and the default camera's stencil copy
+// (5.6 GB beside 1.6 GB of bricks) fit, and a third structure evicts a copy.
+constexpr uint64_t kDerivedBudgetBricks = 4;
+uint64_t effective_budget(const vr_ctx *c)
+{
+    if (c->budget != VR_MEMORY_BUDGET_DEFAULT) return c->budget;
+    // + brick_bytes / 32: the skip-empty classification, 10 B per brick of >= 648 B
+    return kDerivedBudgetBricks * (uint64_t)c->brick_bytes + (uint64_t)c->brick_bytes / 32 +
+           64ull * kBrickSlackBytes;
+}
 // Would adding `extra` bytes (replacing `replaced` bytes of the same structure) stay within the
-// budget?  The default budget (~0) always allows; the 2 GiB free-memory reserve applies apart.
+// budget?  VR_MEMORY_BUDGET_UNLIMITED always allows; the 2 GiB free-memory reserve applies apart.
 bool budget_allows(const vr_ctx *c, size_t extra, size_t replaced)
 {
-    if (c->budget == ~0ull) return true;
+    if (c->budget == VR_MEMORY_BUDGET_UNLIMITED) return true;
     const size_t now = derived_bytes(c) - replaced;
-    return now + extra <= c->budget;
+    return now + extra <= effective_budget(c);
 }
 // Free every alternative copy but `keep` (frames in flight may still read them: the device
 // drains first, as for any resource swap).
@@ -1757,7 +1788,7 @@ int vr_set_memory_budget(vr_ctx *c, uint64_t bytes)
     }
     if (int rc = wait_idle(c)) return rc;  // frames in flight may read what is freed
     c->budget = bytes;
-    if (derived_bytes(c) > bytes) free_derived(c);
+    if (bytes != VR_MEMORY_BUDGET_UNLIMITED && derived_bytes(c) > effective_budget(c)) free_derived(c);
     return VR_OK;
 }
 
@@ -1773,7 +1804,7 @@ int vr_memory_report(const vr_ctx *c, vr_memory_info *out)
         *copies[i] = c->alt[i].bricks ? c->alt[i].bytes + kBrickSlackBytes : 0;
     out->skip_bytes = c->nbricks_alloc * kSkipBytesPerBrick;
     out->derived_bytes = derived_bytes(c);
-    out->budget_bytes = c->budget;
+    out->budget_bytes = c->budget == VR_MEMORY_BUDGET_UNLIMITED ? c->budget : effective_budget(c);
     return VR_OK;
 }
 

@@ -48,7 +48,8 @@ class vr_params(C.Structure):
                 ("ambient", C.c_float), ("diffuse", C.c_float), ("specular", C.c_float),
                 ("spec_power", C.c_int32), ("tile_order", C.c_int32),
                 ("skip_empty", C.c_int32), ("wave_shape", C.c_int32),
-                ("frames_in_flight", C.c_int32), ("exact_gradient", C.c_int32)]
+                ("frames_in_flight", C.c_int32), ("exact_gradient", C.c_int32),
+                ("depth_zero_to_one", C.c_int32)]
 
 
 class vr_stats(C.Structure):
@@ -116,7 +117,7 @@ KNOBS = {"pipeline": 1, "pair": 2, "pair_lanes": 3, "grad_field": 4, "u8_layout"
 KNOB_AUTO = {"pipeline": -1, "pair": -1, "pair_lanes": 0, "grad_field": -1,
              "u8_layout": -1, "tile_order": 0, "narrow": 1, "alt_geometry": -1}
 
-ABI_VERSION = 7  # include/vr/vr.h VR_ABI_VERSION
+ABI_VERSION = 8  # include/vr/vr.h VR_ABI_VERSION
 _LIB = None
 
 
