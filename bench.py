@@ -403,8 +403,8 @@ def cpu_baseline_other(name, device, budget_s, nthreads):
 def load_traffic(cfg_name, world, kernel, layout):
     """Measured HBM bytes per frame (rocprofv3 PMC, profiles/pmc_traffic.json written by
     tools/traffic_json.py from tools/measure_round.sh) for this config: (bytes, source, status).
-    The entry counts only if it was measured on the kernel this run launches, from the same
-    kernel sources (vr_amd.kernel_source_hash) and the same volume layout; otherwise bytes is
+    The entry counts only if it was measured on the kernel this run launches, in the same
+    device code (vr_amd.kernel_code_hash) and the same volume layout; otherwise bytes is
     None and status says why ("stale: ...")."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
@@ -415,7 +415,7 @@ def load_traffic(cfg_name, world, kernel, layout):
         return None, None, f"unreadable: {ex}"
     if not e:
         return None, None, f"missing: no entry for {cfg_name}"
-    want = dict(n_gpus=world, kernel=kernel, source_hash=vr_amd.kernel_source_hash(), layout=layout)
+    want = dict(n_gpus=world, kernel=kernel, code_hash=vr_amd.kernel_code_hash(), layout=layout)
     for k, v in want.items():
         if e.get(k) != v:
             return None, e.get("source"), f"stale: {k} {e.get(k)!r} != this run's {v!r}"
@@ -805,7 +805,7 @@ def main():
                 "frac": round(traffic / frame_s / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
                 "traffic": traffic,
                 "traffic_status": traffic_status,
-                "kernel_source_hash": vr_amd.kernel_source_hash(),
+                "kernel_code_hash": vr_amd.kernel_code_hash(),
                 "volume_layout": layout,
                 "traffic_source": (f"profiles/pmc_traffic.json ({traffic_src}): rocprofv3 --pmc "
                                    "FETCH_SIZE x2 + WRITE_SIZE per frame launch") if traffic else None,

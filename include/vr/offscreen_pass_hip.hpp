@@ -141,6 +141,20 @@ class BasicOffscreenPass {
     using Sampler = typename Traits::Sampler;
     using ImageView = typename Traits::ImageView;
 
+    // The host's glm clip form (vr_params.depth_zero_to_one, ABI 8).  glm fixes it when it is
+    // first included (setup.hpp: GLM_CONFIG_CLIP_CONTROL from GLM_FORCE_DEPTH_ZERO_TO_ONE), so
+    // read glm's own configuration when glm came before this header; without glm the default
+    // [-1, 1] form -- the reference's build, whose define at offscreen_pass.cpp:3 comes after
+    // glm's first include through offscreen_pass.h:3.
+    static constexpr int32_t host_depth_zero_to_one()
+    {
+#if defined(GLM_CONFIG_CLIP_CONTROL) && defined(GLM_CLIP_CONTROL_ZO_BIT)
+        return (GLM_CONFIG_CLIP_CONTROL & GLM_CLIP_CONTROL_ZO_BIT) ? 1 : 0;
+#else
+        return 0;
+#endif
+    }
+
     // offscreen_pass.cpp:112-134 (the GPUs: Traits::device_mask() if declared, else `device`)
     explicit BasicOffscreenPass(Context *context, uint32_t width, uint32_t height, int device = 0)
         : ctx_(detail::create_ctx(detail::traits_device_mask<Traits>(), device, width, height)),
@@ -148,6 +162,7 @@ class BasicOffscreenPass {
     {
         if (!ctx_) throw std::runtime_error(std::string("vr_create: ") + vr_last_error(nullptr));
         vr_params_default(&params_);
+        params_.depth_zero_to_one = host_depth_zero_to_one();
     }
     // every frame split over the devices of `mask` (vr_create_mask)
     BasicOffscreenPass(Context *context, uint32_t width, uint32_t height, DeviceMask mask)
@@ -156,6 +171,7 @@ class BasicOffscreenPass {
     {
         if (!ctx_) throw std::runtime_error(std::string("vr_create_mask: ") + vr_last_error(nullptr));
         vr_params_default(&params_);
+        params_.depth_zero_to_one = host_depth_zero_to_one();
     }
     uint32_t device_mask() const
     {

@@ -147,7 +147,7 @@ def test_no_cpu_fallback_in_product():
 def test_stale_pmc_traffic_is_never_used():
     """bench.py's roofline divides measured HBM bytes (profiles/pmc_traffic.json) by its frame
     period only when the entry was measured on this kernel, these kernel sources
-    (vr_amd.kernel_source_hash) and this volume layout: any mismatch gives traffic None and a
+    (vr_amd.kernel_code_hash) and this volume layout: any mismatch gives traffic None and a
     "stale: ..." status in the bench line, never old bytes."""
     import json
     import bench
@@ -156,29 +156,28 @@ def test_stale_pmc_traffic_is_never_used():
     assert e["hbm_bytes_per_launch"] > 0 and e["layout"].startswith("st4:")
     good = dict(world=e["n_gpus"], kernel=e["kernel"], layout=e["layout"])
     byts, _, status = bench.load_traffic("c3", **good)
-    if e["source_hash"] == vr_amd.kernel_source_hash():
+    if e.get("code_hash") == vr_amd.kernel_code_hash():
         assert status == "ok" and byts == float(e["hbm_bytes_per_launch"])
     else:
-        assert byts is None and status.startswith("stale: source_hash")
+        assert byts is None and status.startswith("stale: code_hash")
     for k, v in (("world", e["n_gpus"] + 1), ("kernel", "other"), ("layout", "st4:1")):
         byts, _, status = bench.load_traffic("c3", **dict(good, **{k: v}))
         assert byts is None and status.startswith("stale:"), (k, status)
     assert bench.load_traffic("no_such_config", **good)[2].startswith("missing:")
 
 
-def test_committed_pmc_traffic_matches_the_kernel_sources():
-    """profiles/pmc_traffic.json was measured on these kernel sources: the C3 entries carry the
-    current vr_amd.kernel_source_hash, so a kernel change cannot leave a stale roofline behind
-    unnoticed (re-measure with tools/measure_round.sh on the GPU).  While a re-measurement is
-    pending this reports XFAIL, naming the hashes (bench.py then prints traffic null with a
-    "stale" status, test_stale_pmc_traffic_is_never_used)."""
+def test_committed_pmc_traffic_matches_the_kernel_code():
+    """profiles/pmc_traffic.json was measured on this library's device code: every config entry
+    carries the current vr_amd.kernel_code_hash (the .hip_fatbin bytes), so a kernel change
+    cannot leave a stale roofline behind (re-measure with tools/measure_round.sh on the GPU).
+    No xfail: a stale entry fails here; host-only edits do not move the hash."""
     import json
     d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
-    now = vr_amd.kernel_source_hash()
-    stale = [cfg for cfg in ("c3", "c3_default", "c3_ref") if d[cfg]["source_hash"] != now]
-    if stale:
-        pytest.xfail(f"PMC traffic measured on kernel sources {d['c3']['source_hash']}, "
-                     f"now {now}: re-measure pending (tools/measure_round.sh) for {stale}")
-    for cfg in ("c3", "c3_default", "c3_ref"):
+    now = vr_amd.kernel_code_hash()
+    for cfg in ("c3", "c3_default", "c3_ref", "c2", "c4", "c5"):
+        assert cfg in d, f"no PMC traffic for {cfg}"
         e = d[cfg]
-        assert e["hbm_bytes_per_launch"] > 0 and e["layout"].startswith("st4:")
+        assert e.get("code_hash") == now, (cfg, e.get("code_hash"), now)
+        assert e["hbm_bytes_per_launch"] > 0
+    for cfg in ("c3", "c3_default", "c3_ref"):
+        assert d[cfg]["layout"].startswith("st4:")

@@ -81,3 +81,36 @@ def test_frame_rendered_into_imported_memory(gpu, mask):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "match=1" in r.stdout and "guard=1" in r.stdout
     assert "fd_open_after_release=1" in r.stdout  # the caller keeps the fd (vr.h)
+
+
+def test_shim_takes_the_clip_form_from_glms_configuration():
+    """vr_params.depth_zero_to_one (ABI 8) in the shim: glm's GLM_CONFIG_CLIP_CONTROL (fixed at
+    glm's first include) selects it; without glm, or in glm's default [-1, 1] form, it is 0 --
+    the reference's build (offscreen_pass.cpp:3 defines GLM_FORCE_DEPTH_ZERO_TO_ONE after glm
+    came in through offscreen_pass.h:3).  glm is an un-vendored submodule of the reference, so
+    its setup.hpp macros are stated here as glm >= 0.9.9 defines them."""
+    src = os.path.join("/tmp", "vr_shim_clip.cpp")
+    exe = os.path.join("/tmp", "vr_shim_clip")
+    body = r"""
+#include <vr/offscreen_pass_hip.hpp>
+#include <cstdio>
+int main() { std::printf("%d\n", (int)Vol::Rendering::Hip::OffscreenPass::host_depth_zero_to_one()); return 0; }
+"""
+    outs = {}
+    for name, pre in (("none", ""),
+                      ("glm_no", "#define GLM_CLIP_CONTROL_ZO_BIT (1 << 0)\n#define GLM_CLIP_CONTROL_NO_BIT (1 << 1)\n"
+                                 "#define GLM_CLIP_CONTROL_RH_BIT (1 << 3)\n"
+                                 "#define GLM_CONFIG_CLIP_CONTROL (GLM_CLIP_CONTROL_RH_BIT | GLM_CLIP_CONTROL_NO_BIT)\n"),
+                      ("glm_zo", "#define GLM_CLIP_CONTROL_ZO_BIT (1 << 0)\n#define GLM_CLIP_CONTROL_RH_BIT (1 << 3)\n"
+                                 "#define GLM_CONFIG_CLIP_CONTROL (GLM_CLIP_CONTROL_RH_BIT | GLM_CLIP_CONTROL_ZO_BIT)\n")):
+        with open(src, "w") as f:
+            f.write(pre + body)
+        r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-I", os.path.join(ROOT, "include"), src],
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr[-3000:]
+        r = subprocess.run(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), src, "-o", exe,
+                            "-L", LIBDIR, "-lvr_amd", "-Wl,-rpath," + LIBDIR],
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr[-3000:]
+        outs[name] = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.strip()
+    assert outs == {"none": "0", "glm_no": "0", "glm_zo": "1"}

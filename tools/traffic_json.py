@@ -85,7 +85,7 @@ def main():
         rf = b.get("roofline", {})
         if rf.get("kernel") and rf["kernel"] != kern:
             print(f"{cfg}: profiled kernel {kern} != bench's {rf['kernel']}", file=sys.stderr)
-        res[cfg] = dict(n_gpus=1, kernel=kern, source_hash=rf.get("kernel_source_hash"),
+        res[cfg] = dict(n_gpus=1, kernel=kern, code_hash=rf.get("kernel_code_hash"),
                         layout=rf.get("volume_layout"), dispatches=n, fetch_size_kb=f, write_size_kb=w,
                         hbm_bytes_per_launch=2 * f * 1024 + (w or 0) * 1024,
                         method="rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate runs of "

@@ -830,7 +830,8 @@ bool ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s, bool half)
         }
         c->grad_valid = false;
     }
-    const size_t bytes = c->brick_bytes / element_size(ST_F32) * kGradElemBytes;
+    const size_t bytes =
+        c->brick_bytes / element_size(ST_F32) * (half ? kHalfGradElemBytes : kGradElemBytes);
     if (!c->grad || c->grad_bytes != bytes) {
         if (c->grad) hipFree(c->grad);
         c->grad = nullptr;

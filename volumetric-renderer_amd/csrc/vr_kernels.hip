@@ -26,6 +26,7 @@
 #include "vr_exact_math.h"
 #include "vr_internal.h"
 
+#include <atomic>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -36,6 +37,7 @@ namespace vr {
 namespace {
 
 constexpr int kTile = 16;       // pixels per workgroup side
+constexpr int kMaxDevices = 64;  // per-device launch caches
 constexpr int kThreads = 256;   // lane-pair kernel workgroup: 4 waves
 constexpr int kTfLds = 256;     // TF texels staged in LDS
 constexpr int kTfLut = 2 * (kTfLds + 2);  // float4s of the staged LUT (tf_lookup: + 2 sentinels)
@@ -682,7 +684,11 @@ struct FieldRowsT {
 };
 template <>
 struct FieldRowsT<true> {
+#if VR_FIELD_PLAIN
+    u4a r[4];  // rows (y|y+1, z|z+1), r = dy + 2 dz: {Dx, Dy}(x), {Dz, 0}(x), the same at x + 1
+#else
     u4a a0, a1, a2;
+#endif
 };
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2v h2f(uint32_t w)  // two binary16 -> two f32 (exact)
@@ -692,10 +698,18 @@ __device__ __forceinline__ f2v h2f(uint32_t w)  // two binary16 -> two f32 (exac
 __device__ __forceinline__ void field_rows_load(const char *__restrict__ gbase, size_t e,
                                                 FieldRowsT<true> &r)
 {
+#if VR_FIELD_PLAIN
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        r.r[q] = *reinterpret_cast<const u4a *>(
+            gbase + (e + (size_t)((q & 1) * GeomWide::Row + (q >> 1) * GeomWide::Slice)) *
+                        kHalfGradElemBytes);
+#else
     const char *p = gbase + e * kGradElemBytes;
     r.a0 = *reinterpret_cast<const u4a *>(p);
     r.a1 = *reinterpret_cast<const u4a *>(p + 16);
     r.a2 = *reinterpret_cast<const u4a *>(p + 32);
+#endif
 }
 // The f32 path's filter (below) on the converted pairs: per axis a, words 2a / 2a + 1 of
 // element x are the y / y + 1 pairs {D(z), D(z+1)}, words 6 + 2a / 7 + 2a those of x + 1.
@@ -722,6 +736,24 @@ __device__ __forceinline__ float mix_lerp(uint32_t a, uint32_t b, float w)
 __device__ __forceinline__ void field_rows_filter(const FieldRowsT<true> &r, float ax, float ay,
                                                   float az, float &gx, float &gy, float &gz)
 {
+#if VR_FIELD_PLAIN
+    // per axis: the x lerps of the four rows (x in word 0|1 of the 16 B, x + 1 in word 2|3; the
+    // axis' half selected in place), then y over {z, z + 1} pairs and z: tri8's order
+    auto axis = [&](int a) {
+        const int wo = a == 2 ? 1 : 0;  // Dx, Dy in word 0 / 2 (lo, hi); Dz in word 1 / 3 (lo)
+        auto xl = [&](const u4a &q) {
+            const uint32_t lo = wo ? q.y : q.x, hi = wo ? q.w : q.z;
+            return a == 1 ? mix_lerp<true>(lo, hi, ax) : mix_lerp<false>(lo, hi, ax);
+        };
+        const f2v c0 = {xl(r.r[0]), xl(r.r[2])};  // row y: z, z + 1
+        const f2v c1 = {xl(r.r[1]), xl(r.r[3])};  // row y + 1
+        const f2v q = lerp2(c0, c1, ay);
+        return lerpf(q.x, q.y, az);
+    };
+    gx = axis(0);
+    gy = axis(1);
+    gz = axis(2);
+#else
     const uint32_t w[12] = {r.a0.x, r.a0.y, r.a0.z, r.a0.w, r.a1.x, r.a1.y,
                             r.a1.z, r.a1.w, r.a2.x, r.a2.y, r.a2.z, r.a2.w};
     auto axis = [&](int a) {
@@ -740,6 +772,7 @@ __device__ __forceinline__ void field_rows_filter(const FieldRowsT<true> &r, flo
     gx = axis(0);
     gy = axis(1);
     gz = axis(2);
+#endif
 }
 __device__ __forceinline__ void field_rows_load(const char *__restrict__ gbase, size_t e,
                                                 FieldRowsT<false> &r)
@@ -2009,6 +2042,17 @@ __global__ __launch_bounds__(256) void grad_field_kernel(const float *__restrict
         uint32_t bx, by, bz;
         brick_coords((uint32_t)bidx, nbx, nby, bx, by, bz);
         const int x = (int)(bx * G::BX + lx), y = (int)(by * G::BY + lyy), z = (int)(bz * G::BZ + lz);
+        if constexpr (H && VR_FIELD_PLAIN) {
+            auto V = [&](int dx, int dy, int dz) {
+                return padded_voxel(bricks, x + dx, y + dy, z + dz, nx, ny, nz, nbx, nby);
+            };
+            const h2v xy = {field_half(V(1, 0, 0) - V(-1, 0, 0), scale),
+                            field_half(V(0, 1, 0) - V(0, -1, 0), scale)};
+            const h2v zw = {field_half(V(0, 0, 1) - V(0, 0, -1), scale), (_Float16)0.0f};
+            reinterpret_cast<uint2 *>(grad)[g] =
+                make_uint2(__builtin_bit_cast(uint32_t, xy), __builtin_bit_cast(uint32_t, zw));
+            continue;
+        }
         if constexpr (H) {
             _Float16 hv[12];
 #pragma unroll
@@ -2174,17 +2218,23 @@ hipError_t launch_march_t(const MarchParams &p, hipStream_t stream)
     if constexpr (!COUNT && !SKIP) {
         if (p.queue) {  // tile_order 5: the persistent wavefront queue (host: a strip permutation)
             if (p.tiles_x * p.tiles_y == 0) return hipSuccess;
-            // as many workgroups as the chip holds at once (occupancy x CUs), once per variant
-            static unsigned grid = 0;
+            // as many workgroups as the device holds at once (occupancy x CUs), once per variant
+            // and device: frame-worker threads of a multi-device context launch concurrently
+            // (ADVICE r4), so the cache is per device and atomic
+            static std::atomic<unsigned> grids[kMaxDevices];
+            int dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices)
+                return hipErrorInvalidValue;
+            unsigned grid = grids[dev].load(std::memory_order_relaxed);
             if (grid == 0) {
-                int per_cu = 0, dev = 0, cus = 0;
+                int per_cu = 0, cus = 0;
                 if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
                         &per_cu, march_queue_kernel<VT, SHADE, GF, PIPE>, kThreadsPerTile, 0) != hipSuccess ||
-                    hipGetDevice(&dev) != hipSuccess ||
                     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
                     per_cu <= 0 || cus <= 0)
                     return hipErrorInvalidValue;
                 grid = (unsigned)(per_cu * cus);
+                grids[dev].store(grid, std::memory_order_relaxed);  // same value from any thread
             }
             hipLaunchKernelGGL((march_queue_kernel<VT, SHADE, GF, PIPE>), dim3(grid),
                                dim3(kThreadsPerTile), 0, stream, p);

@@ -675,14 +675,33 @@ KERNEL_SOURCES = ("csrc/vr_kernels.hip", "csrc/vr_internal.h", "csrc/vr_exact_ma
 
 
 def kernel_source_hash() -> str:
-    """sha256 (16 hex digits) of the kernel sources: keys measured per-kernel figures (the PMC
-    traffic bench.py's roofline reads) to the code they were measured on."""
+    """sha256 (16 hex digits) of the kernel sources (round 4's key; kept for the record)."""
     import hashlib
     h = hashlib.sha256()
     for rel in KERNEL_SOURCES:
         with open(os.path.join(HERE, rel), "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:16]
+
+
+def kernel_code_hash(path: Optional[str] = None) -> str:
+    """sha256 (16 hex digits) of the device code the library carries: the bytes of its
+    `.hip_fatbin` ELF section (every gfx950 code object of the build).  Keys measured
+    per-kernel figures (the PMC traffic bench.py's roofline reads) to the machine code they
+    were measured on: host-only edits leave it unchanged, any kernel change moves it (the
+    build is deterministic: two builds of the same sources give the same bytes)."""
+    import hashlib
+    import struct
+    b = open(path or LIB_PATH, "rb").read()
+    shoff = struct.unpack_from("<Q", b, 0x28)[0]
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", b, shoff + i * shentsize) for i in range(shnum)]
+    names_off = secs[shstrndx][4]
+    for name_i, _, _, _, off, size, *_ in secs:
+        end = b.index(b"\0", names_off + name_i)
+        if b[names_off + name_i:end] == b".hip_fatbin":
+            return hashlib.sha256(b[off:off + size]).hexdigest()[:16]
+    raise RuntimeError(f"{path or LIB_PATH} has no .hip_fatbin section")
 
 
 def shard_rows(height: int, row_block: int, nranks: int) -> int:
