@@ -398,6 +398,8 @@ int narrow_storage(vr_ctx *c, const void *data_dev, int dtype, size_t count, hip
     return VR_OK;
 }
 
+void free_derived(vr_ctx *c);
+
 // (Re)allocate the bricked volume for layout code `storage`.
 int set_bricks(vr_ctx *c, int storage, uint32_t nx, uint32_t ny, uint32_t nz, void **out)
 {
@@ -410,6 +412,9 @@ int set_bricks(vr_ctx *c, int storage, uint32_t nx, uint32_t ny, uint32_t nz, vo
         *out = c->bricks;
         return VR_OK;
     }
+    // another volume size: the derived structures' allocations (sized for the old volume) would
+    // hold budget and memory they can no longer use (the caller drained the device)
+    free_derived(c);
     if (c->bricks) {
         hipFree(c->bricks);
         c->bricks = nullptr;
@@ -837,9 +842,14 @@ bool ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s, bool half)
         c->grad = nullptr;
         c->grad_bytes = 0;
         c->grad_valid = false;
+        // over the budget: the alternative copies (other views') make room first, as one
+        // copy evicts another (ensure_alt); the field serves the dense-row view drawn now
+        if (!budget_allows(c, bytes, 0)) {
+            if (evict_alt_except(c, -1, s) != VR_OK) return built;
+            if (!budget_allows(c, bytes, 0)) return built;
+        }
         size_t free_b = 0, total_b = 0;
-        if (!budget_allows(c, bytes, 0) || hipMemGetInfo(&free_b, &total_b) != hipSuccess ||
-            free_b < bytes + (2ull << 30))
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < bytes + (2ull << 30))
             return built;
         void *g = nullptr;
         if (hipMalloc(&g, bytes) != hipSuccess) {
