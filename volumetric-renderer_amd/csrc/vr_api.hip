@@ -964,8 +964,17 @@ int ensure_alt(vr_ctx *c, int lay, hipStream_t s, bool *ready)
         const size_t had = a.bricks ? a.bytes + kBrickSlackBytes : 0;
         if (!budget_allows(c, bytes + kBrickSlackBytes, had)) {
             // over the budget: drop the other views' copies (the next view change rebuilds
-            // them) if that makes room, else this frame reads the 8^3 bricks (same pixels)
+            // them), then the difference field (read only by dense-row views, never by a frame
+            // that reads a copy), if that makes room; else this frame reads the 8^3 bricks
+            // (same pixels)
             if (int rc = evict_alt_except(c, alt_index(lay), s)) return rc;
+            if (!budget_allows(c, bytes + kBrickSlackBytes, had) && c->grad) {
+                HIP_TRY(c, hipDeviceSynchronize(), "hipDeviceSynchronize (evict field)");
+                hipFree(c->grad);
+                c->grad = nullptr;
+                c->grad_bytes = 0;
+                c->grad_valid = false;
+            }
             if (!budget_allows(c, bytes + kBrickSlackBytes, had)) return VR_OK;
         }
         if (a.bricks) hipFree(a.bricks);
