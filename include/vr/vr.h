@@ -109,7 +109,8 @@ typedef struct vr_params {
      * 0 auto (= 4), 1 raster (consecutive tiles round-robin over the 8 XCDs), 2 XCD bands
      * (each XCD a contiguous band of rows), 3 XCD-interleaved 64x64-pixel super-tiles,
      * 4 adaptive: as 3, each XCD's tiles dispatched longest first by the durations the
-     * previous launch of the same tile geometry recorded (the first launch runs as 3). */
+     * previous launch of the same tile geometry recorded (the first launch runs as 3).
+     * 5 (ABI 7, the wavefront work queue) runs as 4 since ABI 8 (measured 2-4x slower). */
     int32_t tile_order;
     /* 1: skip the trilinear fetch of samples proven fully transparent: the sample's cell lies
      * in an 8^3 brick whose stored value range (widened by a rounding margin) maps only to TF

@@ -231,60 +231,5 @@ def test_budget_between_copies_evicts_and_prepare_builds_ahead(gpu):
         rp.close()
 
 
-# ---- wavefront work queue (tile_order 5) ------------------------------------------------------
-
-@pytest.mark.parametrize("dtype", [np.float32, np.uint8])
-def test_queue_order_renders_the_same_frames(gpu, dtype):
-    """tile_order 5 (march_queue_kernel: a persistent grid whose wavefronts pull strips from
-    their XCD's longest-first list and steal from the others) renders every view and kernel
-    variant byte-identical to the adaptive workgroup order, launch after launch (the queue heads
-    reset by the last wavefront), on several streams at once, and as a rank's share."""
-    import torch
-    W, H = 200, 150
-    vol = synth.gaussians_numpy((70, 64, 60), seed=9)
-    if dtype == np.uint8:
-        vol = np.clip(np.rint(vol / vol.max() * 255), 0, 255).astype(np.uint8)
-    else:
-        vol = vol.astype(np.float32)
-    rp = vr_amd.OffscreenPass(W, H, device=0)
-    try:
-        rp.volume_dataset_changed(synth.dataset(vol))
-        rp.transfer_function_changed(synth.tf_band(0.1, 0.9))
-        for camname in ("fill", "default", "diag", "rotA"):
-            cam = synth.camera(camname).to_vr_camera()
-            for shading in (0, 1):
-                for exact in (0, 1):
-                    base = vr_amd.default_params(shading=shading, ert_eps=1e-5, exact_gradient=exact,
-                                                 frames_in_flight=3)
-                    q = vr_amd.default_params(shading=shading, ert_eps=1e-5, exact_gradient=exact,
-                                              frames_in_flight=3, tile_order=5)
-                    ref = torch.empty((H, W), dtype=torch.int32, device="cuda")
-                    rp.render_device(cam, base, ref.data_ptr(), vr_amd.OUT_RGBA8, 8, 0, 1)
-                    outs = [torch.zeros((H, W), dtype=torch.int32, device="cuda") for _ in range(3)]
-                    streams = [torch.cuda.Stream() for _ in range(3)]
-                    torch.cuda.synchronize()  # the allocations' fills ran on the null stream
-                    for it in range(9):  # order kernel every 4 launches: sorted strip lists too
-                        k = it % 3
-                        with torch.cuda.stream(streams[k]):  # ordered before that frame
-                            outs[k].zero_()
-                        rp.render_device(cam, q, outs[k].data_ptr(), vr_amd.OUT_RGBA8, 8, 0, 1,
-                                         streams[k].cuda_stream)
-                    torch.cuda.synchronize()
-                    for k in range(3):
-                        assert torch.equal(outs[k], ref), (camname, shading, exact, k)
-        # a rank's share (3 ranks, 8-row blocks) through the queue
-        cam = synth.camera("rotB").to_vr_camera()
-        q = vr_amd.default_params(shading=1, tile_order=5, frames_in_flight=2)
-        full = torch.empty((H, W), dtype=torch.int32, device="cuda")
-        rp.render_device(cam, vr_amd.default_params(shading=1), full.data_ptr(), vr_amd.OUT_RGBA8, 8, 0, 1)
-        sr = rp.shard_rows(H, 8, 3)
-        g = torch.zeros((3, sr, W), dtype=torch.int32, device="cuda")
-        for _ in range(5):
-            for r in range(3):
-                rp.render_device(cam, q, g[r].data_ptr(), vr_amd.OUT_RGBA8, 8, r, 3)
-        out = torch.empty((H, W), dtype=torch.int32, device="cuda")
-        rp.assemble_rows(g.data_ptr(), out.data_ptr(), vr_amd.OUT_RGBA8, 8, 3)
-        torch.cuda.synchronize()
-        assert torch.equal(out, full)
-    finally:
-        rp.close()
+# (The wavefront work queue, tile_order 5, measured 2-4x slower in round 5, is in
+# tools/experiments/r05_pruned/ with its test; tile_order 5 now runs as 4, test_gpu_parity.py.)

@@ -94,8 +94,6 @@ struct vr_ctx {
         uint32_t kernel = 0;  // march variant (tile_kernel_key): its tiles' durations differ
         void *stream = nullptr;
         uint32_t *cost = nullptr, *perm = nullptr, *lists = nullptr;
-        uint32_t *queue = nullptr;  // tile_order 5: the wavefront queue's heads (9 words)
-        uint32_t order = 4;         // 4: tiles per workgroup; 5: strips per wavefront (queue)
         bool have_perm = false;
         uint32_t launches = 0;
     };
@@ -685,7 +683,8 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.share_w = share.w;
     P.tiles_x = (c->width + 15) / 16;
     P.tiles_y = (P.local_rows + kMarchRows - 1) / kMarchRows;
-    P.tile_order = p->tile_order >= 1 && p->tile_order <= 5 ? (uint32_t)p->tile_order : 4u;
+    // 5 (ABI 7's wavefront queue, measured 2-4x slower and removed in round 5) runs as 4
+    P.tile_order = p->tile_order >= 1 && p->tile_order <= 4 ? (uint32_t)p->tile_order : 4u;
     if (p->tile_order == 0 && c->knobs.tile_order >= 1)  // experiment knob: the default order
         P.tile_order = (uint32_t)c->knobs.tile_order;
     // wavefront footprint: 1 8x8, 2 16x4, 3 4x16; auto = 16x4 (x-contiguous brick rows:
@@ -835,8 +834,7 @@ bool ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s, bool half)
         }
         c->grad_valid = false;
     }
-    const size_t bytes =
-        c->brick_bytes / element_size(ST_F32) * (half ? kHalfGradElemBytes : kGradElemBytes);
+    const size_t bytes = c->brick_bytes / element_size(ST_F32) * kGradElemBytes;
     if (!c->grad || c->grad_bytes != bytes) {
         if (c->grad) hipFree(c->grad);
         c->grad = nullptr;
@@ -1021,21 +1019,17 @@ uint32_t tile_kernel_key(const MarchParams &P, bool shading, int layout)
 // P.tile_cost, and P.tile_perm once a permutation exists.
 vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P, void *stream, uint32_t kernel)
 {
-    if (P.tile_order != 4 && P.tile_order != 5) return nullptr;
+    if (P.tile_order != 4) return nullptr;
     auto use = [&P](vr_ctx::TileSched &t) {
         P.tile_cost = t.cost;
         if (t.have_perm) {
             P.tile_perm = t.perm;
             P.nperm = 8 * t.per_xcd;
         }
-        if (t.order == 5) {  // the wavefront queue over the strip lists
-            P.queue = t.queue;
-            P.per_xcd = t.per_xcd;
-        }
     };
     for (auto &t : c->sched)
         if (t.tiles_x == P.tiles_x && t.tiles_y == P.tiles_y && t.pair == P.pair &&
-            t.kernel == kernel && t.order == P.tile_order &&
+            t.kernel == kernel &&
             t.stream == stream && t.row_block == P.row_block && t.rank == P.rank &&
             t.nranks == P.nranks && t.share_w0 == P.share_w0 && t.share_w == P.share_w) {
             use(t);
@@ -1045,7 +1039,6 @@ vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P, void *stream, uint32_t 
         hipFree(c->sched.front().cost);
         hipFree(c->sched.front().perm);
         hipFree(c->sched.front().lists);
-        hipFree(c->sched.front().queue);
         c->sched.erase(c->sched.begin());
     }
     vr_ctx::TileSched t;
@@ -1060,7 +1053,6 @@ vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P, void *stream, uint32_t 
     t.nranks = P.nranks;
     t.share_w0 = P.share_w0;
     t.share_w = P.share_w;
-    t.order = P.tile_order;
     // per-XCD tile lists (tile_order 3's super-tile assignment), padded with ~0
     std::vector<std::vector<uint32_t>> xl(8);
     if (VR_LIST_ORDER == 1) {  // super-tile major
@@ -1078,50 +1070,27 @@ vr_ctx::TileSched *tile_sched(vr_ctx *c, MarchParams &P, void *stream, uint32_t 
                 xl[((ty >> kSuperShift) * P.supers_x + (tx >> kSuperShift)) & 7u].push_back(
                     ty * P.tiles_x + tx);
     }
-    // tile_order 5: the unit is a wavefront's strip, each tile's strips consecutive in its list
-    const uint32_t units = t.order == 5 ? kThreadsPerTile / 64 : 1;
-    if (units > 1)
-        for (auto &l : xl) {
-            std::vector<uint32_t> st;
-            st.reserve(l.size() * units);
-            for (uint32_t tile : l)
-                for (uint32_t w = 0; w < units; ++w) st.push_back(tile * units + w);
-            l.swap(st);
-        }
     for (int x = 0; x < 8; ++x) t.per_xcd = xl[x].size() > t.per_xcd ? (uint32_t)xl[x].size() : t.per_xcd;
     std::vector<uint32_t> lists(8 * (size_t)t.per_xcd, 0xFFFFFFFFu);
     for (int x = 0; x < 8; ++x)
         std::copy(xl[x].begin(), xl[x].end(), lists.begin() + (size_t)x * t.per_xcd);
-    // the queue starts from the lists' own order (perm[x + 8 j] = list x entry j) until the first
-    // durations have been recorded and sorted
-    std::vector<uint32_t> perm0(lists.size(), 0xFFFFFFFFu);
-    for (int x = 0; x < 8; ++x)
-        for (uint32_t j = 0; j < t.per_xcd; ++j) perm0[x + 8 * (size_t)j] = lists[(size_t)x * t.per_xcd + j];
-    const size_t nt = (size_t)P.tiles_x * P.tiles_y * units;
-    // uploads on the frame's stream: a plain hipMemcpy from pageable memory may return before
-    // its DMA lands, and the first launch, on a non-blocking stream, would then read recycled
-    // memory (queue heads past the lists' end: a frame left unwritten).  Pageable sources are
-    // staged before hipMemcpyAsync returns, so the vectors may go out of scope.
+    const size_t nt = (size_t)P.tiles_x * P.tiles_y;
+    // upload on the frame's stream: a plain hipMemcpy from pageable memory may return before its
+    // DMA lands, and the order kernel, on a non-blocking stream, would then read recycled memory.
+    // Pageable sources are staged before hipMemcpyAsync returns, so the vector may go out of
+    // scope.
     hipStream_t hs = static_cast<hipStream_t>(stream);
     if (hipMalloc(&t.cost, nt * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&t.perm, lists.size() * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&t.lists, lists.size() * sizeof(uint32_t)) != hipSuccess ||
         hipMemcpyAsync(t.lists, lists.data(), lists.size() * sizeof(uint32_t),
-                       hipMemcpyHostToDevice, hs) != hipSuccess ||
-        (t.order == 5 &&
-         (hipMalloc(&t.queue, 9 * sizeof(uint32_t)) != hipSuccess ||
-          hipMemsetAsync(t.queue, 0, 9 * sizeof(uint32_t), hs) != hipSuccess ||
-          hipMemcpyAsync(t.perm, perm0.data(), perm0.size() * sizeof(uint32_t),
-                         hipMemcpyHostToDevice, hs) != hipSuccess))) {
+                       hipMemcpyHostToDevice, hs) != hipSuccess) {
         (void)hipGetLastError();
         hipFree(t.cost);
         hipFree(t.perm);
         hipFree(t.lists);
-        hipFree(t.queue);
-        if (P.tile_order == 5) P.tile_order = 4;  // no queue: the workgroup kernel, order-3 mapping
         return nullptr;  // no adaptive order (tile_order 3 mapping)
     }
-    if (t.order == 5) t.have_perm = true;
     c->sched.push_back(t);
     use(c->sched.back());
     return &c->sched.back();
@@ -1209,7 +1178,7 @@ bool knob_value_ok(int knob, int v)
         case VR_KNOB_PAIR_LANES: return v == 0 || v == 2 || v == 4;
         case VR_KNOB_NARROW: return v == 0 || v == 1;
         case VR_KNOB_ALT_GEOMETRY: return v >= -1 && v <= 4 && v != 2;
-        case VR_KNOB_TILE_ORDER: return v >= 0 && v <= 5;
+        case VR_KNOB_TILE_ORDER: return v >= 0 && v <= 4;
         default: return v >= -1 && v <= 1;
     }
 }
@@ -1453,7 +1422,6 @@ void vr_destroy(vr_ctx *c)
         hipFree(t.cost);
         hipFree(t.perm);
         hipFree(t.lists);
-        hipFree(t.queue);
     }
     if (c->counters) hipFree(c->counters);
     if (c->frame_dev) hipFree(c->frame_dev);
@@ -1894,9 +1862,6 @@ int render_device_impl(vr_ctx *c, const vr_camera *cam, const vr_params *p, void
         P.tiles_y = (P.local_rows + th - 1) / th;
         P.supers_total = P.supers_x * ((P.tiles_y + kSuper - 1) / kSuper);
     }
-    // the wavefront queue serves the single-lane kernels without skip-empty (they have a queue
-    // instantiation); lane groups and skip-empty frames keep the adaptive workgroup order
-    if (P.tile_order == 5 && (P.pair || P.skip_empty)) P.tile_order = 4;
     // oblique and sparse f32 views: an alternative-geometry copy (want_alt)
     int layout = c->layout;
     if (const int lay = want_alt(c, p, P); lay != c->layout) {

@@ -356,10 +356,6 @@ struct MarchParams {
     int32_t grad_half;
     float inv_range;        // RN(1 / range) (div_fast)
     uint32_t share_w0, share_w;  // RowShare of the row blocks over nranks
-    // tile_order 5 (march_queue_kernel): per-XCD strip lists in tile_perm (x + 8 j, per_xcd
-    // entries each, ~0 = none), queue heads (9 words, zero between launches), persistent grid
-    uint32_t *queue;
-    uint32_t per_xcd;
     // bytes of the volume copy P.vol points at and of the output buffer (bounds-checking
     // debug builds, -DVR_BOUNDS_CHECK: an out-of-range access is printed and skipped)
     unsigned long long vol_bytes, out_bytes;
@@ -436,14 +432,6 @@ hipError_t launch_minmax(int storage, const void *linear, size_t count, float *m
 constexpr int kSkipCap = 16;
 // f32 gradient field (see MarchParams::grad) from the bricked density: same brick grid.
 constexpr size_t kGradElemBytes = 24;
-// VR_FIELD_PLAIN = 1 (experiment builds, round 5): the binary16 field holds each voxel's
-// differences once, {Dx, Dy, Dz, 0} at (x, y, z) in 8 B (1x the z-pair bricks instead of 3x:
-// 512^3 1.6 instead of 4.8 GB); a shaded sample reads 4 x 16 B (elements x, x + 1 of the rows
-// (y|y+1, z|z+1)) instead of 3.  Same differences, same filter order: identical frames.
-#ifndef VR_FIELD_PLAIN
-#define VR_FIELD_PLAIN 0
-#endif
-constexpr size_t kHalfGradElemBytes = VR_FIELD_PLAIN ? 8 : 24;
 // half: the binary16 field of MarchParams::grad_half, each difference times 2^scale_log2 and
 // clamped to +-65504 (NaN kept) before rounding to nearest even
 hipError_t launch_grad_field(const float *bricks, float *grad, uint32_t nx, uint32_t ny,

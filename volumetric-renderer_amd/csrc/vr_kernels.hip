@@ -26,7 +26,6 @@
 #include "vr_exact_math.h"
 #include "vr_internal.h"
 
-#include <atomic>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -37,7 +36,6 @@ namespace vr {
 namespace {
 
 constexpr int kTile = 16;       // pixels per workgroup side
-constexpr int kMaxDevices = 64;  // per-device launch caches
 constexpr int kThreads = 256;   // lane-pair kernel workgroup: 4 waves
 constexpr int kTfLds = 256;     // TF texels staged in LDS
 constexpr int kTfLut = 2 * (kTfLds + 2);  // float4s of the staged LUT (tf_lookup: + 2 sentinels)
@@ -267,8 +265,6 @@ struct CellRaw {  // generic: the decoded cell itself (loaded and decoded togeth
 template <typename VT>
 struct CellRaw<VT, std::enable_if_t<kZPair<VT> && !kPlainF32<VT>>> {
     f4a r0, r1;  // rows y and y + 1: elements x, x + 1 as z-pairs
-    uint32_t mode;  // kShareF: 0 own loads; 1 / 2 the partner lane loaded row y + 1 / y (r0
-                    // holds this lane's row)
 };
 template <typename VT>
 struct CellRaw<VT, std::enable_if_t<kStencilWide<VT>>> {
@@ -277,59 +273,11 @@ struct CellRaw<VT, std::enable_if_t<kStencilWide<VT>>> {
 template <typename VT>
 struct CellRaw<VT, std::enable_if_t<kPlainByte<VT> && GeomByte::EX == 8>> {
     u4a q0, q1;    // slices z and z + 1: the 16 bytes from the 4-aligned address at or below e
-    uint32_t sh;   // e mod 4 (kShare: the cell's byte in its 8-byte row, 0..6)
-    uint32_t mode; // kShare: 0 own loads; 1 / 2 shared with the partner lane, which loaded
-                   // slice z + 1 / z (this lane's q0 holds the other slice)
+    uint32_t sh;   // e mod 4
 };
 
-// ---- cross-lane sharing of 8-bit cells (VR_U8_SHARE, pipelined plain-byte march) ----------
-// At the C4/C5 pixel spans (0.5-0.8 voxels per pixel) neighbouring lanes mostly sample cells in
-// the same brick row pair.  A lane pair whose cells share the row pair (y, y + 1) of one brick
-// issues ONE 16-B load each -- the two rows of slice z from one lane, of slice z + 1 from the
-// other, both from the 8-aligned row start -- instead of two each, and the lanes trade their
-// load through a cross-lane move before the filter: half the lanes' data returns through the
-// texture data path (TD, busy 0.93 of the C4 frame).  Pairs stay together in the march loop
-// until both rays end, so the partner is active at every exchange.  The cell's voxels and the
-// filter are the same: frames are identical.
-//   VR_U8_SHARE = 1: partners are x-neighbours l, l ^ 1 (DPP quad_perm);
-//   VR_U8_SHARE = 2: partners l, l ^ 32, x-neighbours by a 16x4 lane map with x = 2 (l & 7) +
-//                    (l >> 5), so a shared pair leaves lanes 32-63 (two whole quarter-waves)
-//                    out of its second load (v_permlane32_swap).
-#ifndef VR_U8_SHARE
-#define VR_U8_SHARE 0
-#endif
-template <typename VT>
-constexpr bool kShare = kPlainByte<VT> && GeomByte::EX == 8 && VR_U8_SHARE != 0;
-// VR_F32_SHARE = 1: the same for f32 z-pair cells (x-neighbour lanes l, l ^ 1): a lane pair
-// whose two cells are the same cell loads row y in one lane and row y + 1 in the other and
-// trades them (4 DPP moves), instead of two 16-B loads in each lane.
-#ifndef VR_F32_SHARE
-#define VR_F32_SHARE 0
-#endif
-template <typename VT>
-constexpr bool kShareF = kZPair<VT> && !kPlainF32<VT> && VR_F32_SHARE != 0;
-// the march loop keeps partner lanes stepping together (both rays ended before either leaves)
-template <typename VT>
-constexpr bool kPairStep = kShare<VT> || kShareF<VT>;
-__device__ __forceinline__ uint32_t partner_u32(uint32_t v, uint32_t lane)
-{
-#if VR_U8_SHARE == 2
-    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    return lane < 32 ? r[1] : r[0];
-#else
-    (void)lane;
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // l ^ 1
-#endif
-}
-__device__ __forceinline__ bool share_role(uint32_t lane)
-{
-    return VR_U8_SHARE == 2 ? lane >= 32 : (lane & 1) != 0;
-}
-// bytes x, x + 1 of an 8-byte row held as (lo, hi) (x <= 6), in the low 16 bits
-__device__ __forceinline__ uint32_t row_bytes(uint32_t lo, uint32_t hi, uint32_t x)
-{
-    return x < 4 ? __builtin_amdgcn_alignbyte(hi, lo, x) : hi >> (8 * (x - 4));
-}
+// (Cross-lane sharing of a cell's loads, VR_U8_SHARE for 8-bit and VR_F32_SHARE for f32 cells,
+// measured 1.5-1.8x and 1.6x slower in round 5: tools/experiments/r05_pruned/.)
 
 // the stencil copy with 16-B density loads keeps each row's x - 1 / x + 2 voxels for the
 // gradient (row r = dy + 2 dz)
@@ -684,11 +632,7 @@ struct FieldRowsT {
 };
 template <>
 struct FieldRowsT<true> {
-#if VR_FIELD_PLAIN
-    u4a r[4];  // rows (y|y+1, z|z+1), r = dy + 2 dz: {Dx, Dy}(x), {Dz, 0}(x), the same at x + 1
-#else
     u4a a0, a1, a2;
-#endif
 };
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2v h2f(uint32_t w)  // two binary16 -> two f32 (exact)
@@ -698,18 +642,10 @@ __device__ __forceinline__ f2v h2f(uint32_t w)  // two binary16 -> two f32 (exac
 __device__ __forceinline__ void field_rows_load(const char *__restrict__ gbase, size_t e,
                                                 FieldRowsT<true> &r)
 {
-#if VR_FIELD_PLAIN
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        r.r[q] = *reinterpret_cast<const u4a *>(
-            gbase + (e + (size_t)((q & 1) * GeomWide::Row + (q >> 1) * GeomWide::Slice)) *
-                        kHalfGradElemBytes);
-#else
     const char *p = gbase + e * kGradElemBytes;
     r.a0 = *reinterpret_cast<const u4a *>(p);
     r.a1 = *reinterpret_cast<const u4a *>(p + 16);
     r.a2 = *reinterpret_cast<const u4a *>(p + 32);
-#endif
 }
 // The f32 path's filter (below) on the converted pairs: per axis a, words 2a / 2a + 1 of
 // element x are the y / y + 1 pairs {D(z), D(z+1)}, words 6 + 2a / 7 + 2a those of x + 1.
@@ -736,24 +672,6 @@ __device__ __forceinline__ float mix_lerp(uint32_t a, uint32_t b, float w)
 __device__ __forceinline__ void field_rows_filter(const FieldRowsT<true> &r, float ax, float ay,
                                                   float az, float &gx, float &gy, float &gz)
 {
-#if VR_FIELD_PLAIN
-    // per axis: the x lerps of the four rows (x in word 0|1 of the 16 B, x + 1 in word 2|3; the
-    // axis' half selected in place), then y over {z, z + 1} pairs and z: tri8's order
-    auto axis = [&](int a) {
-        const int wo = a == 2 ? 1 : 0;  // Dx, Dy in word 0 / 2 (lo, hi); Dz in word 1 / 3 (lo)
-        auto xl = [&](const u4a &q) {
-            const uint32_t lo = wo ? q.y : q.x, hi = wo ? q.w : q.z;
-            return a == 1 ? mix_lerp<true>(lo, hi, ax) : mix_lerp<false>(lo, hi, ax);
-        };
-        const f2v c0 = {xl(r.r[0]), xl(r.r[2])};  // row y: z, z + 1
-        const f2v c1 = {xl(r.r[1]), xl(r.r[3])};  // row y + 1
-        const f2v q = lerp2(c0, c1, ay);
-        return lerpf(q.x, q.y, az);
-    };
-    gx = axis(0);
-    gy = axis(1);
-    gz = axis(2);
-#else
     const uint32_t w[12] = {r.a0.x, r.a0.y, r.a0.z, r.a0.w, r.a1.x, r.a1.y,
                             r.a1.z, r.a1.w, r.a2.x, r.a2.y, r.a2.z, r.a2.w};
     auto axis = [&](int a) {
@@ -772,7 +690,6 @@ __device__ __forceinline__ void field_rows_filter(const FieldRowsT<true> &r, flo
     gx = axis(0);
     gy = axis(1);
     gz = axis(2);
-#endif
 }
 __device__ __forceinline__ void field_rows_load(const char *__restrict__ gbase, size_t e,
                                                 FieldRowsT<false> &r)
@@ -1165,8 +1082,7 @@ __device__ __forceinline__ void shade_sample(const MarchParams &P, const char *_
 // not the chip's throughput, sets the time.  Reference-semantics results are identical.
 // One wavefront's strip of a tile (wave index `wave` of the 16 x kMarchRows tile (tile_x,
 // tile_y)): every ray of it marched and its pixels written.  s_tf: the TF staged in LDS (when
-// tf_in_lds).  march_kernel runs one tile per workgroup; march_queue_kernel runs strips pulled
-// from a queue by each wavefront on its own.
+// tf_in_lds).  march_kernel runs one tile per workgroup.
 template <typename VT, bool SHADE, bool COUNT, bool SKIP, bool GF, bool PIPE>
 __device__ __forceinline__ void march_strip(const MarchParams &P, LdsF4 *s_tf,
                                             bool tf_in_lds, uint32_t tile_x, uint32_t tile_y,
@@ -1179,13 +1095,7 @@ __device__ __forceinline__ void march_strip(const MarchParams &P, LdsF4 *s_tf,
     // wavefront -> (ww x wh) pixels, ww = 2^wave_w_shift, together tiling the 16 x kMarchRows tile
     const uint32_t ws = P.wave_w_shift, ww = 1u << ws, wh = 64u >> ws;
     const uint32_t wpr = kTile >> ws;  // wavefronts per tile row
-    uint32_t lx_ = lane & (ww - 1), ly_ = lane >> ws;
-    if constexpr (kShare<VT> && PIPE && VR_U8_SHARE == 2) {
-        if (ws == 4) {  // 16x4: lanes l and l ^ 32 are x-neighbours
-            lx_ = ((lane & 7u) << 1) | (lane >> 5);
-            ly_ = (lane >> 3) & 3u;
-        }
-    }
+    const uint32_t lx_ = lane & (ww - 1), ly_ = lane >> ws;
     const uint32_t px = tile_x * kTile + (wave % wpr) * ww + lx_;
     const uint32_t ly = tile_y * kMarchRows + (wave / wpr) * wh + ly_;
     bool active = px < P.W && ly < P.local_rows;
@@ -1249,61 +1159,7 @@ __device__ __forceinline__ void march_strip(const MarchParams &P, LdsF4 *s_tf,
             S.pk = kk + kPad;
             S.ce = cell_offset<VT>(S.pi, S.pj, S.pk, P.nbx, P.nby);
             if (VR_OOB(3, S.ce * kElemBytes<VT>, P.vol_bytes)) S.ce = 0;
-            if constexpr (kShare<VT> && PIPE) {
-                // the cell's row pair (y, y + 1) of slice z starts at the 8-aligned row start
-                const uint32_t bx = (uint32_t)S.pi % (uint32_t)G::BX;
-                const size_t row = S.ce - bx;
-                const uint32_t plo = partner_u32((uint32_t)row, lane);
-                const uint32_t phi = partner_u32((uint32_t)(row >> 32), lane);
-                const uint32_t pslab = partner_u32(S.slab ? 1u : 0u, lane);
-                const bool shared = S.slab && pslab != 0u && plo == (uint32_t)row &&
-                                    phi == (uint32_t)(row >> 32);
-                const bool role = share_role(lane);
-                S.w.sh = bx;
-                S.w.mode = shared ? (role ? 2u : 1u) : 0u;
-                S.w.q0 = *reinterpret_cast<const u4a *>(vol + row + (shared && role ? G::Slice : 0));
-                if (!shared) S.w.q1 = *reinterpret_cast<const u4a *>(vol + row + G::Slice);
-            } else if constexpr (kShareF<VT> && PIPE) {
-                const uint32_t clo = (uint32_t)S.ce, chi = (uint32_t)(S.ce >> 32);
-                const uint32_t plo = partner_u32(clo, lane);
-                const uint32_t phi = partner_u32(chi, lane);
-                const uint32_t pslab = partner_u32(S.slab ? 1u : 0u, lane);
-                const bool shared = S.slab && pslab != 0u && plo == clo && phi == chi;
-                const bool role = share_role(lane);
-                S.w.mode = shared ? (role ? 2u : 1u) : 0u;
-                S.w.r0 = zpair_load2(vol, S.ce + (shared && role ? (size_t)G::Row : 0));
-                if (!shared) S.w.r1 = zpair_load2(vol, S.ce + G::Row);
-            } else {
-                Cell8<VT>::issue(S.w, vol, S.ce);
-            }
-        };
-        // kShare: the exchange with the partner lane (every loop-active lane runs it) and the
-        // cell's 8 voxels from the row pairs of slices z and z + 1
-        auto decode_shared = [&](const Stage &S, Cell8<VT> &c) {
-            if constexpr (kShare<VT> && PIPE) {
-                const u4a o = {partner_u32(S.w.q0.x, lane), partner_u32(S.w.q0.y, lane),
-                               partner_u32(S.w.q0.z, lane), partner_u32(S.w.q0.w, lane)};
-                const u4a z0 = S.w.mode == 2u ? o : S.w.q0;
-                const u4a z1 = S.w.mode == 1u ? o : (S.w.mode == 2u ? S.w.q0 : S.w.q1);
-                const uint32_t q[4] = {row_bytes(z0.x, z0.y, S.w.sh), row_bytes(z0.z, z0.w, S.w.sh),
-                                       row_bytes(z1.x, z1.y, S.w.sh), row_bytes(z1.z, z1.w, S.w.sh)};
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {  // r = dy + 2 dz
-                    c.v[2 * r] = byte_value<VT>(q[r], 0);
-                    c.v[2 * r + 1] = byte_value<VT>(q[r], 1);
-                }
-            } else if constexpr (kShareF<VT> && PIPE) {
-                auto xf = [&](float v) {
-                    return __uint_as_float(partner_u32(__float_as_uint(v), lane));
-                };
-                const f4a o = {xf(S.w.r0.x), xf(S.w.r0.y), xf(S.w.r0.z), xf(S.w.r0.w)};
-                CellRaw<VT> w;
-                w.r0 = S.w.mode == 2u ? o : S.w.r0;
-                w.r1 = S.w.mode == 1u ? o : (S.w.mode == 2u ? S.w.r0 : S.w.r1);
-                c.decode(w);
-            } else {
-                c.decode(S.w);
-            }
+            Cell8<VT>::issue(S.w, vol, S.ce);
         };
         auto composite = [&](const float4 &sm) -> bool {  // volume.frag:44-45
             cr = cr + (sm.x * sm.w) * T;
@@ -1368,27 +1224,7 @@ __device__ __forceinline__ void march_strip(const MarchParams &P, LdsF4 *s_tf,
         };
         Stage A, B;
         int k = 0;
-        if constexpr (kPairStep<VT>) {
-            // pairs leave together: a lane whose ray ended keeps stepping (stages not ok, dummy
-            // loads, nothing composited) until its partner's ray has ended too
-            prep(A, k);
-            bool done = !A.ok;
-            auto both_done = [&]() { return done && partner_u32(done ? 1u : 0u, lane) != 0u; };
-            if (!both_done())
-                for (;;) {
-                    advance();
-                    prep(B, ++k, !done);
-                    Cell8<VT> c;
-                    decode_shared(A, c);
-                    if (!done) done = consume_cell(A, c) || !B.ok;
-                    if (both_done()) break;
-                    advance();
-                    prep(A, ++k, !done);
-                    decode_shared(B, c);
-                    if (!done) done = consume_cell(B, c) || !A.ok;
-                    if (both_done()) break;
-                }
-        } else {
+        {
             prep(A, k);
             while (A.ok) {  // ping-pong: no register copies between the two stages
                 advance();
@@ -1557,58 +1393,6 @@ __global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<COUNT, SKIP, GF, P
     __syncthreads();
     if (tid == 0) wg_times_record((unsigned long long)wg_start, tile_y * P.tiles_x + tile_x);
 #endif
-}
-
-// ---- wavefront work queue (tile_order 5) -------------------------------------------------------
-// A persistent grid (as many workgroups as fit the chip at once): every wavefront pulls strips
-// (one wavefront's 16x4 part of a tile) from its XCD's list, longest first by the strips' last
-// recorded durations (order_tiles_kernel over strip lists), and when that list is empty steals
-// from the other XCDs' lists.  A workgroup never waits for its slowest wavefront (tiles of a
-// sparse view mix long and short strips), the strips at a list's end are the shortest, and an
-// XCD that runs out of work takes another's: the frame's tail shrinks to the longest strip.
-// Queue heads: P.queue[0..7] (one per XCD list), P.queue[8] counts finished wavefronts; the last
-// one resets all nine for the next launch on the stream (stream order: the next launch starts
-// after this one has finished).  Same strips, same rays, same operations: frames are identical.
-template <typename VT, bool SHADE, bool GF, bool PIPE>
-__global__ __launch_bounds__(kThreadsPerTile, (kMarchMinWaves<false, false, GF, PIPE>)) void
-march_queue_kernel(const MarchParams P)
-{
-    __shared__ float4 s_tf[kTfLut];
-    const int tid = threadIdx.x;
-    const bool tf_in_lds = P.tf_n <= kTfLds;
-    if (tf_in_lds)
-        for (int i = tid; i < 2 * (P.tf_n + 2); i += (int)kThreadsPerTile) s_tf[i] = P.tf[i];
-    __syncthreads();
-    const uint32_t lane = (uint32_t)tid & 63u;
-    const uint32_t wpt = kThreadsPerTile / 64;  // strips per tile
-    // the XCD this wavefront runs on (HW_REG_XCC_ID): its own list first
-    uint32_t x = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;
-    for (uint32_t tried = 0; tried < 8;) {
-        uint32_t j = 0;
-        if (lane == 0) j = atomicAdd(&P.queue[x], 1u);
-        j = (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
-        const uint32_t strip = j < P.per_xcd ? P.tile_perm[x + 8 * j] : 0xFFFFFFFFu;
-        if (strip == 0xFFFFFFFFu) {  // this list is done: the next XCD's
-            x = (x + 1) & 7u;
-            ++tried;
-            continue;
-        }
-        const long long t0 = wall_clock64();
-        const uint32_t tile = strip / wpt;
-        march_strip<VT, SHADE, false, false, GF, PIPE>(P, (LdsF4 *)s_tf, tf_in_lds, tile % P.tiles_x,
-                                                       tile / P.tiles_x, strip % wpt, lane);
-        if (P.tile_cost && lane == 0)
-            P.tile_cost[strip] = (uint32_t)min(wall_clock64() - t0, 0x7FFFFFFFLL);
-#ifdef VR_WG_TIMES
-        if (lane == 0) wg_times_record((unsigned long long)t0, strip);
-#endif
-    }
-    if (lane == 0) {
-        const uint32_t done = atomicAdd(&P.queue[8], 1u);
-        if (done + 1 == gridDim.x * wpt) {  // the last wavefront: reset the heads
-            for (int q = 0; q < 9; ++q) atomicExch(&P.queue[q], 0u);
-        }
-    }
 }
 
 // ---- lane-pair march (small launches) ----------------------------------------------------------
@@ -2042,17 +1826,6 @@ __global__ __launch_bounds__(256) void grad_field_kernel(const float *__restrict
         uint32_t bx, by, bz;
         brick_coords((uint32_t)bidx, nbx, nby, bx, by, bz);
         const int x = (int)(bx * G::BX + lx), y = (int)(by * G::BY + lyy), z = (int)(bz * G::BZ + lz);
-        if constexpr (H && VR_FIELD_PLAIN) {
-            auto V = [&](int dx, int dy, int dz) {
-                return padded_voxel(bricks, x + dx, y + dy, z + dz, nx, ny, nz, nbx, nby);
-            };
-            const h2v xy = {field_half(V(1, 0, 0) - V(-1, 0, 0), scale),
-                            field_half(V(0, 1, 0) - V(0, -1, 0), scale)};
-            const h2v zw = {field_half(V(0, 0, 1) - V(0, 0, -1), scale), (_Float16)0.0f};
-            reinterpret_cast<uint2 *>(grad)[g] =
-                make_uint2(__builtin_bit_cast(uint32_t, xy), __builtin_bit_cast(uint32_t, zw));
-            continue;
-        }
         if constexpr (H) {
             _Float16 hv[12];
 #pragma unroll
@@ -2215,32 +1988,6 @@ __global__ __launch_bounds__(256) void assemble_kernel(const PixT *__restrict__ 
 template <typename VT, bool SHADE, bool COUNT, bool SKIP, bool GF = false, bool PIPE = false>
 hipError_t launch_march_t(const MarchParams &p, hipStream_t stream)
 {
-    if constexpr (!COUNT && !SKIP) {
-        if (p.queue) {  // tile_order 5: the persistent wavefront queue (host: a strip permutation)
-            if (p.tiles_x * p.tiles_y == 0) return hipSuccess;
-            // as many workgroups as the device holds at once (occupancy x CUs), once per variant
-            // and device: frame-worker threads of a multi-device context launch concurrently
-            // (ADVICE r4), so the cache is per device and atomic
-            static std::atomic<unsigned> grids[kMaxDevices];
-            int dev = 0;
-            if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices)
-                return hipErrorInvalidValue;
-            unsigned grid = grids[dev].load(std::memory_order_relaxed);
-            if (grid == 0) {
-                int per_cu = 0, cus = 0;
-                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                        &per_cu, march_queue_kernel<VT, SHADE, GF, PIPE>, kThreadsPerTile, 0) != hipSuccess ||
-                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-                    per_cu <= 0 || cus <= 0)
-                    return hipErrorInvalidValue;
-                grid = (unsigned)(per_cu * cus);
-                grids[dev].store(grid, std::memory_order_relaxed);  // same value from any thread
-            }
-            hipLaunchKernelGGL((march_queue_kernel<VT, SHADE, GF, PIPE>), dim3(grid),
-                               dim3(kThreadsPerTile), 0, stream, p);
-            return hipGetLastError();
-        }
-    }
     const uint32_t nblocks = p.tile_perm ? p.nperm
                              : p.tile_order >= 3 ? ((p.supers_total + 7) / 8) * 8 * kSuper * kSuper
                                                  : p.tiles_x * p.tiles_y;

@@ -684,24 +684,60 @@ def kernel_source_hash() -> str:
     return h.hexdigest()[:16]
 
 
+def _elf_sections(b: bytes, base: int = 0):
+    import struct
+    shoff = struct.unpack_from("<Q", b, base + 0x28)[0]
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, base + 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", b, base + shoff + i * shentsize) for i in range(shnum)]
+    names = base + secs[shstrndx][4]
+    return [(b[names + s[0]:b.index(b"\0", names + s[0])],) + s for s in secs]
+
+
 def kernel_code_hash(path: Optional[str] = None) -> str:
-    """sha256 (16 hex digits) of the device code the library carries: the bytes of its
-    `.hip_fatbin` ELF section (every gfx950 code object of the build).  Keys measured
-    per-kernel figures (the PMC traffic bench.py's roofline reads) to the machine code they
-    were measured on: host-only edits leave it unchanged, any kernel change moves it (the
-    build is deterministic: two builds of the same sources give the same bytes)."""
+    """sha256 (16 hex digits) of the ray-march kernels' machine code in the library: every
+    march_kernel instantiation's gfx950 code bytes and kernel descriptor (register counts, LDS,
+    kernarg size; the descriptor's layout-dependent code-entry offset zeroed), read from the
+    code object in the `.hip_fatbin` ELF section.  Keys measured per-kernel figures (the PMC
+    traffic bench.py's roofline reads) to the machine code they were measured on: host-only
+    edits and changes to other kernels leave it unchanged, any change to the march kernels
+    moves it (the build is deterministic)."""
     import hashlib
+    import re
     import struct
     b = open(path or LIB_PATH, "rb").read()
-    shoff = struct.unpack_from("<Q", b, 0x28)[0]
-    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
-    secs = [struct.unpack_from("<IIQQQQIIQQ", b, shoff + i * shentsize) for i in range(shnum)]
-    names_off = secs[shstrndx][4]
-    for name_i, _, _, _, off, size, *_ in secs:
-        end = b.index(b"\0", names_off + name_i)
-        if b[names_off + name_i:end] == b".hip_fatbin":
-            return hashlib.sha256(b[off:off + size]).hexdigest()[:16]
-    raise RuntimeError(f"{path or LIB_PATH} has no .hip_fatbin section")
+    fb = [s for s in _elf_sections(b) if s[0] == b".hip_fatbin"]
+    if not fb:
+        raise RuntimeError(f"{path or LIB_PATH} has no .hip_fatbin section")
+    fat = b[fb[0][5]:fb[0][5] + fb[0][6]]
+    syms = []
+    for p in (m.start() for m in re.finditer(b"__CLANG_OFFLOAD_BUNDLE__", fat)):
+        q = p + 32
+        for _ in range(struct.unpack_from("<Q", fat, p + 24)[0]):
+            off, size, tl = struct.unpack_from("<QQQ", fat, q)
+            triple = fat[q + 24:q + 24 + tl]
+            q += 24 + tl
+            if b"gfx950" not in triple:
+                continue
+            co = fat[p + off:p + off + size]
+            secs = _elf_sections(co)
+            st = next(s for s in secs if s[0] == b".symtab")
+            strt = next(s for s in secs if s[0] == b".strtab")
+            for i in range(st[6] // 24):
+                nm, _, _, shndx, val, sz = struct.unpack_from("<IBBHQQ", co, st[5] + i * 24)
+                name = co[strt[5] + nm:co.index(b"\0", strt[5] + nm)]
+                if b"12march_kernel" in name and 0 < shndx < len(secs) and sz > 0:
+                    sec = secs[shndx]
+                    code = bytearray(co[sec[5] + val - sec[4]:sec[5] + val - sec[4] + sz])
+                    if name.endswith(b".kd") and len(code) >= 24:
+                        code[16:24] = bytes(8)  # kernel_code_entry_byte_offset
+                    syms.append((name, bytes(code)))
+    if not syms:
+        raise RuntimeError(f"{path or LIB_PATH}: no march_kernel code in the gfx950 code object")
+    h = hashlib.sha256()
+    for name, code in sorted(syms):
+        h.update(name)
+        h.update(code)
+    return h.hexdigest()[:16]
 
 
 def shard_rows(height: int, row_block: int, nranks: int) -> int:
