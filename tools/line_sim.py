@@ -285,3 +285,65 @@ def tcp_model(view_name="fill", n=512, W=1920, H=1080, ntiles=40, seed=0, vb=4):
     return dict(view=view_name, wave_loads=loads, h0_lines_per_wave=tot[0] / loads,
                 h1_sectors_per_quarter=tot[1] / loads, h2_lines_per_quarter=tot[2] / loads,
                 pair_same_cell=same_cell / max(1, pairs))
+
+
+# ---- round 5: the reading td_mask settled (TCP accesses = active 4-lane quads x 64-B sectors) --
+def quad_sectors(addr, width, lanes_on, sector=64):
+    """L1 accesses of one wave-level load under the measured reading of
+    TCP_TOTAL_CACHE_ACCESSES (profiles/r05/m3/td_pmc.json): per 4-lane quad with an active
+    lane, the distinct 64-B sectors its active lanes' `width`-byte loads touch."""
+    a = np.asarray(addr)
+    on = np.asarray(lanes_on)
+    tot = 0
+    for q in range(len(a) // 4):
+        m = on[q * 4:(q + 1) * 4]
+        if not m.any():
+            continue
+        aa = a[q * 4:(q + 1) * 4][m]
+        tot += len(np.unique(np.concatenate([aa // sector, (aa + width - 1) // sector])))
+    return tot
+
+
+def quad_model(view_name, layout, n, W, H, lane_xy=lambda l: (l & 15, l >> 4), ntiles=20, seed=0):
+    """Mean quad_sectors per wave-level load of `layout` ((i, j, k, nb) -> [(addr, width)])
+    over random 16x4 wavefront strips of the view; lane_xy maps a lane to its pixel in the
+    strip (the kernel's 16x4 raster by default).  C3 fill: 24.1 (measured ~22); C4: 23.8 (21.4)."""
+    sys.path.insert(0, os.path.join(ROOT, "volumetric-renderer_amd"))
+    import synth
+    vc = synth.camera(view_name).to_vr_camera()
+    view, pos = list(vc.view), list(vc.position)
+    rng = np.random.default_rng(seed)
+    nb = (n + 3) // 4 + 1
+    lx = np.array([lane_xy(l)[0] for l in range(64)])
+    ly = np.array([lane_xy(l)[1] for l in range(64)])
+    tot = loads = tiles = 0
+    while tiles < ntiles:
+        tx, ty = rng.integers(0, W // 16), rng.integers(0, H // 4)
+        ok, pos0, dirs = rays(view, pos, W, H, (lx + tx * 16).astype(float), (ly + ty * 4).astype(float))
+        if ok.sum() < 32:
+            continue
+        tiles += 1
+        p = np.clip(pos0.copy(), 0.0, 1.0)
+        alive = ok.copy()
+        for _ in range(360):
+            alive &= np.all((p >= 0) & (p <= 1), axis=1)
+            if not alive.any():
+                break
+            i0 = np.floor(np.clip(p, 0, 1) * n - 0.5).astype(np.int64)
+            for addr, width in layout(i0[:, 0], i0[:, 1], i0[:, 2], nb):
+                tot += quad_sectors(addr, width, alive)
+                loads += 1
+            p = p + dirs * 0.005
+    return tot / max(1, loads)
+
+
+def zpair_geom(BX, BY, BZ, vb=4):
+    """f32 z-pairs in BX x BY x BZ-cell bricks (the -DVR_BRICK_CELLS geometries)."""
+    EX, EY, EZ = BX + 1, BY + 1, BZ + 1
+
+    def fn(i, j, k, nb):
+        pi, pj, pk = i + 2, j + 2, k + 2
+        b = ((pk // BZ) * nb + (pj // BY)) * nb + (pi // BX)
+        base = (b * EX * EY * EZ + ((pk % BZ) * EY + (pj % BY)) * EX + (pi % BX)) * 2 * vb
+        return [(base, 4 * vb), (base + EX * 2 * vb, 4 * vb)]
+    return fn
