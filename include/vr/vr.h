@@ -238,7 +238,10 @@ int vr_render(vr_ctx *ctx, const vr_camera *cam, const vr_params *p, void *out,
 /* Render into DEVICE memory `out_dev` on `stream` (hipStream_t, NULL = default),
  * asynchronously.  Image-space sharding for multi-GPU: the frame's rows are cut into
  * blocks of `row_block` rows and block b is rendered by rank (b % nranks); this rank's
- * blocks are written densely, in order, to `out_dev` (vr_shard_rows() rows x W pixels).
+ * blocks are written densely, in order, to `out_dev`: vr_shard_rows_ctx(ctx, H, row_block,
+ * nranks) rows x W pixels, sized with the row share in force at this call (vr_set_row_share;
+ * with the default 1:1 share that is vr_shard_rows()).  A buffer sized before the share was
+ * changed may be too small: size it again (vr_dist_render refuses a changed share).
  * nranks = 1, rank = 0 renders the whole frame.  A vr_create_mask context renders whole frames
  * only (rank 0 of 1; row_block is ignored), into memory of its lowest device, complete once
  * `stream` (a stream of that device) passes this point; p->frames_in_flight (1..8) frames may
