@@ -347,3 +347,32 @@ def zpair_geom(BX, BY, BZ, vb=4):
         base = (b * EX * EY * EZ + ((pk % BZ) * EY + (pj % BY)) * EX + (pi % BX)) * 2 * vb
         return [(base, 4 * vb), (base + EX * 2 * vb, 4 * vb)]
     return fn
+
+
+def tile_box_model(view_name="fill", n=512, W=1920, H=1080, K=8, ntiles=40, seed=1):
+    """Cells in the box a 16x16-pixel tile's rays sample over a stage of K steps (the LDS
+    staging a tile-stage would need): median / p90 / max over stages."""
+    sys.path.insert(0, os.path.join(ROOT, "volumetric-renderer_amd"))
+    import synth
+    vc = synth.camera(view_name).to_vr_camera()
+    view, pos = list(vc.view), list(vc.position)
+    rng = np.random.default_rng(seed)
+    sizes, tiles = [], 0
+    while tiles < ntiles:
+        tx, ty = rng.integers(0, W // 16), rng.integers(0, H // 16)
+        px, py = np.meshgrid(np.arange(16) + tx * 16, np.arange(16) + ty * 16)
+        ok, p0, d = rays(view, pos, W, H, px.ravel().astype(float), py.ravel().astype(float))
+        if ok.sum() < 200:
+            continue
+        tiles += 1
+        p0, d = np.clip(p0[ok], 0, 1), d[ok]
+        for s in range(0, 360 // K):
+            ks = np.arange(s * K, (s + 1) * K)
+            P = p0[:, None, :] + ks[None, :, None] * d[:, None, :] * 0.005
+            inb = np.all((P >= 0) & (P <= 1), axis=2)
+            if not inb.any():
+                break
+            u = np.floor(P[inb] * n - 0.5)
+            sizes.append(float(np.prod(u.max(0) + 1 - u.min(0) + 1)))
+    s = np.array(sizes)
+    return dict(K=K, median=float(np.median(s)), p90=float(np.percentile(s, 90)), max=float(s.max()))
