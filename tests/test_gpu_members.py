@@ -178,3 +178,49 @@ def test_dist_rejects_a_row_share_changed_after_creation(gpu):
         df.close()
     finally:
         rp.close()
+
+
+def test_members_random_sequence_of_frames_shares_and_flights(gpu):
+    """A seeded random sequence on 4 members of device 0 (copy exchange): frames in flight
+    1..8, row shares, output formats, cameras and TF changes interleaved; after every burst
+    each frame equals the one-device context's bytes (pipeline rebuilds, slot reuse and the
+    exchange's handshakes under changing shapes)."""
+    import torch
+    rng = np.random.default_rng(505)
+    W, H = 120, 90
+    vol = synth.gaussians_numpy((36, 40, 32), seed=12).astype(np.float32)
+    one = vr_amd.OffscreenPass(W, H, device=0)
+    grp = vr_amd.OffscreenPass(W, H, members=(0, 0, 0, 0), exchange=vr_amd.EXCHANGE_COPY)
+    try:
+        tfs = [synth.tf_color(), synth.tf_band(0.1, 0.9), synth.tf2()]
+        for rp in (one, grp):
+            _scene(rp, vol, tfs[0])
+        s = torch.cuda.Stream()
+        for burst in range(12):
+            if burst % 4 == 3:
+                tf = tfs[int(rng.integers(len(tfs)))]
+                for rp in (one, grp):
+                    rp.transfer_function_changed(tf)
+            w0, w = int(rng.integers(1, 5)), int(rng.integers(1, 5))
+            grp.set_row_share(w0, w)
+            f = int(rng.integers(1, 9))
+            cam = vr_amd.make_camera(radius=float(rng.uniform(1.4, 3.0)),
+                                     rotate=(float(rng.uniform(0, 360)), float(rng.uniform(-60, 60)))).to_vr_camera()
+            p = vr_amd.default_params(shading=int(rng.integers(2)), ert_eps=1e-5, frames_in_flight=f)
+            fmt = vr_amd.OUT_RGBA8 if rng.integers(2) else vr_amd.OUT_RGBA32F
+            words = 1 if fmt == vr_amd.OUT_RGBA8 else 4
+            ref = torch.empty((H, W * words), dtype=torch.int32, device="cuda")
+            one.render_device(cam, p, ref.data_ptr(), fmt, 16, 0, 1)
+            torch.cuda.synchronize()
+            frame = torch.zeros((H, W * words), dtype=torch.int32, device="cuda")
+            outs = [torch.zeros_like(frame) for _ in range(int(rng.integers(3, 10)))]
+            for o in outs:
+                grp.render_device(cam, p, frame.data_ptr(), fmt, 8, 0, 1, s.cuda_stream)
+                with torch.cuda.stream(s):
+                    o.copy_(frame)
+            torch.cuda.synchronize()
+            for i, o in enumerate(outs):
+                assert torch.equal(o, ref), (burst, i, f, (w0, w), fmt)
+    finally:
+        grp.close()
+        one.close()
