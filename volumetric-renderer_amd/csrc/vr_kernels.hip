@@ -940,7 +940,7 @@ __device__ __forceinline__ void wg_times_record(unsigned long long t0, uint32_t 
         const unsigned long long xcc = (unsigned)__builtin_amdgcn_s_getreg((3 << 11) | 20);
         g_wg_times[4 * slot] = t0;
         g_wg_times[4 * slot + 1] = (unsigned long long)wall_clock64();
-        g_wg_times[4 * slot + 2] = tile;
+        g_wg_times[4 * slot + 2] = ((unsigned long long)blockIdx.x << 32) | tile;
         g_wg_times[4 * slot + 3] = (xcc << 32) | hw;
     }
 }
