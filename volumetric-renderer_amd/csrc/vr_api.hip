@@ -1230,7 +1230,8 @@ vr_ctx *create_members(const std::vector<int> &devices, uint32_t width, uint32_t
         return nullptr;
     }
     c->device = devices[0];
-    for (int d : devices) c->device_mask |= 1u << d;
+    for (int d : devices)
+        if (d < 32) c->device_mask |= 1u << d;  // vr_get_device_mask reports devices 0..31
     c->width = width;
     c->height = height;
 #ifdef VR_EXPERIMENTS
