@@ -26,6 +26,7 @@
 #include "vr_exact_math.h"
 #include "vr_internal.h"
 
+#include <cstdlib>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -1985,6 +1986,21 @@ __global__ __launch_bounds__(256) void assemble_kernel(const PixT *__restrict__ 
     }
 }
 
+#ifdef VR_EXPERIMENTS
+// Experiment builds only: dynamic LDS reserved per march workgroup (VR_MARCH_LDS_PAD bytes),
+// which caps the workgroups resident on a CU -- fewer waves sharing its L1.
+static uint32_t march_lds_pad()
+{
+    static const uint32_t v = [] {
+        const char *e = std::getenv("VR_MARCH_LDS_PAD");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+    }();
+    return v;
+}
+#else
+constexpr uint32_t march_lds_pad() { return 0; }
+#endif
+
 template <typename VT, bool SHADE, bool COUNT, bool SKIP, bool GF = false, bool PIPE = false>
 hipError_t launch_march_t(const MarchParams &p, hipStream_t stream)
 {
@@ -1992,8 +2008,8 @@ hipError_t launch_march_t(const MarchParams &p, hipStream_t stream)
                              : p.tile_order >= 3 ? ((p.supers_total + 7) / 8) * 8 * kSuper * kSuper
                                                  : p.tiles_x * p.tiles_y;
     if (p.tiles_x * p.tiles_y == 0) return hipSuccess;
-    hipLaunchKernelGGL((march_kernel<VT, SHADE, COUNT, SKIP, GF, PIPE>), dim3(nblocks), dim3(kThreadsPerTile), 0,
-                       stream, p);
+    hipLaunchKernelGGL((march_kernel<VT, SHADE, COUNT, SKIP, GF, PIPE>), dim3(nblocks), dim3(kThreadsPerTile),
+                       march_lds_pad(), stream, p);
     return hipGetLastError();
 }
 
