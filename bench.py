@@ -331,6 +331,88 @@ def run_variant(rp, cfg, steps, warmup, rank, world, inflight, row_block=8, grou
                 keep=slots)
 
 
+def orbit_cameras(n=360):
+    """A camera drag like the reference's (main_window.cpp:284-289 -> Camera::rotate,
+    camera.cpp:15-29): every frame rotate((4, 1)) -- 1 degree of yaw, 0.25 degree of pitch at the
+    0.25 sensitivity -- while the radius swings 1.6 -> 3.0 -> 1.6 (zoom), so the path crosses the
+    frame-filling, oblique, side and default-radius view classes."""
+    cam = vr_amd.make_camera(radius=1.6)
+    out = []
+    for i in range(n):
+        cam.rotate(4.0, 1.0)
+        cam.set_radius(1.6 + 1.4 * (1.0 - np.cos(2.0 * np.pi * i / n)) / 2.0)
+        out.append(cam.to_vr_camera())
+    return out
+
+
+def orbit(rp, cfg, frame_ptr, n=360):
+    """The renderer under a moving camera: the orbit path, default memory
+    budget, derived structures freed first.  Serial frames timed on the host (enqueue + device
+    synchronize: every build, eviction and kernel switch on the path lands in its frame) ->
+    p50 / p99 / max; then the same path with 3 frames in flight (ms per frame over the path);
+    the library's derived-structure history (builds, evictions, downgrades) for each pass."""
+    cams = orbit_cameras(n)
+    p1 = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"])
+    p3 = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"], frames_in_flight=3)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def history():
+        m = rp.memory_report()
+        return {k: m[k] for k in ("builds", "evictions", "downgrades", "derived_bytes", "budget_bytes")}
+
+    def fresh():
+        rp.set_memory_budget(0)
+        rp.set_memory_budget(BUDGET_DEFAULT)
+        torch.cuda.synchronize()
+
+    fresh()
+    h0 = history()
+    times = []
+    for cam in cams:
+        t0 = time.perf_counter()
+        rp.render_device(cam, p1, frame_ptr, vr_amd.OUT_RGBA8, 8, 0, 1, stream)
+        torch.cuda.synchronize()
+        times.append((time.perf_counter() - t0) * 1e3)
+    h1 = history()
+    t = np.array(times)
+    serial = dict(p50_ms=round(float(np.percentile(t, 50)), 4), p99_ms=round(float(np.percentile(t, 99)), 4),
+                  max_ms=round(float(t.max()), 4), mean_ms=round(float(t.mean()), 4),
+                  slowest_frames=[int(i) for i in np.argsort(-t)[:5]],
+                  **{k: h1[k] - h0[k] for k in ("builds", "evictions", "downgrades")})
+    serial["p99_over_p50"] = round(serial["p99_ms"] / serial["p50_ms"], 3)
+    # second lap, structures as the first lap left them (a user dragging on)
+    times2 = []
+    for cam in cams:
+        t0 = time.perf_counter()
+        rp.render_device(cam, p1, frame_ptr, vr_amd.OUT_RGBA8, 8, 0, 1, stream)
+        torch.cuda.synchronize()
+        times2.append((time.perf_counter() - t0) * 1e3)
+    h2 = history()
+    t2 = np.array(times2)
+    lap2 = dict(p50_ms=round(float(np.percentile(t2, 50)), 4), p99_ms=round(float(np.percentile(t2, 99)), 4),
+                max_ms=round(float(t2.max()), 4),
+                **{k: h2[k] - h1[k] for k in ("builds", "evictions", "downgrades")})
+    # frames in flight over the same path (fresh structures)
+    fresh()
+    hp = history()
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    bufs = [torch.empty((cfg["H"], cfg["W"]), dtype=torch.int32, device="cuda") for _ in streams]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i, cam in enumerate(cams):
+        rp.render_device(cam, p3, bufs[i % 3].data_ptr(), vr_amd.OUT_RGBA8, 8, 0, 1,
+                         streams[i % 3].cuda_stream)
+    torch.cuda.synchronize()
+    pip = (time.perf_counter() - t0) / n * 1e3
+    h3 = history()
+    return dict(path=f"{n} frames of Camera::rotate((4, 1)) with the radius 1.6 -> 3.0 -> 1.6, C3 "
+                     "volume and params, default memory budget, derived structures freed first",
+                serial_frames=serial, second_lap=lap2,
+                frames_in_flight_3=dict(ms_per_frame=round(pip, 4),
+                                        **{k: h3[k] - hp[k] for k in ("builds", "evictions", "downgrades")}),
+                memory_after=h2)
+
+
 def host_cores():
     """(threads, description): the host CPUs this process can actually use: nproc (the
     affinity mask), capped by the cgroup CPU quota when one is set.  On the MI355X boxes nproc
@@ -440,18 +522,47 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def launch_ranks(n: int) -> int:
+def gpu_fds(pid="self"):
+    """The GPU device files a process holds open (/dev/kfd, /dev/dri/*): the HIP runtime opens
+    them when it initialises, so a parent that holds none has not touched the GPU."""
+    d = f"/proc/{pid}/fd"
+    out = []
+    for fd in os.listdir(d):
+        try:
+            t = os.readlink(os.path.join(d, fd))
+        except OSError:
+            continue
+        if t == "/dev/kfd" or t.startswith("/dev/dri/"):
+            out.append(t)
+    return sorted(out)
+
+
+def launch_ranks(n: int, rehearsal: bool = False) -> int:
     """--gpus N > 1 without WORLD_SIZE: run this script under torch.distributed.run, one process
-    per GPU, as a child (nothing here has touched the GPU: torch.cuda.device_count() does not
-    initialise it), and return its exit status.  The child's rank 0 prints the JSON line on the
-    stdout this process hands down."""
+    per GPU, as a child, and return its exit status.  The child's rank 0 prints the JSON line on
+    the stdout this process hands down.  The parent must not have initialised the GPU (it only
+    counted devices, which does not): it checks that it holds no GPU device file before it
+    spawns, refuses (exit 2) otherwise, and hands the check's result to the ranks, which report
+    it in the JSON line (`launch`).  rehearsal: the N ranks share the visible device(s) and
+    gather through gloo (VR_DIST_BACKEND=gloo), the driver's exact launch path on one GPU."""
     import subprocess
+    held = gpu_fds()
+    if held:
+        fail_exit(f"the launching process holds GPU device files {held} before spawning the "
+                  "ranks: something initialised HIP in the parent")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.abspath(__file__)] + sys.argv[1:]
-    print(f"bench: --gpus {n} without WORLD_SIZE: launching {' '.join(cmd)}", file=sys.stderr,
-          flush=True)
-    return subprocess.run(cmd).returncode
+    env = dict(os.environ)
+    env["VR_BENCH_LAUNCH"] = json.dumps(dict(path="bench.py launch_ranks -> torch.distributed.run",
+                                             parent_pid=os.getpid(), parent_gpu_fds=held,
+                                             rehearsal=rehearsal))
+    if rehearsal:
+        env["VR_DIST_BACKEND"] = "gloo"
+    print(f"bench: --gpus {n} without WORLD_SIZE: launching {' '.join(cmd)} (parent holds no GPU "
+          f"device file{'; rehearsal: gloo ranks sharing the visible GPU' if rehearsal else ''})",
+          file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
 
 
 def main():
@@ -480,17 +591,25 @@ def main():
     ap.add_argument("--members-on-one-gpu", type=int, default=0,
                     help="rehearsal: a multi-device context of M members all on device 0 "
                          "(vr_debug_create_members, copy exchange); --gpus must be 1")
+    ap.add_argument("--rehearse-launch", action="store_true",
+                    help="rehearsal: --gpus N > 1 through the driver's launch path (launch_ranks, "
+                         "torch.distributed.run) with N gloo ranks sharing the visible GPU(s)")
     args = ap.parse_args()
     if args.gpus < 1:
         fail_exit("--gpus must be >= 1")
     if args.members_on_one_gpu and (args.gpus != 1 or os.environ.get("WORLD_SIZE")):
         fail_exit("--members-on-one-gpu needs --gpus 1 and no torch.distributed launch")
+    if args.rehearse_launch and (args.gpus < 2 or args.multi_device_context or args.members_on_one_gpu):
+        fail_exit("--rehearse-launch needs --gpus N >= 2 and the per-process path")
     if (os.environ.get("WORLD_SIZE") is None and args.gpus > 1 and not args.multi_device_context):
-        ndev = torch.cuda.device_count()
-        if ndev < args.gpus:
+        ndev = torch.cuda.device_count()  # counts devices without initialising HIP
+        if args.rehearse_launch:
+            if ndev < 1:
+                fail_exit(f"--rehearse-launch needs a HIP device; device 0 is not present ({ndev} visible)")
+        elif ndev < args.gpus:
             fail_exit(f"--gpus {args.gpus} needs {args.gpus} HIP devices; device {ndev} is not "
                       f"present ({ndev} visible)")
-        sys.exit(launch_ranks(args.gpus))
+        sys.exit(launch_ranks(args.gpus, rehearsal=args.rehearse_launch))
 
     # stdout carries exactly one line, the JSON result (rank 0).  Libraries print banners to
     # fd 1 on their own (RCCL writes its version block when a communicator is created), so fd
@@ -701,6 +820,9 @@ def main():
             note="host-timed serial frames around vr_render_device; vr_prepare builds the copy "
                  "outside the frame (vr.h ABI 7)")
 
+    if not args.no_variants and args.config == "c3" and world == 1 and not group:
+        variants["orbit"] = orbit(rp, cfg, R["last_frame_ptr"])
+
     if not args.no_variants and world == 1 and not group:
         # PCIe-inclusive: vr_render into (pageable) host memory, the drop-in record() path.
         # The frame's RGBA8 bytes cross PCIe inside the timed region; row bands copy while
@@ -830,6 +952,9 @@ def main():
             "memory_per_device": memory,
             "frame_check": R["check"],  # N > 1: assembled frame == single-GPU frame, bit for bit
             "per_rank": R["per_rank"],
+            # N > 1 started by this script (launch_ranks): the launch path and the parent's
+            # GPU-file check; null when the driver's launcher started the ranks itself
+            "launch": json.loads(os.environ["VR_BENCH_LAUNCH"]) if os.environ.get("VR_BENCH_LAUNCH") else None,
             "variants": variants,
         }
         sys.stdout.flush()

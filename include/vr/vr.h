@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 8
+#define VR_ABI_VERSION 9
 
 /* ---- status codes (negative errno style) ---- */
 #define VR_OK 0
@@ -304,6 +304,13 @@ int vr_release_external_memory(vr_ctx *ctx, vr_external_memory *mem);
  * stencil copy, 5.6 GB).  VR_MEMORY_BUDGET_UNLIMITED builds whatever fits beside a 2 GiB
  * free-memory reserve (ABI 7's default).  A multi-device context applies the budget on every
  * device (each holds its replica's structures).
+ * (ABI 9) A structure that does not fit evicts the least recently read others, one at a time,
+ * never one the frame reads; an evicted (or rewritten) structure is released stream-ordered on
+ * the evicting frame's stream after every frame in flight on the context's other streams (frame
+ * fences), so no frame synchronises the device.  Every frame whose view wanted a structure the
+ * budget or free memory refused -- a slower kernel; the same pixels, except that a refused
+ * binary16 difference field gives the exact_gradient = 1 pixels -- is counted in
+ * vr_memory_info.downgrades, with the refused structure in last_downgrade.
  * Lowering the budget waits for the device and frees the structures.
  * vr_memory_report: the bytes each structure takes now on the (first) device.
  * vr_prepare: builds everything a frame with this camera and params would read, synchronously,
@@ -318,7 +325,20 @@ typedef struct vr_memory_info {
     uint64_t derived_bytes;       /* the sum of the five above: what the budget caps   */
     uint64_t budget_bytes;        /* the budget in force, in bytes (the default's value
                                      for this volume; VR_MEMORY_BUDGET_UNLIMITED)       */
+    /* (ABI 9) history since the context was created */
+    uint64_t builds;              /* structures built (every (re)build counts)          */
+    uint64_t evictions;           /* structures evicted to fit another in the budget    */
+    uint64_t downgrades;          /* frames that read the bricks because the budget or
+                                     free memory refused the structure their view wanted */
+    uint64_t last_downgrade;      /* VR_DERIVED_* refused at the latest downgrade (0: none) */
 } vr_memory_info;
+enum vr_derived {
+    VR_DERIVED_FIELD = 1,          /* difference field            */
+    VR_DERIVED_OBLIQUE_COPY = 2,   /* 7x15x8-cell z-pair copy     */
+    VR_DERIVED_PLAIN_COPY = 3,     /* plain 15^3-cell copy        */
+    VR_DERIVED_STENCIL_COPY = 4,   /* stencil copy                */
+    VR_DERIVED_SKIP = 5            /* skip-empty classification   */
+};
 #define VR_MEMORY_BUDGET_UNLIMITED (~(uint64_t)0)
 #define VR_MEMORY_BUDGET_DEFAULT (~(uint64_t)0 - 1)
 int vr_set_memory_budget(vr_ctx *ctx, uint64_t bytes);

@@ -68,6 +68,18 @@ const char *vr_dist_last_error(const vr_dist *d);
 int vr_dist_timing_enable(vr_dist *d, int enable);
 int vr_dist_timing_read(vr_dist *d, double *render_ms, double *gather_ms, uint64_t *frames);
 
+/* Host cost of the frame path (diagnostics; tools/host_cost.cpp): with host profiling on,
+ * vr_dist_render adds the host microseconds of each step it enqueues -- this rank's render
+ * (vr_render_device), the gather (ncclGather or the copy exchange), the assembly, the event
+ * records and the stream waits of the schedule -- and of the whole call.
+ * vr_dist_host_profile_read returns the sums and the frames counted, and clears them. */
+typedef struct vr_dist_host_profile {
+    uint64_t frames;
+    double render_us, gather_us, assemble_us, record_us, wait_us, total_us;
+} vr_dist_host_profile;
+int vr_dist_host_profile_enable(vr_dist *d, int enable);
+int vr_dist_host_profile_read(vr_dist *d, vr_dist_host_profile *out);
+
 /* Waits for outstanding frames, then frees the slots and the communicator. */
 void vr_dist_destroy(vr_dist *d);
 

@@ -58,7 +58,7 @@ def test_product_never_reads_the_environment():
 
 def test_library_loads_and_pure_entry_points():
     L = vr_amd.lib()
-    assert L.vr_abi_version() == 8
+    assert L.vr_abi_version() == 9
     p = vr_amd.default_params()
     assert p.step == pytest.approx(0.005) and p.ray_dist == pytest.approx(1.8)
     assert list(p.clear_color) == pytest.approx([0.11, 0.11, 0.11, 1.0])
@@ -108,7 +108,7 @@ int main(void) { printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(
                                      vr_amd.vr_params.depth_zero_to_one.offset,
                                      C.sizeof(vr_amd.vr_memory_info), C.sizeof(vr_amd.vr_member_timing),
                                      vr_amd.vr_member_timing.kernel_ms.offset]
-    assert "VR_ABI_VERSION 8" in src
+    assert "VR_ABI_VERSION 9" in src
 
 
 def test_create_without_device_fails_cleanly():

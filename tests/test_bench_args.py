@@ -42,3 +42,17 @@ def test_multi_device_context_needs_the_devices_too():
 def test_member_rehearsal_is_one_gpu_only():
     r = _bench(["--gpus", "2", "--members-on-one-gpu", "2"])
     assert r.returncode == 2 and "--members-on-one-gpu needs --gpus 1" in r.stderr
+
+
+def test_launch_rehearsal_needs_two_ranks_and_a_device():
+    r = _bench(["--gpus", "1", "--rehearse-launch"])
+    assert r.returncode == 2 and "--rehearse-launch needs --gpus N >= 2" in r.stderr
+    import torch
+    if torch.cuda.device_count() == 0:
+        r = _bench(["--gpus", "2", "--rehearse-launch"])
+        assert r.returncode == 2 and "--rehearse-launch needs a HIP device" in r.stderr, r.stderr[-2000:]
+
+
+def test_gpu_fds_sees_no_device_file_in_a_cpu_process():
+    import bench
+    assert bench.gpu_fds() == []

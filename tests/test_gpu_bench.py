@@ -77,3 +77,36 @@ def test_bench_member_rehearsal_on_one_gpu(gpu):
     pr = d["per_rank"]
     assert [x["rank"] for x in pr] == [0, 1] and all(x["device"] == 0 for x in pr)
     assert all(x["frames"] > 0 and x["kernel_ms"] > 0 for x in pr)
+
+
+def test_bench_rehearses_the_driver_launch_path(gpu):
+    """--gpus 2 --rehearse-launch: the driver's exact multi-GPU command path on one MI355X
+    (bench.py -> launch_ranks -> torch.distributed.run -> 2 ranks), the ranks sharing the GPU
+    and gathering through gloo.  One contract line with n_gpus 2, the assembled frame equal to
+    rank 0's own whole-frame render, one per_rank row per rank, and the launching parent held
+    no GPU device file when it spawned the ranks."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rehearse-launch",
+                        "--steps", "3", "--warmup", "0", "--no-cpu-baseline", "--no-variants"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=170)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["frame_check"] is True
+    assert sorted(x["rank"] for x in d["per_rank"]) == [0, 1]
+    ln = d["launch"]
+    assert ln["rehearsal"] is True and ln["parent_gpu_fds"] == [] and "launch_ranks" in ln["path"]
+    assert "rehearsal" in d["config"]["parallelism"]
+
+
+def test_device_count_opens_no_gpu_file_and_init_does(gpu):
+    """The launching parent counts devices with torch.cuda.device_count(): on this image that
+    opens no GPU device file (bench.gpu_fds), whereas initialising HIP does -- so the detector
+    launch_ranks relies on sees a real initialisation."""
+    code = ("import sys; sys.path.insert(0, %r); import bench, torch; n = torch.cuda.device_count(); "
+            "before = bench.gpu_fds(); torch.cuda.init(); torch.empty(1, device='cuda'); "
+            "print(n, len(before), len(bench.gpu_fds()))" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    n, before, after = (int(x) for x in r.stdout.split()[-3:])
+    assert n >= 1 and before == 0 and after > 0

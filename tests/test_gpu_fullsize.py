@@ -4,10 +4,10 @@ C1, C2 and C3 are compared with the CPU oracle over WHOLE frames (every pixel, 4
 the oracle marches a 1080p C3 frame in about 0.4 s on the GPU box's 16 cores), in the float
 parity format (RGBA after blend, before UNORM quantisation: RMSE <= 1e-4, max |d| <= 2e-3,
 SURVEY.md §8c) and in RGBA8 (<= 1 LSB), then bit for bit (against the oracle restating the
-binary16 difference field where the frame read it).  C4 and C5 (1 and 8 GiB of voxels) are compared on 64
-rows spread over the frame, plus size-independent properties: row-block sharding reassembles
-the frame bit for bit, rendering is deterministic, early-ray termination stays within its
-bound.  The spec matched is res/shaders/volume.frag:21-52 under the Vulkan fixed-function
+binary16 difference field where the frame read it).  C4 and C5 (1 and 8 GiB of voxels, the
+multi-GPU configs) are compared over whole frames too, and their 8-way row-block shards,
+assembled, must equal the oracle frame bit for bit; plus size-independent properties:
+rendering is deterministic, early-ray termination stays within its bound.  The spec matched is res/shaders/volume.frag:21-52 under the Vulkan fixed-function
 state of offscreen_pass.cpp (oracle/oracle.c).  Measured errors go to $VR_PARITY_LOG (JSON
 lines) when that is set.
 """
@@ -31,10 +31,13 @@ def _log(**kw):
             f.write(json.dumps(kw) + "\n")
 
 
-def frame_parity(rp, vol, vmin, vmax, tf, cam, W, H, p, name, rows=None):
+def frame_parity(rp, vol, vmin, vmax, tf, cam, W, H, p, name, rows=None, shards=0, row_block=16):
     """The GPU frame against the oracle: every row (rows=None) or the given rows.  A frame
     that read the binary16 difference field (kernel tag F32H, vr_params.exact_gradient = 0)
-    must also equal the oracle restating that rounding bit for bit."""
+    must also equal the oracle restating that rounding bit for bit.  shards = n > 0 (whole
+    frames): the n-way row-block shards (row_block rows per block, the multi-GPU layout)
+    rendered in the float format and assembled into the frame must equal the oracle frame bit
+    for bit as well."""
     img = rp.render(cam, p, vr_amd.OUT_RGBA32F)
     img8 = rp.render(cam, p, vr_amd.OUT_RGBA8)
     half = "F32H" in rp.kernel_name(p)
@@ -61,11 +64,23 @@ def frame_parity(rp, vol, vmin, vmax, tf, cam, W, H, p, name, rows=None):
     assert rmse <= 1e-4 and mx <= 2e-3 and lsb <= 1, msg
     # and bit for bit against the restatement of what the kernel computes
     assert (exact16 if half else exact) == 1.0, msg
+    if shards:
+        import torch
+        assert rows is None
+        want = (ref16 if half else ref.astype(np.float32)).view(np.uint32)
+        sr = vr_amd.shard_rows(H, row_block, shards)
+        g = torch.empty((shards, sr, W, 4), dtype=torch.float32, device="cuda")
+        for r in range(shards):
+            rp.render_device(cam, p, g[r].data_ptr(), vr_amd.OUT_RGBA32F, row_block, r, shards)
+        out = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+        rp.assemble_rows(g.data_ptr(), out.data_ptr(), vr_amd.OUT_RGBA32F, row_block, shards)
+        torch.cuda.synchronize()
+        got_sh = out.cpu().numpy().view(np.uint32)
+        del g, out
+        same = float(np.mean(got_sh == want))
+        _log(case=name, shards=shards, row_block=row_block, assembled_bit_exact_frac=same)
+        assert same == 1.0, f"{name}: {shards}-way assembled frame vs oracle: bit-exact {same:.6f}"
     return img
-
-
-def spread_rows(H, n=64):
-    return np.unique(np.linspace(H // (2 * n), H - 1, n).astype(int))
 
 
 def test_c1_64_f32_256_whole_frame(gpu):
@@ -130,20 +145,30 @@ def test_c2_256_u8_1024_whole_frame(gpu):
     rp.close()
 
 
-def test_c4_1024_u8_2048_rows_match_oracle(gpu):
-    """C4: 1024^3 u8 (generated on the device, seed 7) at 2048x2048: 64 rows spread over the
-    frame against the oracle marching the same voxels."""
+@pytest.fixture(scope="module")
+def c4():
+    """C4: 1024^3 u8 generated on the device (seed 7), 2048x2048, TF-2; the resident voxels
+    read back in their u8 storage type for the oracle (float(u8) is exact)."""
     W, H, N = 2048, 2048, 1024
     rp = vr_amd.OffscreenPass(W, H)
     lo, hi = rp.generate_volume((N, N, N), np.uint8, seed=7)
     tf = synth.tf2()
     rp.transfer_function_changed(tf)
     vol = rp.read_volume(native=True)
-    cam = synth.camera("fill").to_vr_camera()
-    for p in (vr_amd.default_params(), vr_amd.default_params(shading=1, ert_eps=1e-5)):
-        frame_parity(rp, vol, lo, hi, tf, cam, W, H, p, f"C4 shading={p.shading}",
-                     rows=spread_rows(H))
+    assert vol.dtype == np.uint8 and vol.shape == (N, N, N)
+    yield dict(rp=rp, vol=vol, lo=lo, hi=hi, tf=tf, W=W, H=H)
     rp.close()
+
+
+@pytest.mark.parametrize("camname,shading", [("fill", 0), ("fill", 1), ("fill_oblique", 0)])
+def test_c4_1024_u8_2048_whole_frame(gpu, c4, camname, shading):
+    """C4 (the 2/4/8-GPU config, plain-u8 bricks): EVERY row of the 2048x2048 frame against the
+    oracle marching the same voxels, bit for bit, and the 8-way row-block shards assembled into
+    the frame equal the oracle frame bit for bit too."""
+    p = (vr_amd.default_params(shading=1, ert_eps=1e-5) if shading else vr_amd.default_params())
+    cam = synth.camera(camname).to_vr_camera()
+    frame_parity(c4["rp"], c4["vol"], c4["lo"], c4["hi"], c4["tf"], cam, c4["W"], c4["H"], p,
+                 f"C4 {camname} shading={shading}", shards=8)
 
 
 def test_c4_1024_u8_2048_sharding_determinism_ert(gpu):
@@ -178,18 +203,38 @@ def test_c4_1024_u8_2048_sharding_determinism_ert(gpu):
     rp.close()
 
 
-def test_c5_2048_u8_4096_shards_determinism_ert_and_rows(gpu):
-    """C5: 2048^3 u8 (generated on the device, seed 11) at 4096x4096, the multi-GPU config:
-    8-way row-block shards reassemble the single-GPU frame bit for bit, repeated renders are
-    identical, ERT stays within its bound, and rows spread over the frame match the CPU oracle
-    marching the SAME 8 GiB of voxels (read back in their u8 storage type: float(u8) is exact,
-    so the oracle samples what the reference's float Dataset would hold)."""
-    import torch
+@pytest.fixture(scope="module")
+def c5():
+    """C5: 2048^3 u8 generated on the device (seed 11, 8 GiB of voxels, 12.4 GB bricked), 4096x4096,
+    TF-2; the resident voxels read back as u8 for the oracle."""
     W, H, N = 4096, 4096, 2048
     rp = vr_amd.OffscreenPass(W, H)
     lo, hi = rp.generate_volume((N, N, N), np.uint8, seed=11)
     tf = synth.tf2()
     rp.transfer_function_changed(tf)
+    vol = rp.read_volume(native=True)
+    assert vol.dtype == np.uint8 and vol.shape == (N, N, N)
+    assert float(vol.min()) == lo and float(vol.max()) == hi
+    yield dict(rp=rp, vol=vol, lo=lo, hi=hi, tf=tf, W=W, H=H)
+    rp.close()
+
+
+@pytest.mark.parametrize("shading", [0, 1])
+def test_c5_2048_u8_4096_whole_frame(gpu, c5, shading):
+    """C5 (the 8-GPU config): EVERY row of the 4096x4096 frame against the oracle marching the
+    SAME 8 GiB of voxels, bit for bit, and the 8-way row-block shards (8-row blocks, the
+    multi-GPU layout) assembled into the frame equal the oracle frame bit for bit too."""
+    p = (vr_amd.default_params(shading=1, ert_eps=1e-5) if shading else vr_amd.default_params())
+    cam = synth.camera("fill").to_vr_camera()
+    frame_parity(c5["rp"], c5["vol"], c5["lo"], c5["hi"], c5["tf"], cam, c5["W"], c5["H"], p,
+                 f"C5 shading={shading}", shards=8, row_block=8)
+
+
+def test_c5_2048_u8_4096_shards_determinism_ert(gpu, c5):
+    """C5: 8-way row-block shards reassemble the single-GPU RGBA8 frame bit for bit, repeated
+    renders are identical, and ERT stays within its bound."""
+    import torch
+    rp, W, H = c5["rp"], c5["W"], c5["H"]
     cam = synth.camera("fill").to_vr_camera()
     p = vr_amd.default_params()
     full = torch.empty((H, W), dtype=torch.int32, device="cuda")
@@ -207,18 +252,8 @@ def test_c5_2048_u8_4096_shards_determinism_ert_and_rows(gpu):
     rp.assemble_rows(g.data_ptr(), out.data_ptr(), vr_amd.OUT_RGBA8, 8, n)
     torch.cuda.synchronize()
     assert torch.equal(out, full)
-    del g, out, again
-    # oracle rows: the resident voxels, u8
-    vol = rp.read_volume(native=True)
-    assert vol.dtype == np.uint8 and vol.shape == (N, N, N)
-    assert float(vol.min()) == lo and float(vol.max()) == hi
-    a = None
-    for q in (p, vr_amd.default_params(shading=1, ert_eps=1e-5)):
-        img = frame_parity(rp, vol, lo, hi, tf, cam, W, H, q, f"C5 shading={q.shading}",
-                           rows=spread_rows(H))
-        if a is None:
-            a = img
+    del g, out, again, full
     # ERT at eps: colour error <= T_stop * (C + 0.11 + 1) <= 2.2 eps
-    e = rp.render(cam, vr_amd.default_params(ert_eps=1e-3))
+    a = rp.render(cam, p, vr_amd.OUT_RGBA32F)
+    e = rp.render(cam, vr_amd.default_params(ert_eps=1e-3), vr_amd.OUT_RGBA32F)
     assert np.abs(a.astype(np.float64) - e).max() <= 2.2e-3
-    rp.close()

@@ -51,9 +51,10 @@ struct vr_ctx {
     // oblique views, the plain and stencil copies for sparse ones), each built lazily on the
     // first frame that wants it after a volume change
     struct AltCopy {
-        void *bricks = nullptr;
+        void *bricks = nullptr;  // stream-ordered allocation (hipMallocAsync)
         size_t bytes = 0;
         bool valid = false, failed = false;
+        uint64_t used = 0;  // frame_no of the latest frame that read it (eviction order)
     } alt[3];
     uint32_t nx = 1, ny = 1, nz = 1;
     float vmin = 0.0f, vmax = 1.0f;
@@ -71,9 +72,10 @@ struct vr_ctx {
     bool range_valid = false, dist_valid = false;
     // f32 shading: precomputed central differences (3 x the bricked density), built lazily
     // on the first shaded frame after a volume change; absent when memory is short
-    float *grad = nullptr;
+    float *grad = nullptr;  // stream-ordered allocation (hipMallocAsync)
     size_t grad_bytes = 0;
     bool grad_valid = false;
+    uint64_t grad_used = 0;  // frame_no of the latest frame that read it
     bool grad_half = false;      // the field's precision (vr_params.exact_gradient == 0: binary16)
     int grad_scale_log2 = 0;     // and its scale (field_scale_log2 of the data's own range)
     // f32 storage: the stored voxels' min and max, zero border included (measured on the bricks
@@ -102,6 +104,23 @@ struct vr_ctx {
     // frame that first needs them; frames on other streams wait for this event
     hipEvent_t built_ev = nullptr;
     bool built_recorded = false;
+    // Frame fences (round 6): for each stream that launched frames of this context, an event
+    // recorded after its latest frame.  A derived structure that frames in flight may still read
+    // is freed (or rewritten) stream-ordered on the evicting frame's stream after that stream
+    // waited on every other stream's fence -- no device synchronisation on the frame path.
+    struct Fence {
+        hipStream_t stream;
+        hipEvent_t ev;
+        uint64_t used;
+        bool external;        // recorded by the caller (vr_dist slot streams, vr_group.h)
+        uint64_t build_seen;  // build_gen this stream last waited for (ensure_derived)
+    };
+    std::vector<Fence> fences;
+    uint64_t build_gen = 0;  // records of built_ev so far
+    uint64_t frame_no = 0;  // launches so far (the derived structures' recency)
+    // derived-structure history (vr_memory_report, ABI 9)
+    uint64_t n_builds = 0, n_evictions = 0, n_downgrades = 0;
+    uint32_t last_downgrade = 0;
     // scratch
     unsigned long long *counters = nullptr;
     void *frame_dev = nullptr;
@@ -704,12 +723,21 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
 }
 
 // After a build on `s`: frames on other streams wait for it (ensure_derived).
+// The frame fence of stream s (nullptr: none yet).
+vr_ctx::Fence *fence_of(vr_ctx *c, hipStream_t s)
+{
+    for (auto &x : c->fences)
+        if (x.stream == s) return &x;
+    return nullptr;
+}
 int record_build(vr_ctx *c, hipStream_t s)
 {
     if (!c->built_ev)
         HIP_TRY(c, hipEventCreateWithFlags(&c->built_ev, hipEventDisableTiming), "hipEventCreate");
     HIP_TRY(c, hipEventRecord(c->built_ev, s), "hipEventRecord(build)");
     c->built_recorded = true;
+    ++c->build_gen;
+    if (vr_ctx::Fence *f = fence_of(c, s)) f->build_seen = c->build_gen;  // stream order
     return VR_OK;
 }
 
@@ -741,32 +769,98 @@ bool budget_allows(const vr_ctx *c, size_t extra, size_t replaced)
     const size_t now = derived_bytes(c) - replaced;
     return now + extra <= effective_budget(c);
 }
-// Free every alternative copy but `keep` (frames in flight may still read them: the device
-// drains first, as for any resource swap).
-int evict_alt_except(vr_ctx *c, int keep, hipStream_t s)
+// ---- frame fences and stream-ordered release of derived structures ----
+constexpr size_t kMaxFences = 32;
+// After this frame's launches on `s`: re-record the stream's fence.  A stream seen for the first
+// time gets a fence; past kMaxFences streams the least recently used one's is recycled once its
+// last frame has finished (a host wait, only with more than 32 frame streams in use).
+int fence_record(vr_ctx *c, hipStream_t s)
 {
-    bool any = false;
-    for (int i = 0; i < (int)(sizeof c->alt / sizeof c->alt[0]); ++i)
-        if (i != keep && c->alt[i].bricks) any = true;
-    if (!any) return VR_OK;
-    (void)s;
-    HIP_TRY(c, hipDeviceSynchronize(), "hipDeviceSynchronize (evict copy)");
-    for (int i = 0; i < (int)(sizeof c->alt / sizeof c->alt[0]); ++i)
-        if (i != keep && c->alt[i].bricks) {
-            hipFree(c->alt[i].bricks);
-            c->alt[i] = vr_ctx::AltCopy();
+    vr_ctx::Fence *f = fence_of(c, s);
+    if (f && f->external) {  // the caller records it right after this render (vr_dist)
+        f->used = c->frame_no;
+        return VR_OK;
+    }
+    if (!f) {
+        if (c->fences.size() < kMaxFences) {
+            hipEvent_t e = nullptr;
+            HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate(fence)");
+            c->fences.push_back(vr_ctx::Fence{s, e, 0, false, 0});
+            f = &c->fences.back();
+        } else {
+            vr_ctx::Fence *old = nullptr;
+            for (auto &x : c->fences)
+                if (!x.external && (!old || x.used < old->used)) old = &x;
+            if (!old) return VR_OK;  // every fence external: nothing of ours to record
+            HIP_TRY(c, hipEventSynchronize(old->ev), "hipEventSynchronize(fence)");
+            old->stream = s;
+            old->build_seen = 0;
+            f = old;
         }
+    }
+    f->used = c->frame_no;
+    HIP_TRY(c, hipEventRecord(f->ev, s), "hipEventRecord(fence)");
+    return VR_OK;
+}
+// Order `s` after every frame issued so far on every other stream (a structure's readers).
+int fence_others(vr_ctx *c, hipStream_t s)
+{
+    for (const auto &x : c->fences)
+        if (x.stream != s) HIP_TRY(c, hipStreamWaitEvent(s, x.ev, 0), "hipStreamWaitEvent(fence)");
+    return VR_OK;
+}
+// Free a derived structure that frames in flight may still read: stream-ordered on `s`, after
+// every other stream's latest frame (and, on `s`, after everything enqueued there).
+int release_async(vr_ctx *c, void *p, hipStream_t s)
+{
+    if (!p) return VR_OK;
+    if (int rc = fence_others(c, s)) return rc;
+    HIP_TRY(c, hipFreeAsync(p, s), "hipFreeAsync(derived structure)");
+    return VR_OK;
+}
+// Evict derived structures, least recently read first, until `extra` more bytes (replacing
+// `replaced` bytes of the same structure) fit the budget; never the copy `keep_alt` (alt index,
+// or -1) the frame reads, nor the field when `keep_field`.  Returns VR_OK with *fits.
+int make_room(vr_ctx *c, size_t extra, size_t replaced, int keep_alt, bool keep_field, hipStream_t s,
+              bool *fits)
+{
+    *fits = budget_allows(c, extra, replaced);
+    while (!*fits) {
+        int pick = -2;  // -1 the field, 0..2 an alternative copy
+        uint64_t oldest = ~0ull;
+        if (c->grad && !keep_field && c->grad_used < oldest) {
+            pick = -1;
+            oldest = c->grad_used;
+        }
+        for (int i = 0; i < (int)(sizeof c->alt / sizeof c->alt[0]); ++i)
+            if (i != keep_alt && c->alt[i].bricks && c->alt[i].used < oldest) {
+                pick = i;
+                oldest = c->alt[i].used;
+            }
+        if (pick == -2) return VR_OK;  // nothing left to evict: does not fit
+        if (pick == -1) {
+            if (int rc = release_async(c, c->grad, s)) return rc;
+            c->grad = nullptr;
+            c->grad_bytes = 0;
+            c->grad_valid = false;
+        } else {
+            if (int rc = release_async(c, c->alt[pick].bricks, s)) return rc;
+            c->alt[pick] = vr_ctx::AltCopy();
+        }
+        ++c->n_evictions;
+        *fits = budget_allows(c, extra, replaced);
+    }
     return VR_OK;
 }
 // Free every derived structure (after the device drained); rebuilt lazily within the budget.
 void free_derived(vr_ctx *c)
 {
-    if (c->grad) hipFree(c->grad);
+    if (c->grad) (void)hipFreeAsync(c->grad, nullptr);
     c->grad = nullptr;
     c->grad_bytes = 0;
     c->grad_valid = false;
     for (auto &a : c->alt) {
-        if (a.bricks) hipFree(a.bricks);
+        if (a.bricks) (void)hipFreeAsync(a.bricks, nullptr);
         a = vr_ctx::AltCopy();
     }
     if (c->brick_range) hipFree(c->brick_range);
@@ -775,6 +869,7 @@ void free_derived(vr_ctx *c)
     c->skip_dist = nullptr;
     c->nbricks_alloc = 0;
     c->range_valid = c->dist_valid = false;
+    (void)hipStreamSynchronize(nullptr);
 }
 
 // skip_empty: (re)build the per-brick ranges and the distance field when stale, on `s` ahead of
@@ -796,6 +891,7 @@ int ensure_skip(vr_ctx *c, MarchParams &P, hipStream_t s)
         HIP_TRY(c, hipMalloc(&c->skip_dist, 2 * nb), "hipMalloc(skip distance field)");
         c->nbricks_alloc = nb;
     }
+    if (!c->range_valid || !c->dist_valid) ++c->n_builds;
     if (!c->range_valid) {
         HIP_TRY(c, launch_brick_range(c->layout, c->bricks, bricks_for(c->nx, 0, c->layout), bricks_for(c->ny, 1, c->layout),
                                       bricks_for(c->nz, 2, c->layout), c->brick_range, s),
@@ -822,13 +918,16 @@ int ensure_skip(vr_ctx *c, MarchParams &P, hipStream_t s)
 // field in place after the device has drained (frames in flight may still read it).  Returns
 // true when it launched a (re)build on `s`: frames on other streams must then wait for it
 // (ensure_derived records the build event).
-bool ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s, bool half)
+bool ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s, bool half, bool *refused)
 {
     bool built = false;
+    *refused = false;
     if (!use_grad_field(c, half)) return built;
+    *refused = true;  // until the field is in place
     const int k = half ? field_scale_log2(c->data_lo, c->data_hi) : 0;
     if (c->grad_valid && (c->grad_half != half || c->grad_scale_log2 != k)) {
-        if (hipDeviceSynchronize() != hipSuccess) {
+        // rewritten in place: after every frame in flight that may still read it
+        if (fence_others(c, s) != VR_OK) {
             (void)hipGetLastError();
             return built;
         }
@@ -836,21 +935,19 @@ bool ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s, bool half)
     }
     const size_t bytes = c->brick_bytes / element_size(ST_F32) * kGradElemBytes;
     if (!c->grad || c->grad_bytes != bytes) {
-        if (c->grad) hipFree(c->grad);
+        if (c->grad && release_async(c, c->grad, s) != VR_OK) return built;
         c->grad = nullptr;
         c->grad_bytes = 0;
         c->grad_valid = false;
-        // over the budget: the alternative copies (other views') make room first, as one
-        // copy evicts another (ensure_alt); the field serves the dense-row view drawn now
-        if (!budget_allows(c, bytes, 0)) {
-            if (evict_alt_except(c, -1, s) != VR_OK) return built;
-            if (!budget_allows(c, bytes, 0)) return built;
-        }
+        // over the budget: the least recently read alternative copies make room (the field
+        // serves the dense-row view drawn now; a frame that reads it reads no copy)
+        bool fits = false;
+        if (make_room(c, bytes, 0, -1, false, s, &fits) != VR_OK || !fits) return built;
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < bytes + (2ull << 30))
             return built;
         void *g = nullptr;
-        if (hipMalloc(&g, bytes) != hipSuccess) {
+        if (hipMallocAsync(&g, bytes, s) != hipSuccess) {
             (void)hipGetLastError();
             return built;
         }
@@ -862,12 +959,15 @@ bool ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s, bool half)
                               half, k, s) != hipSuccess)
             return built;
         built = true;
+        ++c->n_builds;
         c->grad_valid = true;
         c->grad_half = half;
         c->grad_scale_log2 = k;
     }
+    *refused = false;
     P.grad = c->grad;
     P.grad_half = half ? 1 : 0;
+    c->grad_used = c->frame_no;
     return built;
 }
 
@@ -879,16 +979,25 @@ bool ensure_grad(vr_ctx *c, MarchParams &P, hipStream_t s, bool half)
 // previous record, the new record also covers every earlier build, on whichever stream it ran
 // (a frame that reads a field built on one stream and builds another on its own, e.g. a
 // shaded skip-empty frame, or a later frame reading both).
-int ensure_derived(vr_ctx *c, const vr_params *p, MarchParams &P, hipStream_t s)
+int ensure_derived(vr_ctx *c, const vr_params *p, MarchParams &P, hipStream_t s, uint32_t *refused)
 {
-    if (c->built_recorded) HIP_TRY(c, hipStreamWaitEvent(s, c->built_ev, 0), "hipStreamWaitEvent(build)");
+    if (c->built_recorded) {  // once per stream and build record (a wait costs ~3.7 us of host time)
+        vr_ctx::Fence *f = fence_of(c, s);
+        if (!f || f->build_seen != c->build_gen) {
+            HIP_TRY(c, hipStreamWaitEvent(s, c->built_ev, 0), "hipStreamWaitEvent(build)");
+            if (f) f->build_seen = c->build_gen;
+        }
+    }
     const bool r0 = c->range_valid, d0 = c->dist_valid;
     if (p->skip_empty) {
         int rc = ensure_skip(c, P, s);
         if (rc) return rc;
+        if (!P.skip_empty) *refused = VR_DERIVED_SKIP;
     }
     // (a precision switch rebuilds a field that was valid on entry: ask ensure_grad, not the flag)
-    const bool g_built = p->shading && ensure_grad(c, P, s, p->exact_gradient == 0);
+    bool g_refused = false;
+    const bool g_built = p->shading && ensure_grad(c, P, s, p->exact_gradient == 0, &g_refused);
+    if (g_refused) *refused = VR_DERIVED_FIELD;
     const bool built = (!r0 && c->range_valid) || (!d0 && c->dist_valid) || g_built;
     if (built) return record_build(c, s);
     return VR_OK;
@@ -954,34 +1063,27 @@ int ensure_alt(vr_ctx *c, int lay, hipStream_t s, bool *ready)
     const size_t bytes = alt_bytes_for(c, lay);
     if (a.valid && a.bricks && a.bytes == bytes) {
         *ready = true;
+        a.used = c->frame_no;
         return VR_OK;
     }
     if (a.failed) return VR_OK;
     const size_t lin = (size_t)c->nx * c->ny * c->nz * sizeof(float);
     if (!a.bricks || a.bytes != bytes) {
         const size_t had = a.bricks ? a.bytes + kBrickSlackBytes : 0;
-        if (!budget_allows(c, bytes + kBrickSlackBytes, had)) {
-            // over the budget: drop the other views' copies (the next view change rebuilds
-            // them), then the difference field (read only by dense-row views, never by a frame
-            // that reads a copy), if that makes room; else this frame reads the 8^3 bricks
-            // (same pixels)
-            if (int rc = evict_alt_except(c, alt_index(lay), s)) return rc;
-            if (!budget_allows(c, bytes + kBrickSlackBytes, had) && c->grad) {
-                HIP_TRY(c, hipDeviceSynchronize(), "hipDeviceSynchronize (evict field)");
-                hipFree(c->grad);
-                c->grad = nullptr;
-                c->grad_bytes = 0;
-                c->grad_valid = false;
-            }
-            if (!budget_allows(c, bytes + kBrickSlackBytes, had)) return VR_OK;
-        }
-        if (a.bricks) hipFree(a.bricks);
+        // over the budget: the least recently read other copies, then the field (read only by
+        // dense-row views, never by a frame that reads a copy), make room; else this frame reads
+        // the 8^3 bricks (same pixels)
+        bool fits = false;
+        if (int rc = make_room(c, bytes + kBrickSlackBytes, had, alt_index(lay), false, s, &fits))
+            return rc;
+        if (!fits) return VR_OK;
+        if (int rc = release_async(c, a.bricks, s)) return rc;
         a.bricks = nullptr;
         a.bytes = 0;
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess ||
             free_b < bytes + kBrickSlackBytes + lin + (2ull << 30) ||
-            hipMalloc(&a.bricks, bytes + kBrickSlackBytes) != hipSuccess) {
+            hipMallocAsync(&a.bricks, bytes + kBrickSlackBytes, s) != hipSuccess) {
             (void)hipGetLastError();
             a.bricks = nullptr;
             a.failed = true;
@@ -998,6 +1100,8 @@ int ensure_alt(vr_ctx *c, int lay, hipStream_t s, bool *ready)
     if (e != hipSuccess) return hip_fail(c, e, "alt geometry copy");
     if (f != hipSuccess) return hip_fail(c, f, "hipFreeAsync(alt staging)");
     a.valid = true;
+    a.used = c->frame_no;
+    ++c->n_builds;
     *ready = true;
     // frames on other streams that read the copy wait for this build (ensure_derived; `s`
     // already waited on the previous build record there)
@@ -1263,6 +1367,31 @@ vr_ctx *create_members(const std::vector<int> &devices, uint32_t width, uint32_t
 
 bool vr::is_multi_device(const vr_ctx *c) { return is_group(c); }
 
+int vr::register_stream_fence(vr_ctx *c, hipStream_t stream, hipEvent_t ev)
+{
+    if (vr_ctx::Fence *f = fence_of(c, stream)) {
+        // the context's own fence of this stream: wait for its last record (the caller's event
+        // covers only the caller's frames; setup time, rare)
+        if (!f->external) {
+            HIP_TRY(c, hipEventSynchronize(f->ev), "hipEventSynchronize(fence)");
+            hipEventDestroy(f->ev);
+        }
+        *f = vr_ctx::Fence{stream, ev, c->frame_no, true, 0};
+        return VR_OK;
+    }
+    c->fences.push_back(vr_ctx::Fence{stream, ev, c->frame_no, true, 0});
+    return VR_OK;
+}
+
+void vr::unregister_stream_fence(vr_ctx *c, hipStream_t stream)
+{
+    for (size_t i = 0; i < c->fences.size(); ++i)
+        if (c->fences[i].stream == stream && c->fences[i].external) {
+            c->fences.erase(c->fences.begin() + (long)i);
+            return;
+        }
+}
+
 namespace {
 int render_device_impl(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out_dev,
                        int out_format, uint32_t row_block, uint32_t rank, uint32_t nranks,
@@ -1414,11 +1543,9 @@ void vr_destroy(vr_ctx *c)
     if (c->bricks) hipFree(c->bricks);
     if (c->tf) hipFree(c->tf);
     if (c->tf_nz) hipFree(c->tf_nz);
-    if (c->brick_range) hipFree(c->brick_range);
-    if (c->skip_dist) hipFree(c->skip_dist);
-    if (c->grad) hipFree(c->grad);
-    for (auto &a : c->alt)
-        if (a.bricks) hipFree(a.bricks);
+    free_derived(c);  // field, copies, skip-empty classification
+    for (auto &f : c->fences)
+        if (!f.external) hipEventDestroy(f.ev);
     for (auto &t : c->sched) {
         hipFree(t.cost);
         hipFree(t.perm);
@@ -1794,6 +1921,10 @@ int vr_memory_report(const vr_ctx *c, vr_memory_info *out)
     out->skip_bytes = c->nbricks_alloc * kSkipBytesPerBrick;
     out->derived_bytes = derived_bytes(c);
     out->budget_bytes = c->budget == VR_MEMORY_BUDGET_UNLIMITED ? c->budget : effective_budget(c);
+    out->builds = c->n_builds;
+    out->evictions = c->n_evictions;
+    out->downgrades = c->n_downgrades;
+    out->last_downgrade = c->last_downgrade;
     return VR_OK;
 }
 
@@ -1853,7 +1984,9 @@ int render_device_impl(vr_ctx *c, const vr_camera *cam, const vr_params *p, void
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     hipStream_t s = static_cast<hipStream_t>(stream);
-    rc = ensure_derived(c, p, P, s);
+    ++c->frame_no;
+    uint32_t refused = 0;  // VR_DERIVED_* the budget or free memory refused this frame
+    rc = ensure_derived(c, p, P, s, &refused);
     if (rc) return rc;
     if (use_pair(c, P, p)) {  // L lanes per ray on 16 x (16 / L) tiles (march_pair_kernel)
         // 4 lanes below kPairQuadMaxWaves (N = 8 C3 share: 0.151 -> 0.144 ms), else 2
@@ -1875,9 +2008,15 @@ int render_device_impl(vr_ctx *c, const vr_camera *cam, const vr_params *p, void
             P.vol_bytes = c->alt[alt_index(lay)].bytes;
             P.nbx = bricks_for(c->nx, 0, layout);
             P.nby = bricks_for(c->ny, 1, layout);
+        } else {
+            refused = (uint32_t)(VR_DERIVED_OBLIQUE_COPY + alt_index(lay));
         }
     }
     if (!launch) return VR_OK;
+    if (refused) {  // a budget-forced downgrade: recorded (vr_memory_report), never silent
+        ++c->n_downgrades;
+        c->last_downgrade = refused;
+    }
     vr_ctx::TileSched *ts =
         tile_sched(c, P, stream, tile_kernel_key(P, p->shading != 0, layout));
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1900,7 +2039,7 @@ int render_device_impl(vr_ctx *c, const vr_camera *cam, const vr_params *p, void
                 "tile order kernel");
         ts->have_perm = true;
     }
-    return VR_OK;
+    return fence_record(c, s);
 }
 }  // namespace
 extern "C" {
@@ -2090,7 +2229,8 @@ int vr_count_work(vr_ctx *c, const vr_camera *cam, const vr_params *p, uint32_t 
     int rc = build_params(c, cam, p, c->frame_dev, VR_OUT_RGBA8, row_block, rank, nranks,
                           c->share, P);
     if (rc) return rc;
-    rc = ensure_derived(c, p, P, nullptr);
+    uint32_t refused = 0;  // a count is not a frame: not a downgrade
+    rc = ensure_derived(c, p, P, nullptr, &refused);
     if (rc) return rc;
     HIP_TRY(c, hipMemset(c->counters, 0, 8 * sizeof(unsigned long long)), "hipMemset(counters)");
     HIP_TRY(c, launch_march(c->layout, p->shading != 0, true, P, nullptr), "march (count) launch");

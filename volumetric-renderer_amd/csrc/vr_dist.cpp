@@ -2,16 +2,14 @@
 //
 // Sort-first image tiling: each rank ray-marches its row blocks through the
 // public vr.h entry points, one ncclGather per frame collects the shards on rank 0 over xGMI,
-// and rank 0 de-interleaves them.  The whole frame is stream-ordered:
+// and rank 0 de-interleaves them.  The whole frame is stream-ordered (vr_frame_schedule.h):
 //
-//   slot stream k : render shard_k ─► [rendered_k]                 ┌► assemble (rank 0) ─► [done_k]
-//   comm stream   :        wait rendered_k ─► ncclGather ─► [gathered_k]
-//   slot stream k :                                 wait gathered_k┘
-//   caller stream : ... [called] ─────────────────────────────────────── wait done_k ...
+//   rank 0    slot stream k : [wait gathered_k] render shard_k ─► [rendered_k]
+//             caller stream : wait rendered_k ─► ncclGather ─► assemble ─► [gathered_k]
+//   rank r>0  slot stream k : render shard_k ─► wait gathered_(k-1) ─► ncclGather ─► [gathered_k]
 //
-// Frame i takes slot i mod F, so its render only queues behind frame i-F's assembly (which
-// frees shard_k and gbuf_k) and F frames are in flight.  The gathers are serialised on one
-// communication stream in frame order, which every rank issues identically.
+// Frame i takes slot i mod F, so F frames are in flight and consecutive renders overlap on the
+// device; the gathers run one at a time in frame order, which every rank issues identically.
 //
 // RCCL is resolved with dlopen at creation (the librccl.so.1 already loaded, e.g. PyTorch's,
 // else the system one), so single-GPU users of the library never load it.
@@ -25,6 +23,7 @@
 #include "vr_frame_workers.h"
 #include "vr_group.h"
 
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -122,13 +121,16 @@ struct CopyExchange {
         }
         cv.notify_all();
     }
-    // Waits until pred() holds (true) or the exchange is aborted / 120 s pass (false).
+    // Waits until pred() holds (true) or the exchange is aborted (false).  No time limit: a
+    // member held up in its enqueue (e.g. building a derived structure for a large volume) is
+    // slow, not failed, and a failing member aborts the exchange, which wakes every waiter
+    // (a 120 s limit used to fail a healthy context for good).
     template <class P>
     bool wait(P pred)
     {
         std::unique_lock<std::mutex> g(m);
-        return cv.wait_for(g, std::chrono::seconds(120), [&] { return aborted || pred(); }) &&
-               !aborted;
+        cv.wait(g, [&] { return aborted || pred(); });
+        return !aborted;
     }
 };
 
@@ -155,6 +157,7 @@ struct HipExec {
 
 struct vr_dist {
     vr_ctx *ctx = nullptr;
+    bool fences_registered = false;  // the slot streams' events are ctx's frame fences
     int device = 0;
     int nranks = 1, rank = 0;
     uint32_t row_block = 8, width = 0, height = 0, shard_rows = 0;
@@ -170,6 +173,8 @@ struct vr_dist {
     const vr_params *params = nullptr;
     bool timing = false;
     std::vector<TimedOp> t_render, t_gather, t_assemble;
+    bool hprof = false;       // host profiling (vr_dist_host_profile_enable)
+    vr_dist_host_profile hp{};
     std::string err;
 };
 
@@ -245,13 +250,36 @@ int timed_end(vr_dist *d, std::vector<TimedOp> &v, hipStream_t s)
     return VR_OK;
 }
 
-int HipExec::record(Event e, Stream s) { return hip_check(d, hipEventRecord(e, s), "hipEventRecord"); }
+// Host-time accumulator of one step of the frame path (only when d->hprof).
+struct HostSpan {
+    double *acc;
+    std::chrono::steady_clock::time_point t0;
+    explicit HostSpan(vr_dist *d, double vr_dist_host_profile::*field)
+        : acc(d->hprof ? &(d->hp.*field) : nullptr)
+    {
+        if (acc) t0 = std::chrono::steady_clock::now();
+    }
+    ~HostSpan()
+    {
+        if (acc)
+            *acc += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0)
+                        .count();
+    }
+};
+
+int HipExec::record(Event e, Stream s)
+{
+    HostSpan h(d, &vr_dist_host_profile::record_us);
+    return hip_check(d, hipEventRecord(e, s), "hipEventRecord");
+}
 int HipExec::wait(Stream s, Event e)
 {
+    HostSpan h(d, &vr_dist_host_profile::wait_us);
     return hip_check(d, hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent");
 }
 int HipExec::render(int slot, uint64_t, Stream s)
 {
+    HostSpan h(d, &vr_dist_host_profile::render_us);
     vr_params q = *d->params;
     q.frames_in_flight = (int32_t)d->sched.slots.size();
     DTRY(timed_begin(d, d->t_render, s));
@@ -281,7 +309,7 @@ int copy_gather(vr_dist *d, int slot, uint64_t frame, hipStream_t s)
         x.cv.notify_all();
         if (!x.wait([&] { return x.copied > frame; }))
             return dfail(d, VR_EIO, "copy exchange: member 0 did not copy frame " +
-                                        std::to_string(frame) + " (aborted or timed out)");
+                                        std::to_string(frame) + " (aborted)");
         return hip_check(d, hipStreamWaitEvent(s, x.peers[0]->bufs[slot].xev, 0),
                          "hipStreamWaitEvent(copies done)");
     }
@@ -292,7 +320,7 @@ int copy_gather(vr_dist *d, int slot, uint64_t frame, hipStream_t s)
         if (!x.wait([&] { return x.sent[m] > frame; }))
             return dfail(d, VR_EIO, "copy exchange: member " + std::to_string(m) +
                                         " did not render frame " + std::to_string(frame) +
-                                        " (aborted or timed out)");
+                                        " (aborted)");
         vr_dist *p = x.peers[m];
         DTRY(hip_check(d, hipStreamWaitEvent(s, p->bufs[slot].xev, 0),
                        "hipStreamWaitEvent(shard ready)"));
@@ -315,6 +343,7 @@ int copy_gather(vr_dist *d, int slot, uint64_t frame, hipStream_t s)
 
 int HipExec::gather(int slot, uint64_t frame, Stream s)
 {
+    HostSpan h(d, &vr_dist_host_profile::gather_us);
     const Buffers &b = d->bufs[slot];
     DTRY(timed_begin(d, d->t_gather, s));
     if (d->xch) {
@@ -338,6 +367,7 @@ int HipExec::gather(int slot, uint64_t frame, Stream s)
 }
 int HipExec::assemble(int slot, uint64_t, void *frame_dev, Stream s)
 {
+    HostSpan h(d, &vr_dist_host_profile::assemble_us);
     DTRY(timed_begin(d, d->t_assemble, s));
     if (vr_assemble_rows(d->ctx, d->bufs[slot].gbuf, frame_dev, d->out_format, d->row_block,
                          (uint32_t)d->nranks, s) != VR_OK) {
@@ -385,7 +415,11 @@ void release(vr_dist *d)
     auto &S = d->sched;
     for (auto &s : S.slots)
         if (s.stream) hipStreamSynchronize(s.stream);
-    if (S.comm) hipStreamSynchronize(S.comm);
+    // rank 0's gathers and assemblies ran on the callers' streams
+    if (hipEvent_t e = S.last_gathered()) hipEventSynchronize(e);
+    if (d->fences_registered)
+        for (auto &s : S.slots) vr::unregister_stream_fence(d->ctx, s.stream);
+    d->fences_registered = false;
     if (d->comm && d->owns_comm) rccl().comm_destroy(d->comm);
     free_timing(d);
     for (auto &b : d->bufs) {
@@ -394,12 +428,10 @@ void release(vr_dist *d)
         if (b.xev) hipEventDestroy(b.xev);
     }
     for (auto &s : S.slots) {
-        for (hipEvent_t e : {s.rendered, s.gathered, s.done})
+        for (hipEvent_t e : {s.rendered, s.gathered})
             if (e) hipEventDestroy(e);
         if (s.stream) hipStreamDestroy(s.stream);
     }
-    if (S.called) hipEventDestroy(S.called);
-    if (S.comm) hipStreamDestroy(S.comm);
     S.slots.clear();
     d->bufs.clear();
 }
@@ -423,9 +455,6 @@ int setup(vr_dist *d, const void *id, ncclComm_t comm, int frames)
     }
     auto &S = d->sched;
     S.rank = d->rank;
-    DTRY(hip_check(d, hipStreamCreateWithFlags(&S.comm, hipStreamNonBlocking),
-                   "hipStreamCreate(comm)"));
-    DTRY(hip_check(d, hipEventCreateWithFlags(&S.called, hipEventDisableTiming), "hipEventCreate"));
     const size_t sbytes = shard_bytes(d);
     S.slots.resize(frames);
     d->bufs.resize(frames);
@@ -440,9 +469,15 @@ int setup(vr_dist *d, const void *id, ncclComm_t comm, int frames)
         if (d->xch)
             DTRY(hip_check(d, hipEventCreateWithFlags(&b.xev, hipEventDisableTiming),
                            "hipEventCreate(exchange)"));
-        for (hipEvent_t *e : {&s.rendered, &s.gathered, &s.done})
+        for (hipEvent_t *e : {&s.rendered, &s.gathered})
             DTRY(hip_check(d, hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate"));
     }
+    // the event recorded on a slot stream after each of its renders (rank 0: rendered, after the
+    // render; rank r > 0: gathered, after the render and the gather) is the context's frame
+    // fence there: the context records none of its own (vr_group.h)
+    for (auto &s : S.slots)
+        DTRY(vr::register_stream_fence(d->ctx, s.stream, d->rank == 0 ? s.rendered : s.gathered));
+    d->fences_registered = true;
     return VR_OK;
 }
 
@@ -529,6 +564,7 @@ int vr_dist_render(vr_dist *d, const vr_camera *cam, const vr_params *p, void *f
                    void *stream)
 {
     if (!d) return dfail(nullptr, VR_EINVAL, "dist is NULL");
+    HostSpan total(d, &vr_dist_host_profile::total_us);
     if (!cam || !p) return dfail(d, VR_EINVAL, "camera or params is NULL");
     if (d->rank == 0 && !frame_dev) return dfail(d, VR_EINVAL, "rank 0 needs frame_dev");
     uint32_t w = 0, h = 0, s0 = 1, s1 = 1;
@@ -546,7 +582,23 @@ int vr_dist_render(vr_dist *d, const vr_camera *cam, const vr_params *p, void *f
     const int rc = d->sched.issue(x, static_cast<hipStream_t>(stream), frame_dev);
     d->cam = nullptr;
     d->params = nullptr;
+    if (d->hprof) ++d->hp.frames;
     return rc;
+}
+
+int vr_dist_host_profile_enable(vr_dist *d, int enable)
+{
+    if (!d) return dfail(nullptr, VR_EINVAL, "dist is NULL");
+    d->hprof = enable != 0;
+    return VR_OK;
+}
+
+int vr_dist_host_profile_read(vr_dist *d, vr_dist_host_profile *out)
+{
+    if (!d || !out) return dfail(d, VR_EINVAL, "NULL argument");
+    *out = d->hp;
+    d->hp = vr_dist_host_profile{};
+    return VR_OK;
 }
 
 int vr_dist_synchronize(vr_dist *d)
@@ -555,7 +607,10 @@ int vr_dist_synchronize(vr_dist *d)
     DTRY(hip_check(d, hipSetDevice(d->device), "hipSetDevice"));
     for (auto &s : d->sched.slots)
         DTRY(hip_check(d, hipStreamSynchronize(s.stream), "hipStreamSynchronize"));
-    return hip_check(d, hipStreamSynchronize(d->sched.comm), "hipStreamSynchronize");
+    // rank 0's gathers and assemblies run on the callers' streams: the last one's event
+    if (hipEvent_t e = d->sched.last_gathered())
+        return hip_check(d, hipEventSynchronize(e), "hipEventSynchronize");
+    return VR_OK;
 }
 
 int vr_dist_timing_enable(vr_dist *d, int enable)
@@ -622,9 +677,11 @@ struct Group {
     // frame counters start at 0 with the pipelines'); comms stay null
     int exchange = VR_EXCHANGE_RCCL;
     std::unique_ptr<CopyExchange> xch;
-    // vr_debug_fail_member: member fail_member's issue of pipeline frame fail_frame fails
-    int fail_member = -1;
-    uint64_t fail_frame = 0;
+    // vr_debug_fail_member: member fail_member's issue of pipeline frame fail_frame fails.
+    // Written by the API thread while the frame workers read them (member_issue): atomics, the
+    // frame stored before the member (release) and read after it (acquire).
+    std::atomic<int> fail_member{-1};
+    std::atomic<uint64_t> fail_frame{0};
 };
 
 namespace {
@@ -633,7 +690,8 @@ int member_issue(Group *g, int m, const GroupJob &j, std::string *msg)
 {
     vr_dist *d = g->dists[m];
     int rc;
-    if (m == g->fail_member && d->sched.frame == g->fail_frame)
+    if (m == g->fail_member.load(std::memory_order_acquire) &&
+        d->sched.frame == g->fail_frame.load(std::memory_order_relaxed))
         rc = dfail(d, VR_EIO, "injected failure (vr_debug_fail_member) of frame " +
                                   std::to_string(d->sched.frame));
     else
@@ -850,8 +908,8 @@ int group_fail_member(Group *g, int member, uint64_t frame, std::string *err)
         return VR_EINVAL;
     }
     // frames count from the next pipeline build; the current pipelines' counter otherwise
-    g->fail_member = member;
-    g->fail_frame = frame;
+    g->fail_frame.store(frame, std::memory_order_relaxed);
+    g->fail_member.store(member, std::memory_order_release);
     return VR_OK;
 }
 

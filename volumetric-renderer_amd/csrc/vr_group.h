@@ -25,6 +25,14 @@ constexpr uint32_t kGroupRowBlock = 8;
 // True for a vr_create_mask context (vr_api.hip).
 bool is_multi_device(const vr_ctx *c);
 
+// Frame fences of a context (vr_api.hip): every render on a stream is followed by a record of the
+// stream's fence event, which evictions of derived structures wait on.  A caller that itself
+// records `ev` on `stream` after every render it issues there before its next render call (a
+// vr_dist slot stream) registers it, and the context records nothing of its own on that stream;
+// unregister after the stream's work is complete, before the event or the stream is destroyed.
+int register_stream_fence(vr_ctx *c, hipStream_t stream, hipEvent_t ev);
+void unregister_stream_fence(vr_ctx *c, hipStream_t stream);
+
 // The frame exchange over the members' devices (member 0 = the frame's device):
 // VR_EXCHANGE_RCCL, one communicator per member from ncclCommInitAll (distinct devices), or
 // VR_EXCHANGE_COPY, device copies onto member 0 (any devices, the same one repeated included).

@@ -187,9 +187,10 @@ struct vr_sched_host {
 
 extern "C" {
 
-// rank/frames_in_flight as vr_dist_create; fn(user, op, slot, frame) runs render (0) and
-// assemble (2) on slot streams, gather (1) on the communication stream and consume (3) -- the
-// application's use of rank 0's finished frame -- on the caller stream.  NULL on bad args.
+// rank/frames_in_flight as vr_dist_create; fn(user, op, slot, frame) runs render (0) on slot
+// streams, gather (1) on rank 0's caller stream or rank r > 0's slot streams, assemble (2) and
+// consume (3) -- the application's use of rank 0's finished frame -- on the caller stream, as
+// vr_frame_schedule.h places them.  NULL on bad args.
 vr_sched_host *vr_sched_host_create(int rank, int frames_in_flight, vr_sched_op_fn fn, void *user)
 {
     if (rank < 0 || frames_in_flight < 1 || frames_in_flight > 8 || !fn) return nullptr;
@@ -199,14 +200,11 @@ vr_sched_host *vr_sched_host_create(int rank, int frames_in_flight, vr_sched_op_
     h->x.user = user;
     auto &S = h->sched;
     S.rank = rank;
-    S.comm = h->new_stream();
-    S.called = h->new_event();
     S.slots.resize(frames_in_flight);
     for (auto &s : S.slots) {
         s.stream = h->new_stream();
         s.rendered = h->new_event();
         s.gathered = h->new_event();
-        s.done = h->new_event();
     }
     h->caller = h->new_stream();
     return h;

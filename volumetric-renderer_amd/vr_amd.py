@@ -63,10 +63,20 @@ class vr_orbit_camera(C.Structure):
                 ("radius", C.c_float)]
 
 
-class vr_memory_info(C.Structure):  # vr.h (ABI 7)
+class vr_memory_info(C.Structure):  # vr.h (ABI 7; history fields ABI 9)
     _fields_ = [(n, C.c_uint64) for n in (
         "volume_bytes", "field_bytes", "oblique_copy_bytes", "plain_copy_bytes",
-        "stencil_copy_bytes", "skip_bytes", "derived_bytes", "budget_bytes")]
+        "stencil_copy_bytes", "skip_bytes", "derived_bytes", "budget_bytes",
+        "builds", "evictions", "downgrades", "last_downgrade")]
+
+
+class vr_dist_host_profile(C.Structure):  # vr_dist.h
+    _fields_ = [("frames", C.c_uint64)] + [(n, C.c_double) for n in (
+        "render_us", "gather_us", "assemble_us", "record_us", "wait_us", "total_us")]
+
+
+# vr.h enum vr_derived (vr_memory_info.last_downgrade)
+DERIVED = {1: "field", 2: "oblique_copy", 3: "plain_copy", 4: "stencil_copy", 5: "skip"}
 
 
 class vr_member_timing(C.Structure):  # vr_debug.h (ABI 7)
@@ -105,6 +115,7 @@ HOST_SYMBOLS = [
 DIST_SYMBOLS = [
     "vr_dist_unique_id", "vr_dist_create", "vr_dist_render", "vr_dist_synchronize",
     "vr_dist_last_error", "vr_dist_destroy", "vr_dist_timing_enable", "vr_dist_timing_read",
+    "vr_dist_host_profile_enable", "vr_dist_host_profile_read",
 ]
 DIST_ID_BYTES = 128  # include/vr/vr_dist.h VR_DIST_ID_BYTES
 DEBUG_SYMBOLS = ["vr_debug_set_knob", "vr_debug_get_knob", "vr_debug_timing_member",
@@ -117,7 +128,7 @@ KNOBS = {"pipeline": 1, "pair": 2, "pair_lanes": 3, "grad_field": 4, "u8_layout"
 KNOB_AUTO = {"pipeline": -1, "pair": -1, "pair_lanes": 0, "grad_field": -1,
              "u8_layout": -1, "tile_order": 0, "narrow": 1, "alt_geometry": -1}
 
-ABI_VERSION = 8  # include/vr/vr.h VR_ABI_VERSION
+ABI_VERSION = 9  # include/vr/vr.h VR_ABI_VERSION
 _LIB = None
 
 
@@ -158,6 +169,8 @@ def lib() -> C.CDLL:
         "vr_dist_last_error": (C.c_char_p, [vp]),
         "vr_dist_destroy": (None, [vp]),
         "vr_dist_timing_enable": (i32, [vp, i32]),
+        "vr_dist_host_profile_enable": (i32, [vp, i32]),
+        "vr_dist_host_profile_read": (i32, [vp, C.POINTER(vr_dist_host_profile)]),
         "vr_dist_timing_read": (i32, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                       C.POINTER(C.c_uint64)]),
         "vr_set_volume": (i32, [vp, vp, i32, u32, u32, u32, f32, f32]),
@@ -651,6 +664,19 @@ class DistFrames:
     def timing_enable(self, on: bool = True):
         self._check(lib().vr_dist_timing_enable(self._d, 1 if on else 0), "vr_dist_timing_enable")
 
+    def host_profile(self, enable=None):
+        """Host microseconds per frame of each step vr_dist_render enqueues (vr_dist.h host
+        profile), averaged since the last read, and the frames counted; enable=True/False
+        switches the profiling first (then returns None)."""
+        if enable is not None:
+            self._check(lib().vr_dist_host_profile_enable(self._d, 1 if enable else 0),
+                        "vr_dist_host_profile_enable")
+            return None
+        h = vr_dist_host_profile()
+        self._check(lib().vr_dist_host_profile_read(self._d, C.byref(h)), "vr_dist_host_profile_read")
+        n = max(int(h.frames), 1)
+        return dict(frames=int(h.frames), **{k: getattr(h, k) / n for k, _ in vr_dist_host_profile._fields_[1:]})
+
     def timing_read(self):
         """(render ms, gather ms, frames) summed over the frames since timing was enabled (or
         last read): HIP events around this rank's render and its ncclGather."""
@@ -694,13 +720,15 @@ def _elf_sections(b: bytes, base: int = 0):
 
 
 def kernel_code_hash(path: Optional[str] = None) -> str:
-    """sha256 (16 hex digits) of the ray-march kernels' machine code in the library: every
-    march_kernel instantiation's gfx950 code bytes and kernel descriptor (register counts, LDS,
-    kernarg size; the descriptor's layout-dependent code-entry offset zeroed), read from the
-    code object in the `.hip_fatbin` ELF section.  Keys measured per-kernel figures (the PMC
-    traffic bench.py's roofline reads) to the machine code they were measured on: host-only
-    edits and changes to other kernels leave it unchanged, any change to the march kernels
-    moves it (the build is deterministic)."""
+    """sha256 (16 hex digits) of the frame kernels' machine code in the library: every
+    instantiation of march_kernel, march_pair_kernel (lane groups: small row shares) and
+    order_tiles_kernel (the adaptive tile order inside a frame) -- gfx950 code bytes and kernel
+    descriptor (register counts, LDS, kernarg size; the descriptor's layout-dependent
+    code-entry offset zeroed), read from the code object in the `.hip_fatbin` ELF section.
+    Keys measured per-kernel figures (the PMC traffic bench.py's roofline reads) to the machine
+    code they were measured on: host-only edits and changes to other kernels leave it
+    unchanged, any change to a kernel a frame launches moves it (the build is deterministic;
+    ADVICE r5: the pair and tile-order kernels were not hashed before)."""
     import hashlib
     import re
     import struct
@@ -725,7 +753,9 @@ def kernel_code_hash(path: Optional[str] = None) -> str:
             for i in range(st[6] // 24):
                 nm, _, _, shndx, val, sz = struct.unpack_from("<IBBHQQ", co, st[5] + i * 24)
                 name = co[strt[5] + nm:co.index(b"\0", strt[5] + nm)]
-                if b"12march_kernel" in name and 0 < shndx < len(secs) and sz > 0:
+                frame_kernel = any(k in name for k in (b"12march_kernel", b"17march_pair_kernel",
+                                                         b"18order_tiles_kernel"))
+                if frame_kernel and 0 < shndx < len(secs) and sz > 0:
                     sec = secs[shndx]
                     code = bytearray(co[sec[5] + val - sec[4]:sec[5] + val - sec[4] + sz])
                     if name.endswith(b".kd") and len(code) >= 24:
