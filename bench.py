@@ -68,7 +68,7 @@ GATHER = "native"  # N > 1 over RCCL: "native" (vr_dist.h) or "torch" (torch.dis
 # pipelined frames 10-15% slower (profiles/r02/warm_state/), so a fixed warm-up makes each
 # number independent of what ran before it.  The frames actually run are recorded.
 STEADY_WARMUP = 120
-BUDGET_DEFAULT = 2 ** 64 - 2  # vr.h VR_MEMORY_BUDGET_DEFAULT (ABI 8)
+BUDGET_DEFAULT = 2 ** 64 - 2  # vr.h VR_MEMORY_BUDGET_DEFAULT (ABI 8; 5x the bricks since ABI 9)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "Gsamples/sec + fps, 512³ NRRD @ 1080p; achieved HBM GB/s vs peak"
 
@@ -346,52 +346,63 @@ def orbit_cameras(n=360):
 
 
 def orbit(rp, cfg, frame_ptr, n=360):
-    """The renderer under a moving camera: the orbit path, default memory
-    budget, derived structures freed first.  Serial frames timed on the host (enqueue + device
-    synchronize: every build, eviction and kernel switch on the path lands in its frame) ->
-    p50 / p99 / max; then the same path with 3 frames in flight (ms per frame over the path);
-    the library's derived-structure history (builds, evictions, downgrades) for each pass."""
+    """The renderer under a moving camera: the orbit path (orbit_cameras),
+    default memory budget, derived structures freed first.  Two laps of serial frames, each timed
+    on the host (enqueue + device synchronize: every build, eviction and kernel switch on the
+    path lands in its frame): the first lap builds what the views want, the second runs on what
+    the first left.  Reported per lap: p50 / p99 / max frame ms and the library's derived-
+    structure history (builds, evictions, downgrades).  The frame time also varies with the
+    view's own work (samples per frame move 3-4x along the path), so two stability figures sit
+    beside p99 / p50: each frame's time over the same camera's second-lap time (spikes from
+    builds and evictions; p99 and the frames above 1.5x), and ns per executed sample (p99 /
+    p50).  Then the same path with 3 frames in flight (ms per frame over the path)."""
     cams = orbit_cameras(n)
     p1 = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"])
     p3 = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"], frames_in_flight=3)
     stream = torch.cuda.current_stream().cuda_stream
+    hist = ("builds", "evictions", "downgrades")
 
     def history():
         m = rp.memory_report()
-        return {k: m[k] for k in ("builds", "evictions", "downgrades", "derived_bytes", "budget_bytes")}
+        return {k: m[k] for k in hist + ("derived_bytes", "budget_bytes")}
 
     def fresh():
         rp.set_memory_budget(0)
         rp.set_memory_budget(BUDGET_DEFAULT)
         torch.cuda.synchronize()
 
+    def lap():
+        h0 = history()
+        t = []
+        for cam in cams:
+            t0 = time.perf_counter()
+            rp.render_device(cam, p1, frame_ptr, vr_amd.OUT_RGBA8, 8, 0, 1, stream)
+            torch.cuda.synchronize()
+            t.append((time.perf_counter() - t0) * 1e3)
+        h1 = history()
+        t = np.array(t)
+        return t, dict(p50_ms=round(float(np.percentile(t, 50)), 4),
+                       p99_ms=round(float(np.percentile(t, 99)), 4), max_ms=round(float(t.max()), 4),
+                       mean_ms=round(float(t.mean()), 4),
+                       p99_over_p50=round(float(np.percentile(t, 99) / np.percentile(t, 50)), 3),
+                       slowest_frames=[int(i) for i in np.argsort(-t)[:5]],
+                       **{k: h1[k] - h0[k] for k in hist})
+
     fresh()
-    h0 = history()
-    times = []
-    for cam in cams:
-        t0 = time.perf_counter()
-        rp.render_device(cam, p1, frame_ptr, vr_amd.OUT_RGBA8, 8, 0, 1, stream)
-        torch.cuda.synchronize()
-        times.append((time.perf_counter() - t0) * 1e3)
-    h1 = history()
-    t = np.array(times)
-    serial = dict(p50_ms=round(float(np.percentile(t, 50)), 4), p99_ms=round(float(np.percentile(t, 99)), 4),
-                  max_ms=round(float(t.max()), 4), mean_ms=round(float(t.mean()), 4),
-                  slowest_frames=[int(i) for i in np.argsort(-t)[:5]],
-                  **{k: h1[k] - h0[k] for k in ("builds", "evictions", "downgrades")})
-    serial["p99_over_p50"] = round(serial["p99_ms"] / serial["p50_ms"], 3)
-    # second lap, structures as the first lap left them (a user dragging on)
-    times2 = []
-    for cam in cams:
-        t0 = time.perf_counter()
-        rp.render_device(cam, p1, frame_ptr, vr_amd.OUT_RGBA8, 8, 0, 1, stream)
-        torch.cuda.synchronize()
-        times2.append((time.perf_counter() - t0) * 1e3)
-    h2 = history()
-    t2 = np.array(times2)
-    lap2 = dict(p50_ms=round(float(np.percentile(t2, 50)), 4), p99_ms=round(float(np.percentile(t2, 99)), 4),
-                max_ms=round(float(t2.max()), 4),
-                **{k: h2[k] - h1[k] for k in ("builds", "evictions", "downgrades")})
+    t1, lap1 = lap()
+    t2, lap2 = lap()
+    mem = history()
+    samples = np.array([rp.count_work(c, p1, 8)["samples"] for c in cams], dtype=np.float64)
+    ratio = t1 / t2
+    nsps = t2 * 1e6 / np.maximum(samples, 1.0)
+    stability = dict(
+        first_lap_over_steady_p99=round(float(np.percentile(ratio, 99)), 3),
+        first_lap_frames_above_1p5x_steady=int((ratio > 1.5).sum()),
+        second_lap_over_first_lap_steady_p99=round(float(np.percentile(t2 / np.minimum(t1, t2), 99)), 3),
+        ns_per_sample_p50=round(float(np.percentile(nsps, 50)), 4),
+        ns_per_sample_p99=round(float(np.percentile(nsps, 99)), 4),
+        ns_per_sample_p99_over_p50=round(float(np.percentile(nsps, 99) / np.percentile(nsps, 50)), 3),
+        samples_per_frame_min_max=[int(samples.min()), int(samples.max())])
     # frames in flight over the same path (fresh structures)
     fresh()
     hp = history()
@@ -407,10 +418,11 @@ def orbit(rp, cfg, frame_ptr, n=360):
     h3 = history()
     return dict(path=f"{n} frames of Camera::rotate((4, 1)) with the radius 1.6 -> 3.0 -> 1.6, C3 "
                      "volume and params, default memory budget, derived structures freed first",
-                serial_frames=serial, second_lap=lap2,
+                first_lap=lap1, second_lap=lap2, stability=stability,
                 frames_in_flight_3=dict(ms_per_frame=round(pip, 4),
-                                        **{k: h3[k] - hp[k] for k in ("builds", "evictions", "downgrades")}),
-                memory_after=h2)
+                                        gsamples_per_s=round(float(samples.sum()) / (pip * 1e-3 * n) / 1e9, 3),
+                                        **{k: h3[k] - hp[k] for k in hist}),
+                memory_after=mem)
 
 
 def host_cores():
@@ -948,7 +960,7 @@ def main():
             # device memory of the context after the run, per device (a multi-device context
             # replicates the volume and its derived structures on every device): bricks,
             # derived structures (difference field, alternative copies, skip-empty) and the
-            # budget that caps them (vr.h VR_MEMORY_BUDGET_DEFAULT: 4x the bricks)
+            # budget that caps them (vr.h VR_MEMORY_BUDGET_DEFAULT: 5x the bricks)
             "memory_per_device": memory,
             "frame_check": R["check"],  # N > 1: assembled frame == single-GPU frame, bit for bit
             "per_rank": R["per_rank"],

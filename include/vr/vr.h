@@ -298,10 +298,10 @@ int vr_release_external_memory(vr_ctx *ctx, vr_external_memory *mem);
  * structure that would not fit is not built, and its frames read the bricks instead (the same
  * pixels; with the binary16 field absent a shaded frame forms exact f32 differences, i.e. the
  * exact_gradient = 1 pixels).  An alternative copy may evict the others to fit.  0 keeps only
- * the bricks.  VR_MEMORY_BUDGET_DEFAULT (ABI 8, the default) is 4x the bricked volume's bytes
- * (+ the skip-empty classification): the difference field (3x) and one alternative copy, e.g.
- * C3 512^3 f32: 1.6 GB of bricks, at most 6.4 GB derived (the field and the default camera's
- * stencil copy, 5.6 GB).  VR_MEMORY_BUDGET_UNLIMITED builds whatever fits beside a 2 GiB
+ * the bricks.  VR_MEMORY_BUDGET_DEFAULT (the default) is 5x the bricked volume's bytes (ABI 9;
+ * 4x in ABI 8) (+ the skip-empty classification): the difference field (3x) and the oblique and
+ * stencil copies a shaded camera orbit visits, e.g. C3 512^3 f32: 1.6 GB of bricks, at most
+ * 8.0 GB derived (the three: 7.1 GB).  VR_MEMORY_BUDGET_UNLIMITED builds whatever fits beside a 2 GiB
  * free-memory reserve (ABI 7's default).  A multi-device context applies the budget on every
  * device (each holds its replica's structures).
  * (ABI 9) A structure that does not fit evicts the least recently read others, one at a time,

@@ -48,7 +48,7 @@ enum vr_knob {
  * context has member 0 only, kernel time alone):
  *   kernel_ms    its ray-march kernels (HIP events around each launch)
  *   render_ms    its render step on its slot streams (the march plus the tile-order kernel)
- *   gather_ms    its ncclGather on its communication stream (member 0: receiving every shard)
+ *   gather_ms    its ncclGather (member 0: on the caller's stream, receiving every shard)
  *   assemble_ms  member 0: the de-interleave of the gathered shards into the frame
  *   frames       frames timed on that member
  * (vr_timing_read on a multi-device context sums kernel_ms over the devices.) */

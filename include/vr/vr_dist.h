@@ -13,7 +13,10 @@
  * rotate over `frames_in_flight` internal slots, each with its own stream, shard and gather
  * buffer, so frame k+1 renders while frame k's gather is on the wire and consecutive frames
  * overlap on the device (the reference keeps MAX_FRAMES_IN_FLIGHT = 2,
- * vulkan_context.h:17).  The gathers run in frame order on one communication stream.
+ * vulkan_context.h:17).  The gathers run one at a time in frame order: on rank 0 on the
+ * caller's stream, followed there by the assembly; on the other ranks on the slot streams,
+ * each after the previous frame's (2 event records + 2 stream waits per frame on rank 0, 1 + 1
+ * elsewhere; csrc/vr_frame_schedule.h).
  *
  * RCCL is loaded at vr_dist_create time (the librccl.so.1 already in the process, e.g.
  * PyTorch's, else the system one); single-GPU users of vr.h never load it.  Bootstrap: rank
@@ -48,11 +51,14 @@ vr_dist *vr_dist_create(vr_ctx *ctx, const void *id, int nranks, int rank, uint3
                         int frames_in_flight);
 
 /* One frame: render this rank's rows, gather to rank 0, assemble there into frame_dev
- * (rank 0: W*H*4 bytes of device memory, RGBA8; ignored elsewhere).  Asynchronous: the
- * frame is complete once `stream` (the caller's hipStream_t, NULL = default) passes the
- * point of this call; work the caller enqueued on `stream` before the call (e.g. reading
- * frame_dev's previous contents) happens before frame_dev is written.  Every rank must
- * call it for every frame, in the same order, with the same camera and params. */
+ * (rank 0: W*H*4 bytes of device memory, RGBA8; ignored elsewhere).  Asynchronous: on rank 0
+ * the frame is complete once `stream` (the caller's hipStream_t, NULL = default) passes the
+ * point of this call, and work the caller enqueued on `stream` before the call (e.g. reading
+ * frame_dev's previous contents) happens before frame_dev is written; rank 0's `stream` must
+ * stay alive until the frame is complete (vr_dist_synchronize waits for it through an event
+ * recorded there).  On the other ranks the call only enqueues: `stream` is not used, and
+ * vr_dist_synchronize waits for the frames.  Every rank must call it for every frame, in the
+ * same order, with the same camera and params. */
 int vr_dist_render(vr_dist *d, const vr_camera *cam, const vr_params *p, void *frame_dev,
                    void *stream);
 

@@ -80,6 +80,7 @@ def test_least_recently_read_structure_is_evicted_and_frames_unchanged(gpu):
     try:
         v = _views()
         p = vr_amd.default_params(shading=1, ert_eps=1e-5, exact_gradient=1, frames_in_flight=3)
+        rp.set_memory_budget(BUDGET_UNLIMITED)  # the references: every structure resident
         ref = {k: rp.render(c, p, vr_amd.OUT_RGBA32F) for k, c in v.items()}
         m = rp.memory_report()
         F, O, S = m["field_bytes"], m["oblique_copy_bytes"], m["stencil_copy_bytes"]

@@ -6,7 +6,7 @@ profile's per-dispatch durations can be matched.  Frames go to a device buffer i
 each (vr_render_device): vr_render splits host-output frames into row bands.
   python tools/prof_run.py [--n 512] [--dtype float32] [--size 1920x1080] [--cam fill]
                            [--tf tf2] [--shading 1] [--ert 1e-5] [--frames 10] [--tile-order 0]
-                           [--skip-empty 0] [--exact-gradient 0]
+                           [--skip-empty 0] [--exact-gradient 0] [--knob name=value]
 """
 import argparse
 import json
@@ -37,9 +37,15 @@ def main():
     ap.add_argument("--skip-empty", type=int, default=0)
     ap.add_argument("--wave-shape", type=int, default=0)
     ap.add_argument("--exact-gradient", type=int, default=0)
+    ap.add_argument("--knob", action="append", default=[],
+                    help="name=value: a vr_debug.h launch-policy knob, set before the upload "
+                         "(e.g. u8_layout=1)")
     a = ap.parse_args()
     W, H = (int(x) for x in a.size.split("x"))
     rp = vr_amd.OffscreenPass(W, H)
+    for kv in a.knob:
+        k, v = kv.split("=")
+        rp.set_knob(k, int(v))
     rp.generate_volume((a.n,) * 3, np.dtype(a.dtype), seed=2024)
     rp.transfer_function_changed(synth.TFS[a.tf]())
     cam = synth.camera(a.cam).to_vr_camera()

@@ -174,6 +174,9 @@ int fail(vr_ctx *c, int code, const std::string &msg)
 int hip_fail(vr_ctx *c, hipError_t e, const char *what)
 {
     std::string m = std::string(what) + ": " + hipGetErrorString(e);
+    // reported here: clear the thread's last error, which the launch helpers read after each
+    // launch (a stale one would fail the next, unrelated launch)
+    (void)hipGetLastError();
     return fail(c, e == hipErrorOutOfMemory ? VR_ENOMEM : VR_EIO, m);
 }
 
@@ -750,10 +753,13 @@ size_t derived_bytes(const vr_ctx *c)
         if (a.bricks) b += a.bytes + kBrickSlackBytes;
     return b + c->nbricks_alloc * kSkipBytesPerBrick;
 }
-// The default budget: the difference field (3x the bricks) plus one alternative copy (about 1x),
-// plus the skip-empty classification -- at C3 the field and the default camera's stencil copy
-// (5.6 GB beside 1.6 GB of bricks) fit, and a third structure evicts a copy.
-constexpr uint64_t kDerivedBudgetBricks = 4;
+// The default budget (ABI 9): the difference field (3x the bricks) plus the copies a shaded camera
+// orbit visits (the oblique copy, about 1x, and the stencil copy, about 0.5x), plus the skip-empty
+// classification -- at C3 the field, the oblique and the stencil copy (7.1 GB beside 1.6 GB of
+// bricks) fit, so the reference's drag orbit builds each once and evicts nothing (4x thrashed:
+// 4 builds and 4 evictions per lap, profiles/r06/orbit/).  A fourth structure evicts the least
+// recently read.
+constexpr uint64_t kDerivedBudgetBricks = 5;
 uint64_t effective_budget(const vr_ctx *c)
 {
     if (c->budget != VR_MEMORY_BUDGET_DEFAULT) return c->budget;
@@ -802,11 +808,23 @@ int fence_record(vr_ctx *c, hipStream_t s)
     HIP_TRY(c, hipEventRecord(f->ev, s), "hipEventRecord(fence)");
     return VR_OK;
 }
-// Order `s` after every frame issued so far on every other stream (a structure's readers).
+// Order `s` after every frame issued so far on every other stream (a structure's readers).  A
+// caller may have destroyed a stream it rendered on (ROCm then refuses waits on events recorded
+// there, reading the dead stream's capture state): the device is drained instead, once, and the
+// context's own fences are dropped (all complete).
 int fence_others(vr_ctx *c, hipStream_t s)
 {
     for (const auto &x : c->fences)
-        if (x.stream != s) HIP_TRY(c, hipStreamWaitEvent(s, x.ev, 0), "hipStreamWaitEvent(fence)");
+        if (x.stream != s && hipStreamWaitEvent(s, x.ev, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            HIP_TRY(c, hipDeviceSynchronize(), "hipDeviceSynchronize (fence fallback)");
+            for (size_t i = c->fences.size(); i-- > 0;)
+                if (!c->fences[i].external) {
+                    hipEventDestroy(c->fences[i].ev);
+                    c->fences.erase(c->fences.begin() + (long)i);
+                }
+            return VR_OK;
+        }
     return VR_OK;
 }
 // Free a derived structure that frames in flight may still read: stream-ordered on `s`, after
@@ -1381,6 +1399,26 @@ int vr::register_stream_fence(vr_ctx *c, hipStream_t stream, hipEvent_t ev)
     }
     c->fences.push_back(vr_ctx::Fence{stream, ev, c->frame_no, true, 0});
     return VR_OK;
+}
+
+// Fold the kernel-timing event pairs into the totals (vr_timing_read), e.g. before the streams
+// they were recorded on are destroyed: ROCm refuses to synchronise an event whose recording
+// stream is gone.  The caller has drained those streams.
+void vr::settle_timing(vr_ctx *c)
+{
+    for (auto &pr : c->ev_pending) {
+        float ms = 0.0f;
+        if (hipEventSynchronize(pr.second) == hipSuccess &&
+            hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) {
+            c->timed_ms += ms;
+            c->timed_launches++;
+        } else {
+            (void)hipGetLastError();
+        }
+        c->ev_pool.push_back(pr.first);
+        c->ev_pool.push_back(pr.second);
+    }
+    c->ev_pending.clear();
 }
 
 void vr::unregister_stream_fence(vr_ctx *c, hipStream_t stream)
@@ -2312,7 +2350,11 @@ int vr_timing_read(vr_ctx *c, double *total_ms, uint64_t *launches)
     }
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     for (auto &pr : c->ev_pending) {
-        HIP_TRY(c, hipEventSynchronize(pr.second), "hipEventSynchronize");
+        if (hipEventSynchronize(pr.second) != hipSuccess) {
+            // recorded on a stream the caller destroyed since (fence_others): drain the device
+            (void)hipGetLastError();
+            HIP_TRY(c, hipDeviceSynchronize(), "hipDeviceSynchronize (timing)");
+        }
         float ms = 0.0f;
         HIP_TRY(c, hipEventElapsedTime(&ms, pr.first, pr.second), "hipEventElapsedTime");
         c->timed_ms += ms;

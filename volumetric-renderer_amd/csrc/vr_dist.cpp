@@ -192,6 +192,7 @@ int dfail(vr_dist *d, int code, const std::string &msg)
 int hip_check(vr_dist *d, hipError_t e, const char *what)
 {
     if (e == hipSuccess) return VR_OK;
+    (void)hipGetLastError();  // reported here: not left for the next launch check to find
     return dfail(d, e == hipErrorOutOfMemory ? VR_ENOMEM : VR_EIO,
                  std::string(what) + ": " + hipGetErrorString(e));
 }
@@ -420,6 +421,8 @@ void release(vr_dist *d)
     if (d->fences_registered)
         for (auto &s : S.slots) vr::unregister_stream_fence(d->ctx, s.stream);
     d->fences_registered = false;
+    // the context's kernel-timing events on the slot streams, before the streams go
+    vr::settle_timing(d->ctx);
     if (d->comm && d->owns_comm) rccl().comm_destroy(d->comm);
     free_timing(d);
     for (auto &b : d->bufs) {
@@ -608,8 +611,15 @@ int vr_dist_synchronize(vr_dist *d)
     for (auto &s : d->sched.slots)
         DTRY(hip_check(d, hipStreamSynchronize(s.stream), "hipStreamSynchronize"));
     // rank 0's gathers and assemblies run on the callers' streams: the last one's event
-    if (hipEvent_t e = d->sched.last_gathered())
-        return hip_check(d, hipEventSynchronize(e), "hipEventSynchronize");
+    if (hipEvent_t e = d->sched.last_gathered()) {
+        const hipError_t r = hipEventSynchronize(e);
+        if (r != hipSuccess)
+            return dfail(d, r == hipErrorOutOfMemory ? VR_ENOMEM : VR_EIO,
+                         std::string("hipEventSynchronize (rank ") + std::to_string(d->rank) +
+                             ", frame " + std::to_string(d->sched.frame) + " of " +
+                             std::to_string(d->sched.slots.size()) + " slots): " +
+                             hipGetErrorString(r));
+    }
     return VR_OK;
 }
 

@@ -32,6 +32,9 @@ bool is_multi_device(const vr_ctx *c);
 // unregister after the stream's work is complete, before the event or the stream is destroyed.
 int register_stream_fence(vr_ctx *c, hipStream_t stream, hipEvent_t ev);
 void unregister_stream_fence(vr_ctx *c, hipStream_t stream);
+// Fold the context's pending kernel-timing events into its totals; call after draining, before
+// destroying, the streams they were recorded on (vr_dist slot streams).
+void settle_timing(vr_ctx *c);
 
 // The frame exchange over the members' devices (member 0 = the frame's device):
 // VR_EXCHANGE_RCCL, one communicator per member from ncclCommInitAll (distinct devices), or
