@@ -167,6 +167,29 @@ def test_host_schedule_frames_and_order(world, rb, inflight, nframes):
         assert np.array_equal(img, full), k
 
 
+@pytest.mark.parametrize("rank,inflight", [(0, 1), (0, 3), (1, 1), (1, 3), (2, 8)])
+def test_schedule_edges_per_frame(rank, inflight):
+    """The host cost of a frame is mostly its cross-stream edges (an event record ~2.4 us and a
+    stream wait ~3.7 us against pending events on MI355X, tools/host_cost.cpp): the schedule
+    issues 2 records + 2 waits per frame on rank 0 (the first F frames skip the slot-reuse wait)
+    and 1 + 1 on the other ranks (the first frame has no previous gather to follow)."""
+    lib = _lib()
+    lib.vr_sched_host_edges.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    cb = CB(lambda _u, _op, _slot, _frame: 0)
+    h = lib.vr_sched_host_create(rank, inflight, cb, None)
+    n = 12
+    for _ in range(n):
+        assert lib.vr_sched_host_frame(h) == 0
+    assert lib.vr_sched_host_synchronize(h) == 0
+    rec, wai = C.c_uint64(), C.c_uint64()
+    assert lib.vr_sched_host_edges(h, C.byref(rec), C.byref(wai)) == 0
+    lib.vr_sched_host_destroy(h)
+    if rank == 0:
+        assert (rec.value, wai.value) == (2 * n, n + (n - inflight))
+    else:
+        assert (rec.value, wai.value) == (n, (n - 1) if inflight > 1 else 0)
+
+
 def test_host_schedule_propagates_callback_errors():
     """A failing op (here the render of frame 1) surfaces from synchronize; records and waits
     still run, so the other streams drain instead of deadlocking."""

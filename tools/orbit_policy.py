@@ -1,0 +1,60 @@
+"""Launch-policy check along the orbit path (bench.orbit_cameras), C3 volume and params: for
+every `stride`-th camera, the serial frame time (best of 3, structures built) of the policy's
+own choice and of each forced alternative -- the binary16 field on the 8^3 bricks, the stencil
+gradient on the 8^3 bricks, the oblique copy, the stencil copy (vr_debug.h knobs
+VR_KNOB_GRAD_FIELD / VR_KNOB_ALT_GEOMETRY) -- as JSON lines.  Speed only: every variant renders
+the frame the oracle pins for its gradient mode.
+    python tools/orbit_policy.py [--frames 360] [--stride 4]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+import torch  # noqa: E402
+import vr_amd  # noqa: E402
+
+VARIANTS = {"auto": dict(grad_field=-1, alt_geometry=-1),
+            "field_8cube": dict(grad_field=1, alt_geometry=0),
+            "stencil_8cube": dict(grad_field=0, alt_geometry=0),
+            "oblique_copy": dict(grad_field=0, alt_geometry=1),
+            "stencil_copy": dict(grad_field=0, alt_geometry=4)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=360)
+    ap.add_argument("--stride", type=int, default=4)
+    a = ap.parse_args()
+    cfg = bench.CONFIGS["c3"]
+    rp = bench.setup_pass(cfg, 0)
+    rp.set_memory_budget(2 ** 64 - 1)
+    p = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"])
+    frame = torch.empty((cfg["H"], cfg["W"]), dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    cams = bench.orbit_cameras(a.frames)
+    for i in range(0, a.frames, a.stride):
+        c = cams[i]
+        row = dict(i=i, samples=rp.count_work(c, p, 8)["samples"])
+        for name, knobs in VARIANTS.items():
+            for k, v in knobs.items():
+                rp.set_knob(k, v)
+            best = 1e9
+            for _ in range(4):
+                t0 = time.perf_counter()
+                rp.render_device(c, p, frame.data_ptr(), vr_amd.OUT_RGBA8, 8, 0, 1, s)
+                torch.cuda.synchronize()
+                best = min(best, (time.perf_counter() - t0) * 1e3)
+            k = rp.kernel_name(p)
+            row[name] = round(best, 4)
+            row[name + "_kernel"] = k.split("march_kernel<")[-1].split(",")[0] if "march_kernel<" in k else k
+        print(json.dumps(row), flush=True)
+    rp.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -103,9 +103,11 @@ struct HostExec {
     using Event = HostEvent *;
     vr_sched_op_fn fn = nullptr;
     void *user = nullptr;
+    uint64_t n_records = 0, n_waits = 0;  // cross-stream edges issued (vr_sched_host_edges)
 
     int record(Event e, Stream s)
     {
+        ++n_records;
         uint64_t target;
         {
             std::lock_guard<std::mutex> g(e->m);
@@ -123,6 +125,7 @@ struct HostExec {
     }
     int wait(Stream s, Event e)
     {
+        ++n_waits;
         uint64_t target;
         {
             std::lock_guard<std::mutex> g(e->m);
@@ -223,6 +226,15 @@ int vr_sched_host_frame(vr_sched_host *h)
 
 // Waits for every op enqueued so far; the first failing callback's code, else 0.
 int vr_sched_host_synchronize(vr_sched_host *h) { return h ? h->sync() : -22; }
+
+// Event records and stream waits the schedule has issued so far (each costs host time on HIP).
+int vr_sched_host_edges(const vr_sched_host *h, uint64_t *records, uint64_t *waits)
+{
+    if (!h) return -22;
+    if (records) *records = h->x.n_records;
+    if (waits) *waits = h->x.n_waits;
+    return 0;
+}
 
 void vr_sched_host_destroy(vr_sched_host *h) { delete h; }
 
