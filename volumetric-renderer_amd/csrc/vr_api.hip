@@ -777,6 +777,11 @@ bool budget_allows(const vr_ctx *c, size_t extra, size_t replaced)
 }
 // ---- frame fences and stream-ordered release of derived structures ----
 constexpr size_t kMaxFences = 32;
+#ifndef VR_FENCE_SYSTEM_SCOPE  // experiment builds: 1 = default (system-scope) fence events
+#define VR_FENCE_SYSTEM_SCOPE 0
+#endif
+constexpr unsigned kFenceEventFlags =
+    hipEventDisableTiming | (VR_FENCE_SYSTEM_SCOPE ? 0u : (unsigned)hipEventDisableSystemFence);
 // After this frame's launches on `s`: re-record the stream's fence.  A stream seen for the first
 // time gets a fence; past kMaxFences streams the least recently used one's is recycled once its
 // last frame has finished (a host wait, only with more than 32 frame streams in use).
@@ -789,8 +794,11 @@ int fence_record(vr_ctx *c, hipStream_t s)
     }
     if (!f) {
         if (c->fences.size() < kMaxFences) {
+            // ordering between this device's streams only: no system-scope release (a default
+            // event writes back and invalidates the caches at every record, i.e. every frame;
+            // the timing events avoid it for the same reason)
             hipEvent_t e = nullptr;
-            HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate(fence)");
+            HIP_TRY(c, hipEventCreateWithFlags(&e, kFenceEventFlags), "hipEventCreate(fence)");
             c->fences.push_back(vr_ctx::Fence{s, e, 0, false, 0});
             f = &c->fences.back();
         } else {
