@@ -16,6 +16,7 @@
 #define VR_VR_DEBUG_H
 
 #include "vr.h"
+#include "vr_dist.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -80,6 +81,15 @@ vr_ctx *vr_debug_create_members(const int *devices, int n, uint32_t width, uint3
  * context then aborts the frame exchange and every later frame fails; vr_destroy still returns
  * (no stream waits forever).  member < 0 clears it.  VR_EINVAL on a one-device context. */
 int vr_debug_fail_member(vr_ctx *ctx, int member, uint64_t frame);
+
+/* Host cost of a multi-device context's frames (round 6; tools/host_cost.cpp): with host
+ * profiling on, every member's frame enqueue -- member 0 on the caller's thread, the others on
+ * their frame-worker threads -- adds the host microseconds of its steps as vr_dist_render does
+ * (vr_dist_host_profile, vr_dist.h).  vr_debug_host_profile_member waits until every member has
+ * enqueued the frames issued so far (not for the device), returns member `member`'s sums and
+ * clears them.  VR_EINVAL on a one-device context. */
+int vr_debug_host_profile_enable(vr_ctx *ctx, int enable);
+int vr_debug_host_profile_member(vr_ctx *ctx, int member, vr_dist_host_profile *out);
 
 /* Set / read one knob of `ctx` (a multi-device context sets it on every device).
  * VR_EINVAL for an unknown knob or an out-of-range value. */

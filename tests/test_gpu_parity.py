@@ -559,9 +559,11 @@ def test_f32_gradient_field_equals_stencil_gradient(rp):
 def test_sparse_views_take_the_stencil_gradient(rp):
     """Launch policy (vr_api.hip use_grad_field): a shaded f32 frame reads the difference
     field on dense-row views (the frame-filling r = 1.6 view, 0.6 voxels per pixel here), on
-    axis-aligned side views when the field is binary16, and forms the gradient from the
-    density stencil elsewhere (the reference's default camera, r = 3, 1.2 voxels per pixel
-    here).  All match the oracle (the field frames its binary16 restatement bit for bit)."""
+    axis-aligned views whose ray runs along y or z when the field is binary16 (the top view,
+    image x along the bricks' y), and forms the gradient from the density stencil elsewhere
+    (the reference's default camera, r = 3, 1.2 voxels per pixel here; the side view, whose
+    ray runs along x, reads the oblique copy since round 6).  All match the oracle (the field
+    frames its binary16 restatement bit for bit)."""
     W, H = 192, 120
     rp.framebuffer_size_changed(W, H)
     vol = synth.gaussians_numpy((64, 64, 64), seed=21).astype(np.float32)
@@ -569,17 +571,23 @@ def test_sparse_views_take_the_stencil_gradient(rp):
     tf = synth.tf_band(0.15, 0.9)
     rp.transfer_function_changed(tf)
     p = vr_amd.default_params(shading=1)
-    side = vr_amd.make_camera(radius=1.6, rotate=(360.0, 0.0))  # image x along the bricks' z
-    for camname, field in (("fill", True), ("default", False), ("side", True), ("fill", True)):
-        cam = (side if camname == "side" else synth.camera(camname)).to_vr_camera()
+    extra = {"top": vr_amd.make_camera(radius=1.6, rotate=(360.0, 340.0)),  # ray along z, rows along y
+             "side": vr_amd.make_camera(radius=1.6, rotate=(360.0, 0.0))}  # ray along x
+    for camname, field in (("fill", True), ("default", False), ("top", True), ("side", False),
+                           ("fill", True)):
+        cam = (extra[camname] if camname in extra else synth.camera(camname)).to_vr_camera()
         img = rp.render(cam, p, vr_amd.OUT_RGBA32F)
         name = rp.kernel_name(p)
         gf = "<vr::F32H, true, false, false, true," in name
         assert gf == field, (camname, name)
-        if camname == "side":  # the side view reads the field in binary16 only
+        if camname == "top":  # the top view reads the field in binary16 only
             pe = vr_amd.default_params(shading=1, exact_gradient=1)
             rp.render(cam, pe)
             assert "<float, true, false, false, false," in rp.kernel_name(pe), rp.kernel_name(pe)
+        if camname == "side":  # frames in flight: single-lane kernels, which read the copies
+            p3 = vr_amd.default_params(shading=1, frames_in_flight=3)
+            rp.render(cam, p3)
+            assert "F32Alt" in rp.kernel_name(p3), rp.kernel_name(p3)
         ref, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p)
         check(img, ref, exact=not gf)
         ref16, _ = oracle_render(vol, float(vol.min()), float(vol.max()), tf, cam, W, H, p,

@@ -157,3 +157,39 @@ def test_default_budget_orbit_counts(gpu):
         assert m1["derived_bytes"] <= m1["budget_bytes"]
     finally:
         rp.close()
+
+
+def test_member_host_profile(gpu):
+    """vr_debug_host_profile_member (tools/host_cost.cpp's mask-path rows): every member of a
+    3-member context on device 0 counts every frame it enqueued, across a pipeline rebuild
+    (frames in flight 1 -> 3), with positive host time in its render and its total; a
+    one-device context refuses with VR_EINVAL."""
+    import torch
+    W, H = 96, 80
+    vol = synth.gaussians_numpy((40, 36, 44), seed=64).astype(np.float32)
+    grp = vr_amd.OffscreenPass(W, H, members=(0, 0, 0), exchange=vr_amd.EXCHANGE_COPY)
+    one = vr_amd.OffscreenPass(W, H, device=0)
+    try:
+        grp.volume_dataset_changed(synth.dataset(vol))
+        grp.transfer_function_changed(synth.tf_band(0.15, 0.9))
+        grp.host_profile_enable(True)
+        cam = synth.camera("fill").to_vr_camera()
+        frame = torch.empty((H, W), dtype=torch.int32, device="cuda")
+        n = 0
+        for fif in (1, 3):
+            p = vr_amd.default_params(shading=1, ert_eps=1e-5, frames_in_flight=fif)
+            for _ in range(7):
+                grp.render_device(cam, p, frame.data_ptr(), vr_amd.OUT_RGBA8, 8, 0, 1)
+                n += 1
+        rows = [grp.host_profile_member(m) for m in range(3)]
+        for m, r in enumerate(rows):
+            assert r["frames"] == n, (m, r)
+            assert r["render_us"] > 0 and r["total_us"] >= r["render_us"], (m, r)
+        assert rows[0]["assemble_us"] > 0 and rows[1]["assemble_us"] == 0, rows
+        assert grp.host_profile_member(1)["frames"] == 0  # read clears
+        torch.cuda.synchronize()
+        with pytest.raises(RuntimeError):
+            one.host_profile_enable(True)
+    finally:
+        grp.close()
+        one.close()

@@ -8,13 +8,16 @@
 // Rows: the HIP primitives the frame schedule uses (hipSetDevice, hipEventRecord,
 // hipStreamWaitEvent), one kernel launch through the library (vr_assemble_rows), a bare
 // vr_render_device, ncclGather on a one-rank communicator, and the whole vr_dist_render at 1 and
-// 3 frames in flight (one rank).  The frame is 128x72 over a 256^3 f32 volume with the
+// 3 frames in flight (one rank), and vr_render_device on a multi-device context of 2, 3 and 8
+// members on device 0 (copy exchange; the per-member profile is what each frame-worker thread
+// spent enqueueing its part).  The frame is 128x72 over a 256^3 f32 volume with the
 // reference's startup TF (one opaque texel: every ray ends at its first sample), so the kernels
 // take microseconds.
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
 #include "vr/vr.h"
+#include "vr/vr_debug.h"
 #include "vr/vr_dist.h"
 #include "vr/vr_host.h"
 
@@ -204,6 +207,52 @@ int main(int argc, char **argv)
         vr_dist_destroy(d);
     }
 
+    // multi-device contexts on device 0 (vr_debug_create_members, copy exchange): the caller's
+    // vr_render_device (member 0 on its thread: its render, the wait for every member's shard,
+    // the copies, the assembly) and each member's host profile (the worker's enqueue)
+    std::vector<std::string> members;
+    for (int nm : {2, 3, 8}) {
+        std::vector<int> devs(nm, 0);
+        vr_ctx *g = vr_debug_create_members(devs.data(), nm, W, H, VR_EXCHANGE_COPY);
+        if (!g) die("vr_debug_create_members", -1);
+        if (int rc = vr_generate_volume(g, 0, VR_DTYPE_F32, 256, 256, 256, 2024, &lo, &hi))
+            die("vr_generate_volume (members)", rc);
+        if (int rc = vr_set_transfer_function(g, &tf, 1)) die("vr_set_transfer_function", rc);
+        vr_params p;
+        vr_params_default(&p);
+        p.shading = 1;
+        p.ert_eps = 1e-5f;
+        p.frames_in_flight = 3;
+        vr_debug_host_profile_enable(g, 1);
+        const std::string nm_s = "vr_render_device (" + std::to_string(nm) +
+                                 " members on device 0, copy exchange, frames_in_flight 3)";
+        rows.push_back(measure(nm_s.c_str(), n, [&](int) {
+            if (int rc = vr_render_device(g, &cam, &p, frame, VR_OUT_RGBA8, 8, 0, 1, caller))
+                die("vr_render_device (members)", rc);
+        }, [&] {
+            double ms;
+            uint64_t launches;
+            (void)vr_timing_read(g, &ms, &launches);  // drains the workers and the devices
+        }));
+        std::string row = "{\"members\": " + std::to_string(nm) + ", \"per_member\": [";
+        for (int m = 0; m < nm; ++m) {
+            vr_dist_host_profile hp;
+            if (int rc = vr_debug_host_profile_member(g, m, &hp)) die("vr_debug_host_profile_member", rc);
+            const double f = hp.frames ? (double)hp.frames : 1.0;
+            char buf[400];
+            std::snprintf(buf, sizeof buf,
+                          "%s{\"member\": %d, \"frames\": %llu, \"render_us\": %.2f, "
+                          "\"gather_us\": %.2f, \"assemble_us\": %.2f, \"record_us\": %.2f, "
+                          "\"wait_us\": %.2f, \"total_us\": %.2f}",
+                          m ? ", " : "", m, (unsigned long long)hp.frames, hp.render_us / f,
+                          hp.gather_us / f, hp.assemble_us / f, hp.record_us / f, hp.wait_us / f,
+                          hp.total_us / f);
+            row += buf;
+        }
+        members.push_back(row + "]}");
+        vr_destroy(g);
+    }
+
     std::printf("{\"viewport\": \"%ux%u\", \"volume\": \"256^3 f32\", \"calls\": %d, "
                 "\"sync_every\": %d, \"rows\": [\n", W, H, n, kBatch);
     for (size_t i = 0; i < rows.size(); ++i)
@@ -214,6 +263,9 @@ int main(int argc, char **argv)
     std::printf("], \"dist_render_breakdown_per_frame\": [\n");
     for (size_t i = 0; i < breakdown.size(); ++i)
         std::printf("  %s%s\n", breakdown[i].c_str(), i + 1 < breakdown.size() ? "," : "");
+    std::printf("], \"members_host_profile_per_frame\": [\n");
+    for (size_t i = 0; i < members.size(); ++i)
+        std::printf("  %s%s\n", members[i].c_str(), i + 1 < members.size() ? "," : "");
     std::printf("]}\n");
     vr_destroy(ctx);
     return 0;

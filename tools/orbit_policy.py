@@ -4,7 +4,7 @@ own choice and of each forced alternative -- the binary16 field on the 8^3 brick
 gradient on the 8^3 bricks, the oblique copy, the stencil copy (vr_debug.h knobs
 VR_KNOB_GRAD_FIELD / VR_KNOB_ALT_GEOMETRY) -- as JSON lines.  Speed only: every variant renders
 the frame the oracle pins for its gradient mode.
-    python tools/orbit_policy.py [--frames 360] [--stride 4]"""
+    python tools/orbit_policy.py [--frames 360] [--stride 4] [--shading 0]"""
 import argparse
 import json
 import os
@@ -23,24 +23,42 @@ VARIANTS = {"auto": dict(grad_field=-1, alt_geometry=-1),
             "stencil_8cube": dict(grad_field=0, alt_geometry=0),
             "oblique_copy": dict(grad_field=0, alt_geometry=1),
             "stencil_copy": dict(grad_field=0, alt_geometry=4)}
+# unshaded frames read no gradient: the 8^3 bricks, the oblique copy or the plain copy
+VARIANTS_UNSHADED = {"auto": dict(alt_geometry=-1), "bricks_8cube": dict(alt_geometry=0),
+                     "oblique_copy": dict(alt_geometry=1), "plain_copy": dict(alt_geometry=3)}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=360)
     ap.add_argument("--stride", type=int, default=4)
+    ap.add_argument("--shading", type=int, default=1)
+    ap.add_argument("--path", default="orbit", choices=("orbit", "grid"),
+                    help="grid: yaw {0, 45, 90} x pitch {0 .. 85} x radius {1.6 .. 3.2} degrees")
     a = ap.parse_args()
     cfg = bench.CONFIGS["c3"]
     rp = bench.setup_pass(cfg, 0)
     rp.set_memory_budget(2 ** 64 - 1)
-    p = vr_amd.default_params(shading=cfg["shading"], ert_eps=cfg["ert"])
+    p = vr_amd.default_params(shading=a.shading, ert_eps=cfg["ert"])
+    variants = VARIANTS if a.shading else VARIANTS_UNSHADED
     frame = torch.empty((cfg["H"], cfg["W"]), dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
-    cams = bench.orbit_cameras(a.frames)
-    for i in range(0, a.frames, a.stride):
+    if a.path == "grid":  # Camera::rotate takes mouse deltas at 0.25 degree each
+        grid = [(y, pt, r) for y in (0.0, 45.0, 90.0) for pt in (0.0, 10.0, 20.0, 30.0, 60.0, 75.0, 85.0)
+                for r in (1.6, 2.0, 2.4, 2.8, 3.2)]
+        cams = [vr_amd.make_camera(radius=r, rotate=(4.0 * y, 4.0 * pt)).to_vr_camera() for y, pt, r in grid]
+        tags = [dict(yaw=y, pitch=pt, radius=r) for y, pt, r in grid]
+        idx = range(len(cams))
+    else:
+        cams = bench.orbit_cameras(a.frames)
+        tags = [{} for _ in cams]
+        idx = range(0, a.frames, a.stride)
+    for i in idx:
         c = cams[i]
-        row = dict(i=i, samples=rp.count_work(c, p, 8)["samples"])
-        for name, knobs in VARIANTS.items():
+        st = rp.count_work(c, p, 8)
+        row = dict(i=i, samples=st["samples"], shaded=st["shaded_samples"], view=[round(x, 4) for x in c.view[:12]],
+                   **tags[i])
+        for name, knobs in variants.items():
             for k, v in knobs.items():
                 rp.set_knob(k, v)
             best = 1e9

@@ -47,6 +47,8 @@ struct vr_ctx {
     bool dense_rows = false;
     double pixel_span = 0.0;  // voxels per pixel step at the volume centre (view_dense_rows)
     double axis_align = 1.0;  // largest |component| of the centre ray's unit direction
+    int ray_axis = 2;         // the volume axis of that component (0 x, 1 y, 2 z)
+    double row_align = 1.0;   // |x component| of the unit pixel step along the image x axis
     // f32 volumes: further resident copies in the alternative geometries (kAltFlag for
     // oblique views, the plain and stencil copies for sparse ones), each built lazily on the
     // first frame that wants it after a volume change
@@ -542,12 +544,15 @@ int check_params(vr_ctx *c, const vr_params *p)
 // pixel's ray passes closest to the volume centre, the world step of one pixel along the image
 // x axis.  True when that step runs along the volume's x (|x component| >= 0.9 of it: a
 // wavefront's 16-pixel rows follow the bricks' contiguous rows) and spans at most 0.8 voxels
-// (neighbouring lanes share cache lines).  *span = that step's length in voxels.
+// (neighbouring lanes share cache lines).  *span = that step's length in voxels, *row_align =
+// its unit |x component|; *align = the centre ray's largest unit |component|, *axis = its axis.
 bool view_dense_rows(const double *inv, uint32_t W, uint32_t nx, uint32_t ny, uint32_t nz,
-                     double *span, double *align)
+                     double *span, double *align, int *axis, double *row_align)
 {
     *span = 0.0;
     *align = 1.0;
+    *axis = 2;
+    *row_align = 1.0;
     auto unproject = [&](double x, double z, double out[3]) {
         double h[4];
         for (int r = 0; r < 4; ++r) h[r] = inv[0 * 4 + r] * x + inv[2 * 4 + r] * z + inv[3 * 4 + r];
@@ -567,6 +572,8 @@ bool view_dense_rows(const double *inv, uint32_t W, uint32_t nx, uint32_t ny, ui
     }
     if (!(dd > 0.0)) return false;
     *align = std::fmax(std::fabs(d[0]), std::fmax(std::fabs(d[1]), std::fabs(d[2]))) / std::sqrt(dd);
+    *axis = std::fabs(d[0]) >= std::fabs(d[1]) ? (std::fabs(d[0]) >= std::fabs(d[2]) ? 0 : 2)
+                                               : (std::fabs(d[1]) >= std::fabs(d[2]) ? 1 : 2);
     const double t = -od / dd;
     double n2 = 0.0, v2 = 0.0;
     const double nv[3] = {(double)nx, (double)ny, (double)nz};
@@ -577,7 +584,8 @@ bool view_dense_rows(const double *inv, uint32_t W, uint32_t nx, uint32_t ny, ui
     }
     if (!(n2 > 0.0)) return false;
     *span = std::sqrt(v2);
-    return std::fabs(s[0]) >= 0.9 * std::sqrt(n2) && *span <= 0.8;
+    *row_align = std::fabs(s[0]) / std::sqrt(n2);
+    return *row_align >= 0.9 && *span <= 0.8;
 }
 
 // Shaded f32 frames read the difference field only on dense-row views (view_dense_rows:
@@ -594,13 +602,21 @@ bool view_dense_rows(const double *inv, uint32_t W, uint32_t nx, uint32_t ny, ui
 // stencil and their alternative copies.  C3, 3 frames in flight, ms per frame, two rounds
 // (profiles/r03/field_views/): side 0.566 / 0.563 -> 0.541 / 0.542; diagonal 0.651 -> 0.80 and
 // default camera 0.244 -> 0.307 with the field, so those stay.
+// Round 6, measured over a grid of views and along the orbit (yaw x pitch x radius, every
+// variant forced; profiles/r06/policy/): rays along the volume's x lose with the field (1.23-
+// 1.38x the oblique copy's time at 0.7-0.8 voxels per pixel, even at 0.55), so axis-aligned
+// views read it only when the ray runs along y or z; and rays along z keep it on sparse views
+// whose image rows follow the bricks' rows (row_align >= kRowsAlign: the stencil copy there
+// takes 1.11-1.40x the field's time, while rays along y keep the stencil copy, want_alt).
 // Knob VR_KNOB_GRAD_FIELD 0 / 1: the stencil / the field for every view (A/B, tests).
-constexpr double kAltAlign = 0.9, kAltSpan = 0.8;
+constexpr double kAltAlign = 0.9, kAltSpan = 0.8, kRowsAlign = 0.97;
 bool use_grad_field(const vr_ctx *c, bool half)
 {
     if (c->storage != ST_F32) return false;
     if (c->knobs.grad_field >= 0) return c->knobs.grad_field == 1;
-    return c->dense_rows || (half && c->axis_align >= kAltAlign && c->pixel_span <= kAltSpan);
+    if (c->dense_rows) return true;
+    if (!half || c->axis_align < kAltAlign || c->ray_axis == 0) return false;
+    return c->pixel_span <= kAltSpan || (c->ray_axis == 2 && c->row_align >= kRowsAlign);
 }
 
 // Pipelined march (two samples of a ray in flight, vr_kernels.hip PIPE): for launches of
@@ -720,7 +736,7 @@ int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
     P.slab_default = c->smin[0] == 0.0f && c->smin[1] == 0.0f && c->smin[2] == 0.0f &&
                      c->smax[0] == 1.0f && c->smax[1] == 1.0f && c->smax[2] == 1.0f;
     c->dense_rows = view_dense_rows(P.inv, c->width, c->nx, c->ny, c->nz, &c->pixel_span,
-                                    &c->axis_align);
+                                    &c->axis_align, &c->ray_axis, &c->row_align);
     P.pipelined = use_pipeline(p->shading != 0, P.tiles_x * P.tiles_y, c);
     return VR_OK;
 }
@@ -1049,14 +1065,27 @@ int ensure_derived(vr_ctx *c, const vr_params *p, MarchParams &P, hipStream_t s,
 // measured 1-2% slower than 15^3.  Shaded, they take the stencil copy (kStencilF32Flag: plain
 // voxels with the gradient's apron, vr_internal.h): 0.260 / 0.261 -> 0.232 / 0.230
 // (profiles/r03/stencil2/ .. stencil4/); on the diagonal it loses to the oblique copy.
+// Round 6 (profiles/r06/policy/: a grid of views and the orbit, every variant forced): the plain
+// and stencil copies pay only when the image rows follow the bricks' rows (row_align >=
+// kRowsAlign), whatever the ray's tilt -- elsewhere they took 1.5-2.1x the oblique copy's time
+// (the orbit's slowest frames, side views at r 2.3-2.5) -- and the oblique copy beats the 8^3
+// bricks on every view whose ray runs along x.  So, off the dense-row views: sparse views along
+// the rows take the plain / stencil copy; axis-aligned views with the ray along y or z and at
+// most kAltSpan voxels per pixel keep the 8^3 bricks; every other view reads the oblique copy.
 int want_alt(const vr_ctx *c, const vr_params *p, const MarchParams &P)
 {
     if (c->layout != ST_F32 || p->skip_empty || P.pair || P.grad) return c->layout;
     int which = 0;
     if (c->knobs.alt >= 0)
         which = c->knobs.alt;
-    else if (!c->dense_rows)
-        which = c->axis_align < kAltAlign ? 1 : (c->pixel_span > kAltSpan ? (p->shading ? 4 : 3) : 0);
+    else if (!c->dense_rows) {
+        if (c->pixel_span > kAltSpan && c->row_align >= kRowsAlign)
+            which = p->shading ? 4 : 3;
+        else if (c->axis_align >= kAltAlign && c->ray_axis != 0 && c->pixel_span <= kAltSpan)
+            which = 0;
+        else
+            which = 1;
+    }
     switch (which) {
         case 1: return ST_F32 | kAltFlag;
         case 3: return ST_F32 | kPlainF32Flag;
@@ -2325,6 +2354,23 @@ int vr_debug_timing_member(vr_ctx *c, int member, vr_member_timing *out)
     out->render_ms = ms[0];
     out->gather_ms = ms[1];
     out->assemble_ms = ms[2];
+    return VR_OK;
+}
+
+int vr_debug_host_profile_enable(vr_ctx *c, int enable)
+{
+    if (!c) return fail(nullptr, VR_EINVAL, "ctx is NULL");
+    if (!is_group(c)) return fail(c, VR_EINVAL, "not a multi-device context");
+    vr::group_host_profile_enable(c->group, enable != 0);
+    return VR_OK;
+}
+
+int vr_debug_host_profile_member(vr_ctx *c, int member, vr_dist_host_profile *out)
+{
+    if (!c || !out) return fail(c, VR_EINVAL, "NULL argument");
+    if (!is_group(c)) return fail(c, VR_EINVAL, "not a multi-device context");
+    std::string m;
+    if (int rc = vr::group_host_profile_member(c->group, member, out, &m)) return fail(c, rc, m);
     return VR_OK;
 }
 

@@ -676,6 +676,8 @@ struct Group {
     int frames = 0, out_format = -1;
     uint32_t share_w0 = 1, share_w = 1;  // the row share the pipelines were built for
     bool timing = false;                 // per-member render / gather / assembly spans
+    bool hprof = false;                  // per-member host profile (vr_debug_host_profile_*)
+    std::vector<vr_dist_host_profile> hp;  // per member: host sums of pipelines freed since
     // per member: spans read from the pipelines so far (render, gather, assemble ms; frames)
     struct Spans {
         double ms[3] = {0.0, 0.0, 0.0};
@@ -728,10 +730,28 @@ void fold_spans(Group *g)
     }
 }
 
+void fold_host_profile(Group *g)
+{
+    g->hp.resize(g->members.size());
+    for (size_t m = 0; m < g->dists.size(); ++m) {
+        vr_dist_host_profile &a = g->hp[m];
+        const vr_dist_host_profile &b = g->dists[m]->hp;
+        a.frames += b.frames;
+        a.render_us += b.render_us;
+        a.gather_us += b.gather_us;
+        a.assemble_us += b.assemble_us;
+        a.record_us += b.record_us;
+        a.wait_us += b.wait_us;
+        a.total_us += b.total_us;
+        g->dists[m]->hp = vr_dist_host_profile{};
+    }
+}
+
 void free_pipelines(Group *g)
 {
     g->workers.reset();  // drains the queues and joins the threads
     fold_spans(g);
+    fold_host_profile(g);
     for (vr_dist *d : g->dists) {
         if (!d) continue;
         release(d);
@@ -772,6 +792,7 @@ int ensure_pipelines(Group *g, int frames, int out_format, std::string *err)
             return VR_EIO;
         }
         d->timing = g->timing;
+        d->hprof = g->hprof;
         g->dists.push_back(d);
     }
     if (g->xch) g->xch->peers = g->dists;
@@ -920,6 +941,27 @@ int group_fail_member(Group *g, int member, uint64_t frame, std::string *err)
     // frames count from the next pipeline build; the current pipelines' counter otherwise
     g->fail_frame.store(frame, std::memory_order_relaxed);
     g->fail_member.store(member, std::memory_order_release);
+    return VR_OK;
+}
+
+void group_host_profile_enable(Group *g, bool on)
+{
+    std::string ignored;
+    group_drain(g, &ignored);  // the workers write the sums while they enqueue
+    g->hprof = on;
+    for (vr_dist *d : g->dists) d->hprof = on;
+}
+
+int group_host_profile_member(Group *g, int m, vr_dist_host_profile *out, std::string *err)
+{
+    if (m < 0 || m >= (int)g->members.size()) {
+        *err = "no such member";
+        return VR_EINVAL;
+    }
+    if (int rc = group_drain(g, err)) return rc;
+    fold_host_profile(g);
+    *out = g->hp[(size_t)m];
+    g->hp[(size_t)m] = vr_dist_host_profile{};
     return VR_OK;
 }
 

@@ -14,6 +14,7 @@
 
 #include "../../include/vr/vr.h"
 #include "../../include/vr/vr_debug.h"
+#include "../../include/vr/vr_dist.h"
 
 namespace vr {
 
@@ -58,6 +59,11 @@ int group_render(Group *g, const vr_camera *cam, const vr_params *p, void *out_d
 // Per-member spans (HIP events on the member's own streams; vr_debug_timing_member): render of
 // its row blocks, its ncclGather, and (member 0) the assembly, summed since the last reset.
 void group_timing_enable(Group *g, bool on);
+// Per-member host profile (vr_dist_host_profile of each member's pipeline, summed across
+// pipeline rebuilds): read waits until every member has enqueued the frames issued so far, then
+// returns member m's sums and clears them.
+void group_host_profile_enable(Group *g, bool on);
+int group_host_profile_member(Group *g, int m, vr_dist_host_profile *out, std::string *err);
 int group_timing_member(Group *g, int member, double ms[3], uint64_t *frames, std::string *err);
 int group_timing_reset(Group *g, std::string *err);
 

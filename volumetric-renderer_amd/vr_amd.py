@@ -119,7 +119,8 @@ DIST_SYMBOLS = [
 ]
 DIST_ID_BYTES = 128  # include/vr/vr_dist.h VR_DIST_ID_BYTES
 DEBUG_SYMBOLS = ["vr_debug_set_knob", "vr_debug_get_knob", "vr_debug_timing_member",
-                 "vr_debug_create_members", "vr_debug_fail_member"]
+                 "vr_debug_create_members", "vr_debug_fail_member",
+                 "vr_debug_host_profile_enable", "vr_debug_host_profile_member"]
 # include/vr/vr_debug.h enum vr_exchange (multi-device contexts: how shards reach member 0)
 EXCHANGE_RCCL, EXCHANGE_COPY = 0, 1
 # include/vr/vr_debug.h enum vr_knob (launch-policy overrides: speed only, never results)
@@ -196,6 +197,8 @@ def lib() -> C.CDLL:
         "vr_release_external_memory": (C.c_int, [vp, vp]),
         "vr_debug_set_knob": (i32, [vp, i32, i32]),
         "vr_debug_timing_member": (i32, [vp, i32, C.POINTER(vr_member_timing)]),
+        "vr_debug_host_profile_enable": (i32, [vp, i32]),
+        "vr_debug_host_profile_member": (i32, [vp, i32, C.POINTER(vr_dist_host_profile)]),
         "vr_set_row_share": (i32, [vp, u32, u32]),
         "vr_get_row_share": (i32, [vp, C.POINTER(u32), C.POINTER(u32)]),
         "vr_shard_rows_ctx": (u32, [vp, u32, u32, u32]),
@@ -600,6 +603,18 @@ class OffscreenPass:
         self._check(lib().vr_prepare(self._ctx, C.byref(cam), C.byref(params)), "prepare")
 
     # -- include/vr/vr_debug.h: launch-policy overrides for tests (speed only, never results) --
+    def host_profile_enable(self, on: bool = True):
+        """vr_debug_host_profile_enable (multi-device contexts): per-member host enqueue time."""
+        self._check(lib().vr_debug_host_profile_enable(self._ctx, int(bool(on))), "host_profile_enable")
+
+    def host_profile_member(self, member: int) -> dict:
+        """vr_debug_host_profile_member: member's host microseconds per frame, by step."""
+        h = vr_dist_host_profile()
+        self._check(lib().vr_debug_host_profile_member(self._ctx, member, C.byref(h)),
+                    "host_profile_member")
+        n = max(int(h.frames), 1)
+        return dict(frames=int(h.frames), **{k: getattr(h, k) / n for k, _ in vr_dist_host_profile._fields_[1:]})
+
     def set_knob(self, name: str, value: int):
         self._check(lib().vr_debug_set_knob(self._ctx, KNOBS[name], int(value)), f"set_knob({name})")
 
