@@ -193,3 +193,37 @@ def test_member_host_profile(gpu):
     finally:
         grp.close()
         one.close()
+
+
+def test_layout_policy_by_ray_axis_and_row_alignment(gpu):
+    """vr_api.hip want_alt / use_grad_field (round 6, profiles/r06/policy/): on sparse views
+    (> 0.8 voxels per pixel; r = 3 here) the stencil / plain copy only when the image rows follow
+    the bricks' rows, the oblique copy when they cross them (the orbit's slowest frames before);
+    the binary16 field for sparse row-aligned views whose ray runs along z; the oblique copy for
+    rays along x.  Every choice renders the 8^3 bricks' frame byte for byte (exact gradient)."""
+    W, H = 192, 120
+    rp = _pass(W, H, seed=65)
+    try:
+        cams = {"default": vr_amd.make_camera(radius=3.0),                       # ray y, rows along x
+                "top_far": vr_amd.make_camera(radius=3.0, rotate=(0.0, 340.0)),  # ray z, rows along x
+                "side_far": vr_amd.make_camera(radius=3.0, rotate=(360.0, 80.0)),  # ray x, rows along y
+                "side_near": vr_amd.make_camera(radius=1.6, rotate=(360.0, 0.0))}  # ray x, dense
+        want = {  # (shading, exact_gradient) -> tag per view; None: the 8^3 bricks, no field
+            (1, 0): {"default": "F32S", "top_far": "F32H", "side_far": "F32Alt", "side_near": "F32Alt"},
+            (1, 1): {"default": "F32S", "top_far": "F32S", "side_far": "F32Alt", "side_near": "F32Alt"},
+            (0, 0): {"default": "F32P", "top_far": "F32P", "side_far": "F32Alt", "side_near": "F32Alt"}}
+        for (shading, exact), tags in want.items():
+            p = vr_amd.default_params(shading=shading, ert_eps=1e-5, exact_gradient=exact,
+                                      frames_in_flight=3)
+            for name, oc in cams.items():
+                cam = oc.to_vr_camera()
+                img = rp.render(cam, p, vr_amd.OUT_RGBA32F)
+                tag = tags[name]
+                kname = rp.kernel_name(p)
+                assert tag in kname, (shading, exact, name, kname)
+                if tag != "F32H":  # the same frame as the 8^3 bricks with the stencil gradient
+                    with rp.knobs(grad_field=0, alt_geometry=0):
+                        ref = rp.render(cam, p, vr_amd.OUT_RGBA32F)
+                    assert _bits_equal(img, ref) == 0, (shading, exact, name)
+    finally:
+        rp.close()
