@@ -22,7 +22,8 @@ VARIANTS = {"auto": dict(grad_field=-1, alt_geometry=-1),
             "field_8cube": dict(grad_field=1, alt_geometry=0),
             "stencil_8cube": dict(grad_field=0, alt_geometry=0),
             "oblique_copy": dict(grad_field=0, alt_geometry=1),
-            "stencil_copy": dict(grad_field=0, alt_geometry=4)}
+            "stencil_copy": dict(grad_field=0, alt_geometry=4),
+            "pair_lanes": dict(pair=1)}  # 2-4 lanes per ray on the 8^3 bricks (serial frames)
 # unshaded frames read no gradient: the 8^3 bricks, the oblique copy or the plain copy
 VARIANTS_UNSHADED = {"auto": dict(alt_geometry=-1), "bricks_8cube": dict(alt_geometry=0),
                      "oblique_copy": dict(alt_geometry=1), "plain_copy": dict(alt_geometry=3)}
@@ -59,8 +60,8 @@ def main():
         row = dict(i=i, samples=st["samples"], shaded=st["shaded_samples"], view=[round(x, 4) for x in c.view[:12]],
                    **tags[i])
         for name, knobs in variants.items():
-            for k, v in knobs.items():
-                rp.set_knob(k, v)
+            for k in ("grad_field", "alt_geometry", "pair"):
+                rp.set_knob(k, knobs.get(k, vr_amd.KNOB_AUTO[k]))
             best = 1e9
             for _ in range(4):
                 t0 = time.perf_counter()

@@ -29,6 +29,8 @@ VIEWS = {
     "diag": dict(radius=2.0, rotate=(180.0, 140.0)),
     "diag2": dict(radius=1.8, rotate=(120.0, 60.0)),
     "default": dict(radius=3.0, rotate=None),
+    "far_oblique": dict(radius=3.2, rotate=(180.0, 80.0)),  # yaw 45, pitch 20 (round 6 grid)
+    "far_side": dict(radius=2.4, rotate=(360.0, 80.0)),  # yaw 90, pitch 20: ray along x
 }
 
 

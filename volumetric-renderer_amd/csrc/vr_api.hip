@@ -649,6 +649,7 @@ bool use_pipeline(bool shading, uint32_t tiles, const vr_ctx *c)
 // stay faster single-lane (tools/shard_sweep.py, profiles/r01/multi_gpu/).  Serial frames
 // only (vr_params.frames_in_flight <= 1).  Not for
 // skip-empty frames or TFs beyond the LDS copy.  Knob VR_KNOB_PAIR 0/1 overrides (A/B).
+int want_alt(const vr_ctx *c, const vr_params *p, const MarchParams &P);
 bool use_pair(const vr_ctx *c, const MarchParams &P, const vr_params *p)
 {
     if (p->skip_empty || P.tf_n > 256) return false;
@@ -657,7 +658,18 @@ bool use_pair(const vr_ctx *c, const MarchParams &P, const vr_params *p)
     // per sample decides and the single-lane kernel wins (N = 8 C3 share with 3 frames in
     // flight: 0.070 against 0.107 ms per frame, tools/inflight_sweep.py)
     if (p->frames_in_flight >= 2) return false;
-    return p->shading && P.tiles_x * P.tiles_y * (kThreadsPerTile / 64) < kPairMaxWaves;
+    if (!p->shading) return false;
+    if (P.tiles_x * P.tiles_y * (kThreadsPerTile / 64) < kPairMaxWaves) return true;
+    // Full serial frames of sparse views that would read the oblique copy: their rays are few
+    // and slow (10-23 ps per sample against 3 on the frame-filling view), so halving each
+    // ray's serial chain pays more than the copy's geometry -- 0.64-0.96x the time on such
+    // views of the orbit and the round-6 grid, 6% of the orbit's serial time, its slowest
+    // frames most; not on rays along z, whose sparse views lost (1.10-1.32x), nor on the field
+    // and stencil-copy views (1.06-1.28x) (profiles/r06/policy/pair/).
+    if (c->knobs.alt >= 0 || c->layout != ST_F32 || c->dense_rows || c->pixel_span <= kAltSpan ||
+        (c->ray_axis == 2 && c->axis_align >= kAltAlign))
+        return false;
+    return want_alt(c, p, P) == (ST_F32 | kAltFlag);
 }
 
 int build_params(vr_ctx *c, const vr_camera *cam, const vr_params *p, void *out,
