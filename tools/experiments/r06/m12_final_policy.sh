@@ -3,7 +3,7 @@
 # machine-code key still matches, so no PMC passes): smoke, the headline alone, its rocprofv3
 # kernel-trace summary, and the driver's bench command with variants and the CPU baseline.
 set -o pipefail
-O=$GRAFT_REPO_ROOT/gpurun_out/r06_policy
+O=$GRAFT_REPO_ROOT/gpurun_out/${1:-r06_policy}
 mkdir -p $O
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT

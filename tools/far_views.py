@@ -1,6 +1,7 @@
 """Where the sparse (far) views lose time, C3 volume and params: for a few views of the round-6
 grid, the serial frame (best of 4, host-timed to the device's end), the same with lane groups
-forced (VR_KNOB_PAIR 1: 2-4 lanes per ray), and the wall-clock period with 3 frames in flight,
+forced on and off (VR_KNOB_PAIR 1 / 0: 2-4 lanes per ray or one), and the wall-clock period
+with 3 frames in flight (single lane, the policy, and lane groups forced),
 plus the rays that hit the volume and the samples per such ray.  JSON lines.
     python tools/far_views.py"""
 import json
@@ -42,23 +43,30 @@ def main():
                 rp.render_device(cam, params, frames[0].data_ptr(), vr_amd.OUT_RGBA8, 8, 0, 1, s0)
                 torch.cuda.synchronize()
                 best = min(best, (time.perf_counter() - t0) * 1e3)
-            return round(best, 4), rp.kernel_name(params).split("(")[0][-60:]
+            return round(best, 4)
 
-        row["serial_ms"], row["serial_kernel"] = serial(p1)
+        row["serial_ms"] = serial(p1)
         with rp.knobs(pair=1):
-            row["serial_pair_ms"], row["pair_kernel"] = serial(p1)
-        for i in range(6):
-            rp.render_device(cam, p3, frames[i % 3].data_ptr(), vr_amd.OUT_RGBA8, 8, 0, 1,
-                             streams[i % 3].cuda_stream)
-        torch.cuda.synchronize()
-        n = 30
-        t0 = time.perf_counter()
-        for i in range(n):
-            rp.render_device(cam, p3, frames[i % 3].data_ptr(), vr_amd.OUT_RGBA8, 8, 0, 1,
-                             streams[i % 3].cuda_stream)
-        torch.cuda.synchronize()
-        row["inflight3_ms"] = round((time.perf_counter() - t0) / n * 1e3, 4)
-        row["inflight3_kernel"] = rp.kernel_name(p3).split("(")[0][-60:]
+            row["serial_pair_ms"] = serial(p1)
+        with rp.knobs(pair=0):
+            row["serial_single_lane_ms"] = serial(p1)
+
+        def inflight():
+            for i in range(6):
+                rp.render_device(cam, p3, frames[i % 3].data_ptr(), vr_amd.OUT_RGBA8, 8, 0, 1,
+                                 streams[i % 3].cuda_stream)
+            torch.cuda.synchronize()
+            n = 30
+            t0 = time.perf_counter()
+            for i in range(n):
+                rp.render_device(cam, p3, frames[i % 3].data_ptr(), vr_amd.OUT_RGBA8, 8, 0, 1,
+                                 streams[i % 3].cuda_stream)
+            torch.cuda.synchronize()
+            return round((time.perf_counter() - t0) / n * 1e3, 4)
+
+        row["inflight3_ms"] = inflight()
+        with rp.knobs(pair=1):
+            row["inflight3_pair_ms"] = inflight()
         print(json.dumps(row), flush=True)
     rp.close()
 
