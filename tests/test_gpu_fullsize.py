@@ -104,7 +104,9 @@ def test_c1_64_f32_256_whole_frame(gpu):
 
 def test_c3_512_f32_1080p_whole_frame(gpu):
     """C3: 512^3 f32, 1920x1080, camera r=1.6 and the reference's default camera, Phong + ERT
-    and reference semantics (no shading, no ERT)."""
+    and reference semantics (no shading, no ERT); and two sparse views the round-6 launch policy
+    sends elsewhere: an oblique one at r = 3.2 (serial shaded frames: lane groups on the 8^3
+    bricks) and a side view at r = 2.4 whose ray runs along x (the oblique copy)."""
     W, H = 1920, 1080
     rp = vr_amd.OffscreenPass(W, H)
     lo, hi = rp.generate_volume((512, 512, 512), np.float32, seed=2024)
@@ -120,6 +122,14 @@ def test_c3_512_f32_1080p_whole_frame(gpu):
             frame_parity(rp, vol, lo, hi, tf, cam, W, H, p,
                          f"C3 {camname} shading={p.shading} ert={p.ert_eps:g} "
                          f"exact_gradient={p.exact_gradient}")
+    for camname, oc in (("far_oblique", vr_amd.make_camera(radius=3.2, rotate=(180.0, 80.0))),
+                        ("far_side", vr_amd.make_camera(radius=2.4, rotate=(360.0, 80.0)))):
+        cam = oc.to_vr_camera()
+        for p in (vr_amd.default_params(shading=1, ert_eps=1e-5),
+                  vr_amd.default_params(shading=1, ert_eps=1e-5, frames_in_flight=3),
+                  vr_amd.default_params()):
+            frame_parity(rp, vol, lo, hi, tf, cam, W, H, p,
+                         f"C3 {camname} shading={p.shading} in_flight={p.frames_in_flight}")
     rp.close()
 
 
