@@ -291,7 +291,8 @@ int vr_release_external_memory(vr_ctx *ctx, vr_external_memory *mem);
  * Beside the bricked volume the library may build, per device, structures that speed particular
  * views up without changing a pixel: the difference field of shaded f32 dense-row views (3x the
  * bricks; binary16 unless vr_params.exact_gradient), a 7x15x8-brick copy for oblique f32 views,
- * a plain copy for unshaded sparse ones, a stencil copy for shaded sparse ones, and the
+ * a plain copy for unshaded sparse ones and a stencil copy for shaded sparse ones (sparse views
+ * whose image rows follow the bricks' rows; DESIGN.md section 4.1 has the policy), and the
  * skip-empty classification.  Each is built on the first frame that wants it (1-5 ms for 512^3,
  * inside that frame) unless vr_prepare built it first.
  * vr_set_memory_budget caps their total bytes on each device (the bricks never count): a

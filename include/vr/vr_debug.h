@@ -35,9 +35,10 @@ enum vr_knob {
     VR_KNOB_NARROW = 8,     /* 1 (default): 32/64-bit uploads whose voxels are all integers
                                that fit 8/16 bits are stored in that type (same frames); 0:
                                keep f32 storage (next upload)                              */
-    VR_KNOB_ALT_GEOMETRY = 9 /* f32 volumes: -1 auto (oblique views read a 7x15x8-cell-brick
-                               copy; sparse views the stencil copy when shaded, a plain
-                               one-voxel-per-element 15^3 one when not), 0 never, 1 the
+    VR_KNOB_ALT_GEOMETRY = 9 /* f32 volumes: -1 auto (oblique views and rays along x read a
+                               7x15x8-cell-brick copy; sparse views along the bricks' rows the
+                               stencil copy when shaded, a plain one-voxel-per-element 15^3
+                               one when not), 0 never, 1 the
                                oblique copy, 3 the plain copy, 4 the stencil copy (29^3-cell
                                plain bricks with a 1-below / 2-above apron), whenever the
                                launch allows it (2, the retired z-pair sparse copy: EINVAL) */
