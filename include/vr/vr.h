@@ -358,7 +358,9 @@ int vr_timing_read(vr_ctx *ctx, double *total_ms, uint64_t *launches);
 int vr_timing_reset(vr_ctx *ctx);
 
 /* Name of the ray-march kernel variant vr_render_device launches for the current volume
- * and params (for matching rocprof rows); returns a static string. */
+ * and params (for matching rocprof rows), full frame, single-lane: a serial launch that runs
+ * lane groups (march_pair_kernel: small row shares, serial frames of sparse oblique views)
+ * is named by the march_kernel variant it stands in for; returns a static string. */
 const char *vr_kernel_name(const vr_ctx *ctx, const vr_params *p);
 
 #ifdef __cplusplus
