@@ -1119,8 +1119,8 @@ size_t alt_bytes_for(const vr_ctx *c, int lay)
            brick_elems(lay) * element_size(lay);
 }
 
-// The copy in layout `lay` (kAltFlag or kWideFlag), (re)built on `s` from the 8^3 bricks when
-// stale (unbrick to a linear temporary, brick again; stream-ordered allocations).  *ready =
+// The copy in layout `lay` (kAltFlag, kPlainF32Flag or kStencilF32Flag), (re)built on `s` from
+// the 8^3 bricks when stale (one pass, launch_rebrick_f32; stream-ordered allocation).  *ready =
 // false when it cannot exist (memory short beside a 2 GiB reserve): the launch then stays on
 // the 8^3 copy (same frames).
 int ensure_alt(vr_ctx *c, int lay, hipStream_t s, bool *ready)
@@ -1134,7 +1134,6 @@ int ensure_alt(vr_ctx *c, int lay, hipStream_t s, bool *ready)
         return VR_OK;
     }
     if (a.failed) return VR_OK;
-    const size_t lin = (size_t)c->nx * c->ny * c->nz * sizeof(float);
     if (!a.bricks || a.bytes != bytes) {
         const size_t had = a.bricks ? a.bytes + kBrickSlackBytes : 0;
         // over the budget: the least recently read other copies, then the field (read only by
@@ -1149,7 +1148,7 @@ int ensure_alt(vr_ctx *c, int lay, hipStream_t s, bool *ready)
         a.bytes = 0;
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess ||
-            free_b < bytes + kBrickSlackBytes + lin + (2ull << 30) ||
+            free_b < bytes + kBrickSlackBytes + (2ull << 30) ||
             hipMallocAsync(&a.bricks, bytes + kBrickSlackBytes, s) != hipSuccess) {
             (void)hipGetLastError();
             a.bricks = nullptr;
@@ -1158,14 +1157,9 @@ int ensure_alt(vr_ctx *c, int lay, hipStream_t s, bool *ready)
         }
         a.bytes = bytes;
     }
-    void *tmp = nullptr;
-    HIP_TRY(c, hipMallocAsync(&tmp, lin, s), "hipMallocAsync(alt staging)");
-    hipError_t e = launch_unbrick(c->layout, c->bricks, tmp, c->nx, c->ny, 0, c->nz, s);
-    if (e == hipSuccess)
-        e = launch_brick_from_linear(VR_DTYPE_F32, tmp, a.bricks, c->nx, c->ny, c->nz, lay, s);
-    const hipError_t f = hipFreeAsync(tmp, s);
+    const hipError_t e = launch_rebrick_f32(static_cast<const float *>(c->bricks), a.bricks, c->nx,
+                                            c->ny, c->nz, lay, s);
     if (e != hipSuccess) return hip_fail(c, e, "alt geometry copy");
-    if (f != hipSuccess) return hip_fail(c, f, "hipFreeAsync(alt staging)");
     a.valid = true;
     a.used = c->frame_no;
     ++c->n_builds;

@@ -436,6 +436,10 @@ constexpr size_t kGradElemBytes = 24;
 // clamped to +-65504 (NaN kept) before rounding to nearest even
 hipError_t launch_grad_field(const float *bricks, float *grad, uint32_t nx, uint32_t ny,
                              uint32_t nz, bool half, int scale_log2, hipStream_t stream);
+// The f32 copy in layout `storage` (kAltFlag / kPlainF32Flag / kStencilF32Flag) straight from the
+// 8^3 z-pair bricks: the same bytes as launch_unbrick + launch_brick_from_linear.
+hipError_t launch_rebrick_f32(const float *src_bricks, void *dst, uint32_t nx, uint32_t ny,
+                              uint32_t nz, int storage, hipStream_t stream);
 // The binary16 field's scale: the largest k in [-120, 120] with B 2^k <= 65504, where
 // B = max(vmax, 0) - min(vmin, 0) bounds every central difference of voxels in [vmin, vmax]
 // (and of the zero border); 0 when B is 0 or not finite.  oracle/oracle.c restates it.

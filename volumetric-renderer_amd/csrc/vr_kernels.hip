@@ -1823,6 +1823,44 @@ __device__ __forceinline__ float padded_voxel(const float *__restrict__ bricks, 
     return bricks[kF32VoxelsPerElement * cell_offset<float>(px, py, pz, nbx, nby)];
 }
 
+// The f32 alternative-geometry copies straight from the 8^3 z-pair bricks (round 6; before: an
+// unbrick to a linear f32 temporary, then brick_kernel from it): one thread per stored element
+// of the copy, its voxels read as padded_voxel (0 outside the volume) -- the same values
+// brick_kernel stores, so the same bytes, without the volume-sized temporary and one pass less.
+template <typename DstT>
+__global__ __launch_bounds__(256) void rebrick_f32_kernel(const float *__restrict__ src,
+                                                          float *__restrict__ dst, uint32_t nx,
+                                                          uint32_t ny, uint32_t nz, uint32_t snbx,
+                                                          uint32_t snby, uint32_t snbz, uint32_t nbx,
+                                                          uint32_t nby, size_t nbricks)
+{
+    using G = GeomOf<DstT>;
+    for (size_t bidx = blockIdx.x; bidx < nbricks; bidx += gridDim.x) {
+        uint32_t bx, by, bz;
+        brick_coords((uint32_t)bidx, nbx, nby, bx, by, bz);
+        for (uint32_t l = threadIdx.x; l < (uint32_t)G::Elems; l += blockDim.x) {
+            const size_t g = bidx * G::Elems + l;
+            const uint32_t lx = l % G::EX, lyz = l / G::EX, lyy = lyz % G::EY, lz = lyz / G::EY;
+            // padded coordinates of the element (brick_kernel's logical ones + kPad)
+            const int x = (int)(bx * G::BX + lx) - G::Lo, y = (int)(by * G::BY + lyy) - G::Lo,
+                      z = (int)(bz * G::BZ + lz) - G::Lo;
+            if constexpr (kPlainF32<DstT>) {
+                dst[g] = padded_voxel(src, x, y, z, nx, ny, nz, snbx, snby);
+            } else if (kF32VoxelsPerElement == 2 && x >= 0 && y >= 0 && z >= 0 &&
+                       x < (int)(snbx * GeomWide::BX) && y < (int)(snby * GeomWide::BY) &&
+                       z < (int)(snbz * GeomWide::BZ)) {
+                // a source z-pair element holds {v(z), v(z + 1)} with the border stored as 0
+                reinterpret_cast<float2 *>(dst)[g] =
+                    reinterpret_cast<const float2 *>(src)[cell_offset<float>(x, y, z, snbx, snby)];
+            } else {
+                reinterpret_cast<float2 *>(dst)[g] =
+                    make_float2(padded_voxel(src, x, y, z, nx, ny, nz, snbx, snby),
+                                padded_voxel(src, x, y, z + 1, nx, ny, nz, snbx, snby));
+            }
+        }
+    }
+}
+
 // binary16 of d * 2^k (scale = 2^k): clamped to +-65504 first (NaN passes), rounded to nearest
 // even (v_cvt_f16_f32; f16 denormals kept).  The oracle's round_f16 restates it.
 __device__ __forceinline__ _Float16 field_half(float d, float scale)
@@ -2371,6 +2409,24 @@ hipError_t launch_grad_field(const float *bricks, float *grad, uint32_t nx, uint
     else
         hipLaunchKernelGGL(grad_field_kernel<false>, dim3(grid_bricks(total)), dim3(256), 0, s,
                            bricks, grad, nx, ny, nz, nbx, nby, total, scale);
+    return hipGetLastError();
+}
+
+hipError_t launch_rebrick_f32(const float *src_bricks, void *dst, uint32_t nx, uint32_t ny,
+                              uint32_t nz, int storage, hipStream_t s)
+{
+    const uint32_t snbx = bricks_for(nx, 0, ST_F32), snby = bricks_for(ny, 1, ST_F32),
+                   snbz = bricks_for(nz, 2, ST_F32);
+    const uint32_t nbx = bricks_for(nx, 0, storage), nby = bricks_for(ny, 1, storage),
+                   nbz = bricks_for(nz, 2, storage);
+    const size_t total = (size_t)nbx * nby * nbz;
+    float *d = static_cast<float *>(dst);
+    switch (storage) {
+        case ST_F32 | kAltFlag: hipLaunchKernelGGL((rebrick_f32_kernel<F32Alt>), dim3(grid_bricks(total)), dim3(256), 0, s, src_bricks, d, nx, ny, nz, snbx, snby, snbz, nbx, nby, total); break;
+        case ST_F32 | kPlainF32Flag: hipLaunchKernelGGL((rebrick_f32_kernel<F32P>), dim3(grid_bricks(total)), dim3(256), 0, s, src_bricks, d, nx, ny, nz, snbx, snby, snbz, nbx, nby, total); break;
+        case ST_F32 | kStencilF32Flag: hipLaunchKernelGGL((rebrick_f32_kernel<F32S>), dim3(grid_bricks(total)), dim3(256), 0, s, src_bricks, d, nx, ny, nz, snbx, snby, snbz, nbx, nby, total); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
