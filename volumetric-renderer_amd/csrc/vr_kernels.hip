@@ -1892,14 +1892,27 @@ __global__ __launch_bounds__(256) void grad_field_kernel(const float *__restrict
     // the brick's 24-B elements, assembled here and stored as consecutive 8-B words per lane
     __shared__ uint2 ostage[3 * G::Elems];
     uint2 *__restrict__ out = reinterpret_cast<uint2 *>(grad);
+    const uint32_t nbz = (uint32_t)(nbricks / ((size_t)nbx * nby));
     for (size_t bidx = blockIdx.x; bidx < nbricks; bidx += gridDim.x) {
         uint32_t bx, by, bz;
         brick_coords((uint32_t)bidx, nbx, nby, bx, by, bz);
         const int x0 = (int)(bx * G::BX) - 1, y0 = (int)(by * G::BY) - 1, z0 = (int)(bz * G::BZ) - 1;
         __syncthreads();  // the previous brick's elements have read the box and left ostage
-        for (int i = (int)threadIdx.x; i < LX * LY * LZ; i += (int)blockDim.x) {
-            const int ix = i % LX, iyz = i / LX, iy = iyz % LY, iz = iyz / LY;
-            box[i] = padded_voxel(bricks, x0 + ix, y0 + iy, z0 + iz, nx, ny, nz, nbx, nby);
+        // two z-slices per load: the z-pair element at (x, y, z) holds {v(z), v(z + 1)}, the
+        // border stored as 0 (padded_voxel where the element is outside the stored grid)
+        static_assert(LZ % 2 == 0, "the box is loaded in z-pairs");
+        for (int i = (int)threadIdx.x; i < LX * LY * (LZ / 2); i += (int)blockDim.x) {
+            const int ix = i % LX, iyz = i / LX, iy = iyz % LY, iz = 2 * (iyz / LY);
+            const int px = x0 + ix, py = y0 + iy, pz = z0 + iz;
+            float2 v;
+            if (kF32VoxelsPerElement == 2 && px >= 0 && py >= 0 && pz >= 0 &&
+                px < (int)(nbx * G::BX) && py < (int)(nby * G::BY) && pz < (int)(nbz * G::BZ))
+                v = reinterpret_cast<const float2 *>(bricks)[cell_offset<float>(px, py, pz, nbx, nby)];
+            else
+                v = make_float2(padded_voxel(bricks, px, py, pz, nx, ny, nz, nbx, nby),
+                                padded_voxel(bricks, px, py, pz + 1, nx, ny, nz, nbx, nby));
+            box[(iz * LY + iy) * LX + ix] = v.x;
+            box[((iz + 1) * LY + iy) * LX + ix] = v.y;
         }
         __syncthreads();
         for (uint32_t l = threadIdx.x; l < (uint32_t)G::Elems; l += blockDim.x) {
