@@ -293,7 +293,7 @@ int vr_release_external_memory(vr_ctx *ctx, vr_external_memory *mem);
  * bricks; binary16 unless vr_params.exact_gradient), a 7x15x8-brick copy for oblique f32 views,
  * a plain copy for unshaded sparse ones and a stencil copy for shaded sparse ones (sparse views
  * whose image rows follow the bricks' rows; DESIGN.md section 4.1 has the policy), and the
- * skip-empty classification.  Each is built on the first frame that wants it (0.6-2.3 ms for 512^3,
+ * skip-empty classification.  Each is built on the first frame that wants it (0.6-1.8 ms for 512^3,
  * inside that frame) unless vr_prepare built it first.
  * vr_set_memory_budget caps their total bytes on each device (the bricks never count): a
  * structure that would not fit is not built, and its frames read the bricks instead (the same
