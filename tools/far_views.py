@@ -48,6 +48,8 @@ def main():
         row["serial_ms"] = serial(p1)
         with rp.knobs(pair=1):
             row["serial_pair_ms"] = serial(p1)
+        with rp.knobs(pair=1, pair_lanes=4):
+            row["serial_pair4_ms"] = serial(p1)
         with rp.knobs(pair=0):
             row["serial_single_lane_ms"] = serial(p1)
 
